@@ -1,0 +1,283 @@
+// rs_kernels.hip -- CDNA4 (gfx950) Reed-Solomon coding kernels.
+//
+// One kernel family computes every RS operation the Dag Node needs:
+//   out_row[j][x] = XOR_c coef[j][c] * in_row[c][x]      (GF(2^8), poly 0x11D)
+// Encode (erasure.go:60, upstream Encode) uses the parity rows of the systematic matrix
+// over the k data rows; reconstruct (erasure.go:82/88, ReconstructData/Reconstruct) uses
+// the decode rows over the first k present rows.  Positions x are independent, so the
+// kernel is a pure HBM stream: read K rows, write MT rows, no reuse across workgroups.
+//
+// GF multiply without MFMA: a product a*x is linear in the bits of x, so it is the XOR
+// of three table lookups on bit fields of x (bits 0-2, 3-5, 6-7).  Each lookup is a
+// single v_perm_b32 that selects 4 bytes at once from an 8-byte pool of products, with
+// the field values as per-byte selectors.  Per input dword: 5 VALU ops build the three
+// selector words (shared by all MT outputs); per (output, input) dword: 3 v_perm_b32 and
+// 1.5 v_bitop3_b32 (3-input XOR).  Tables for the current column come from LDS by
+// broadcast ds_read_b128 (same address in every lane).
+//
+// Layout contract (fast path): row r of block b lives at base + b*bstride + r*rstride,
+// every base/stride 16-byte aligned, rstride >= roundup(S,16).  A wave owns a "tile" of
+// 64*D consecutive 16-byte chunks of one block; lanes past the block's last chunk clamp
+// their loads to a valid chunk and skip their stores, and the one partial chunk at the
+// end of a row is stored bytewise so no byte at or past S is ever written.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rs_plan.hpp"
+
+namespace rsmi {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t u4get(const u32x4& v, int i) { return v[i]; }
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row.
+template <int K, int MT, int D, bool NT>
+__global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
+                                                       const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                       uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
+                                                       uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
+                                                       uint32_t ntiles) {
+    __shared__ u32x4 s_tbl[K * kColDwords / 4];
+    {
+        const uint32_t* src = plan->tbl;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
+        for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    constexpr uint32_t kWavesPerWG = kWG / kWave;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t nw = gridDim.x * kWavesPerWG;
+    uint32_t t = blockIdx.x * kWavesPerWG + wid;
+    if (t >= ntiles) return;
+
+    constexpr int P = K < (D == 1 ? 6 : 3) ? K : (D == 1 ? 6 : 3);  // rows in flight per lane
+    uint64_t in_off[K], out_off[MT];
+#pragma unroll
+    for (int c = 0; c < K; c++) in_off[c] = uint64_t(plan->in_row[c]) * in_rs;
+#pragma unroll
+    for (int j = 0; j < MT; j++) out_off[j] = uint64_t(plan->out_row[j]) * out_rs;
+
+    // walk this wave's tiles t, t+nw, ... keeping (block, tile-in-block) incrementally
+    uint32_t blk = t / tpb;
+    uint32_t tib = t - blk * tpb;
+    const uint32_t step_b = nw / tpb, step_t = nw - step_b * tpb;
+
+    for (; t < ntiles; t += nw) {
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        const uint32_t ch0 = tib * (kWave * D) + lane;
+        uint32_t chl[D];  // load chunk, clamped: every lane's loads stay unconditional
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const uint32_t ch = ch0 + kWave * d;
+            chl[d] = ch < cpb ? ch : cpb - 1;
+        }
+        auto load_col = [&](int c, u32x4 (&dst)[D]) {
+#pragma unroll
+            for (int d = 0; d < D; d++) dst[d] = ld16<NT>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
+        };
+
+        // Software pipeline over the K input rows: a ring of P rows in flight, one
+        // scheduling region per row (sched_barrier) so the compiler cannot hoist every
+        // load and table read to the top and blow the 128-VGPR budget.
+        u32x4 v[P][D];
+#pragma unroll
+        for (int c = 0; c < P; c++) load_col(c, v[c]);
+
+        uint32_t acc[MT][4 * D];
+#pragma unroll
+        for (int j = 0; j < MT; j++)
+#pragma unroll
+            for (int w = 0; w < 4 * D; w++) acc[j][w] = 0;
+
+        // Opaque per-tile table base: stops LICM from hoisting all K*20 table words out
+        // of the tile loop (which would pin ~200 VGPRs and drop occupancy to 1 wave).
+        uint32_t tb = 0;
+        asm volatile("" : "+v"(tb));
+        const u32x4* tbl = s_tbl + tb;
+        u32x4 Tn[5];
+#pragma unroll
+        for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
+
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            const int slot = c % P;
+            u32x4 T[5];
+#pragma unroll
+            for (int f = 0; f < 5; f++) T[f] = Tn[f];
+#pragma unroll
+            for (int d = 0; d < D; d++)
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const uint32_t x = u4get(v[slot][d], w);
+                    const uint32_t s1 = x & 0x07070707u;
+                    const uint32_t s2 = (x >> 3) & 0x07070707u;
+                    const uint32_t s3 = (x >> 6) & 0x03030303u;
+#pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
+                        const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
+                        const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
+                        uint32_t& a = acc[j][d * 4 + w];
+                        a = xor3(a, p1, p2);
+                        a ^= p3;
+                    }
+                }
+            if (c + P < K) load_col(c + P, v[slot]);
+            if (c + 1 < K) {
+#pragma unroll
+                for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // Anchor the results outside the store predicate; otherwise the compiler sinks the
+        // whole column pipeline into the `ch < cpb` branch and hoists every table read.
+#pragma unroll
+        for (int j = 0; j < MT; j++)
+#pragma unroll
+            for (int w = 0; w < 4 * D; w++) asm volatile("" : "+v"(acc[j][w]));
+
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const uint32_t ch = ch0 + kWave * d;
+            if (ch < cpb) {
+                const uint32_t boff = ch * 16u;
+                if (boff + 16u <= S) {
+#pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
+                        if constexpr (NT)
+                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                        else
+                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                    }
+                } else {
+                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+#pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        uint8_t* p = ob + out_off[j] + boff;
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const uint32_t val = acc[j][d * 4 + w];
+                            const uint32_t o = boff + 4u * w;
+                            if (o + 4u <= S) {
+                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                            } else if (o < S) {
+                                p[4 * w] = uint8_t(val);
+                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+
+        blk += step_b;
+        tib += step_t;
+        if (tib >= tpb) {
+            tib -= tpb;
+            blk++;
+        }
+    }
+}
+
+// Any K (<= 256), MT <= 4, any alignment: one byte-group of 4 per lane, bytewise memory
+// access.  Correctness path for layouts the fast kernel does not accept.
+__global__ __launch_bounds__(kWG) void rs_generic_kernel(const RsPlanDev* __restrict__ plan, const uint8_t* in,
+                                                         uint8_t* out, uint64_t in_bs, uint64_t in_rs,
+                                                         uint64_t out_bs, uint64_t out_rs, uint64_t S,
+                                                         uint64_t nblocks) {
+    __shared__ u32x4 s_tbl[kMaxK * kColDwords / 4];
+    const int K = int(plan->k), MT = int(plan->mt);
+    {
+        const uint32_t* src = plan->tbl;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
+        for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint64_t groups = (S + 3) / 4;
+    for (uint64_t b = blockIdx.y; b < nblocks; b += gridDim.y) {
+        for (uint64_t g = uint64_t(blockIdx.x) * kWG + threadIdx.x; g < groups; g += uint64_t(gridDim.x) * kWG) {
+            const uint64_t x0 = g * 4;
+            const int nb = int(S - x0 < 4 ? S - x0 : 4);
+            uint32_t acc[4] = {0, 0, 0, 0};
+            for (int c = 0; c < K; c++) {
+                const uint8_t* p = in + b * in_bs + uint64_t(plan->in_row[c]) * in_rs + x0;
+                uint32_t x = 0;
+                for (int i = 0; i < nb; i++) x |= uint32_t(p[i]) << (8 * i);
+                const uint32_t s1 = x & 0x07070707u, s2 = (x >> 3) & 0x07070707u, s3 = (x >> 6) & 0x03030303u;
+                const u32x4 T0 = s_tbl[c * 5 + 0], T1 = s_tbl[c * 5 + 1], T2 = s_tbl[c * 5 + 2],
+                            T3 = s_tbl[c * 5 + 3], T4 = s_tbl[c * 5 + 4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    acc[j] ^= __builtin_amdgcn_perm(u4get(T1, j), u4get(T0, j), s1) ^
+                              __builtin_amdgcn_perm(u4get(T3, j), u4get(T2, j), s2) ^
+                              __builtin_amdgcn_perm(u4get(T4, j), u4get(T4, j), s3);
+                }
+            }
+            for (int j = 0; j < MT; j++) {
+                uint8_t* p = out + b * out_bs + uint64_t(plan->out_row[j]) * out_rs + x0;
+                for (int i = 0; i < nb; i++) p[i] = uint8_t(acc[j] >> (8 * i));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ dispatch table
+template <int K, int MT, int D, bool NT>
+static void* fast_ptr() {
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT>);
+}
+
+template <int K, int D, bool NT>
+static void fill_k(FastKernelTable& t) {
+    t.fn[K][1][D][NT] = fast_ptr<K, 1, D, NT>();
+    t.fn[K][2][D][NT] = fast_ptr<K, 2, D, NT>();
+    t.fn[K][3][D][NT] = fast_ptr<K, 3, D, NT>();
+    t.fn[K][4][D][NT] = fast_ptr<K, 4, D, NT>();
+}
+
+template <int D, bool NT>
+static void fill_d(FastKernelTable& t) {
+    fill_k<1, D, NT>(t);
+    fill_k<2, D, NT>(t);
+    fill_k<3, D, NT>(t);
+    fill_k<4, D, NT>(t);
+    fill_k<5, D, NT>(t);
+    fill_k<6, D, NT>(t);
+    fill_k<8, D, NT>(t);
+    fill_k<10, D, NT>(t);
+    fill_k<12, D, NT>(t);
+    fill_k<16, D, NT>(t);
+}
+
+const FastKernelTable& fast_kernels() {
+    static const FastKernelTable t = [] {
+        FastKernelTable x{};
+        fill_d<1, false>(x);
+        fill_d<2, false>(x);
+        fill_d<1, true>(x);
+        fill_d<2, true>(x);
+        return x;
+    }();
+    return t;
+}
+
+void* generic_kernel() { return reinterpret_cast<void*>(&rs_generic_kernel); }
+
+}  // namespace rsmi

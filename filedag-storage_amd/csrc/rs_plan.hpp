@@ -1,0 +1,32 @@
+// rs_plan.hpp -- device-side coding plan shared by the host launcher and the kernels.
+#pragma once
+#include <cstdint>
+
+namespace rsmi {
+
+constexpr int kWave = 64;       // CDNA wavefront
+constexpr int kWG = 256;        // threads per workgroup (4 waves)
+constexpr int kMaxK = 256;      // k + m <= 256 (erasure.go:22)
+constexpr int kMaxMT = 4;       // outputs per launch tile
+constexpr int kColDwords = 20;  // per input column: 5 table fields x 4 outputs
+constexpr int kMinWavesPerSimd = 4;  // caps the fast kernels at 128 VGPRs (16 waves/CU)
+
+// One launch tile: MT (<= 4) output rows computed from K input rows.
+// tbl[c*20 + f*4 + j] = field-f product word for coefficient coef[j][c] (gf256.hpp
+// perm_tables); padded outputs (j >= MT) have all-zero tables.
+struct RsPlanDev {
+    uint32_t k, mt, pad0[14];
+    uint32_t in_row[kMaxK];
+    uint32_t out_row[kMaxMT], pad1[12];
+    uint32_t tbl[kMaxK * kColDwords];
+};
+
+// Instantiated fast kernels: fn[K][MT][D][NT] (null when K has no instantiation).
+struct FastKernelTable {
+    void* fn[17][kMaxMT + 1][3][2];
+};
+
+const FastKernelTable& fast_kernels();
+void* generic_kernel();
+
+}  // namespace rsmi

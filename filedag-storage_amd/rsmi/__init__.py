@@ -1,0 +1,280 @@
+"""Python host mirror of filedag-storage's Dag Node erasure seam over librsmi.so.
+
+`Erasure` mirrors dag/node/dagnode/erasure.go method for method (NewErasure,
+EncodeData, DecodeDataBlocks, DecodeDataAndParityBlocks, ShardSize) with the same
+argument meaning and error behaviour; every byte it produces comes out of the gfx950
+HIP kernels behind the C-ABI in include/rsmi.h.  There is no CPU fallback: if the
+library or a GPU is missing the calls raise.
+
+`Codec` exposes the batched device-resident and host entry points used by bench.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
+
+# status codes (include/rsmi.h) -- names follow the upstream sentinels
+OK = 0
+ErrShortData = 1
+ErrTooFewShards = 2
+ErrShardNoData = 3
+ErrShardSize = 4
+ErrInvShardNum = 5
+ErrMaxShardNum = 6
+ErrSingular = 7
+ErrInvalidArg = 8
+ErrDevice = 100
+ErrNoDevice = 101
+
+
+class RsmiError(Exception):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"rsmi error {code}: {msg or status_string(code)}")
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librsmi.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"librsmi.so not built at {LIB_PATH}: run `python __graft_entry__.py build`")
+    L = ctypes.CDLL(LIB_PATH)
+    c_size = ctypes.c_size_t
+    u8p = ctypes.c_void_p
+    sig = {
+        "rsmi_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+        "rsmi_close": (None, [ctypes.c_void_p]),
+        "rsmi_device_count": (ctypes.c_int, []),
+        "rsmi_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+        "rsmi_abi_version": (ctypes.c_int, []),
+        "rsmi_shard_size": (c_size, [c_size, ctypes.c_int]),
+        "rsmi_encode_matrix": (ctypes.c_int, [ctypes.c_void_p, u8p]),
+        "rsmi_check_shards": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_size), ctypes.c_int, ctypes.POINTER(c_size)]),
+        "rsmi_decode_matrix": (ctypes.c_int, [ctypes.c_void_p, u8p, u8p, ctypes.POINTER(ctypes.c_int)]),
+        "rsmi_encode_block": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p]),
+        "rsmi_encode": (ctypes.c_int, [ctypes.c_void_p, u8p, u8p, c_size]),
+        "rsmi_reconstruct": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_int]),
+        "rsmi_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
+        "rsmi_reconstruct_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p, ctypes.c_int]),
+        "rsmi_host_alloc": (ctypes.c_void_p, [c_size]),
+        "rsmi_host_free": (None, [ctypes.c_void_p]),
+        "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
+        "rsmi_reconstruct_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, ctypes.c_int, ctypes.c_void_p]),
+        "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
+        "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def status_string(code: int) -> str:
+    try:
+        return lib().rsmi_status_string(code).decode()
+    except Exception:  # pragma: no cover - only when the library is absent
+        return "unknown"
+
+
+def _check(rc: int) -> None:
+    if rc != OK:
+        raise RsmiError(rc)
+
+
+def ceil_frac(numerator: int, denominator: int) -> int:
+    """utils.go:6-21 ceilFrac."""
+    if denominator == 0:
+        return 0
+    if denominator < 0:
+        numerator, denominator = -numerator, -denominator
+    q = abs(numerator) // denominator * (1 if numerator >= 0 else -1)
+    if numerator > 0 and numerator % denominator != 0:
+        q += 1
+    return q
+
+
+def _buf(b) -> ctypes.Array:
+    return (ctypes.c_uint8 * len(b)).from_buffer(b)
+
+
+class Codec:
+    """One RS(k, m) context on one device (rsmi_open)."""
+
+    def __init__(self, k: int, m: int, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().rsmi_open(k, m, device, ctypes.byref(h)))
+        self.k, self.m, self.n, self.device = k, m, k + m, device
+        self._h = h
+
+    def close(self) -> None:
+        if self._h:
+            lib().rsmi_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- host-only helpers
+    def encode_matrix(self) -> bytes:
+        out = bytearray(self.n * self.k)
+        _check(lib().rsmi_encode_matrix(self._h, ctypes.addressof(_buf(out))))
+        return bytes(out)
+
+    def decode_matrix(self, present: Sequence[bool]):
+        p = bytearray(1 if x else 0 for x in present)
+        out = bytearray(self.k * self.k)
+        used = (ctypes.c_int * self.k)()
+        _check(lib().rsmi_decode_matrix(self._h, ctypes.addressof(_buf(p)), ctypes.addressof(_buf(out)), used))
+        return bytes(out), list(used)
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(lib().rsmi_set_option(self._h, key.encode(), int(value)))
+
+    def last_kernel(self) -> str:
+        return lib().rsmi_last_kernel(self._h).decode()
+
+    # -- host memory
+    def encode_block(self, block: bytes) -> bytes:
+        S = lib().rsmi_shard_size(len(block), self.k)
+        out = bytearray(self.n * S)
+        src = bytearray(block)
+        _check(lib().rsmi_encode_block(self._h, ctypes.addressof(_buf(src)) if src else None, len(block),
+                                       ctypes.addressof(_buf(out)) if out else None))
+        return bytes(out)
+
+    def encode(self, data: bytearray, parity: bytearray, S: int) -> None:
+        _check(lib().rsmi_encode(self._h, ctypes.addressof(_buf(data)), ctypes.addressof(_buf(parity)), S))
+
+    def reconstruct(self, shards: bytearray, S: int, present: Sequence[bool], data_only: bool) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_reconstruct(self._h, ctypes.addressof(_buf(shards)), S, ctypes.addressof(_buf(p)),
+                                      1 if data_only else 0))
+
+    def encode_batch_host_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
+                              nblocks: int) -> None:
+        _check(lib().rsmi_encode_batch_host(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks))
+
+    def reconstruct_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
+                                   data_only: bool) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_reconstruct_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                 1 if data_only else 0))
+
+    # -- device memory (raw pointers, e.g. torch tensor.data_ptr()); stream = hipStream_t
+    def encode_batch_dev(self, d_data: int, data_rs: int, data_bs: int, d_parity: int, parity_rs: int,
+                         parity_bs: int, S: int, nblocks: int, stream: int = 0) -> None:
+        _check(lib().rsmi_encode_batch_dev(self._h, d_data, data_rs, data_bs, d_parity, parity_rs, parity_bs, S,
+                                           nblocks, stream or None))
+
+    def reconstruct_batch_dev(self, d_shards: int, rs: int, bs: int, S: int, nblocks: int,
+                              present: Sequence[bool], data_only: bool, stream: int = 0) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_reconstruct_batch_dev(self._h, d_shards, rs, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                1 if data_only else 0, stream or None))
+
+
+def check_shards(lens: Sequence[int], nil_ok: bool):
+    arr = (ctypes.c_size_t * len(lens))(*lens)
+    S = ctypes.c_size_t()
+    rc = lib().rsmi_check_shards(len(lens), arr, 1 if nil_ok else 0, ctypes.byref(S))
+    return rc, S.value
+
+
+class Erasure:
+    """dag/node/dagnode/erasure.go:9-13 Erasure{encoder, dataBlocks, parityBlocks, blockSize}."""
+
+    def __init__(self, data_blocks: int, parity_blocks: int, block_size: int, device: int = 0):
+        # erasure.go:18-24
+        if data_blocks <= 0 or parity_blocks <= 0:
+            raise RsmiError(ErrInvShardNum)
+        if data_blocks + parity_blocks > 256:
+            raise RsmiError(ErrMaxShardNum)
+        self.data_blocks = data_blocks
+        self.parity_blocks = parity_blocks
+        self.block_size = block_size
+        self._device = device
+        self._codec: Optional[Codec] = None
+
+    def encoder(self) -> Codec:
+        """erasure.go:31-45: the codec is built lazily, once."""
+        if self._codec is None:
+            self._codec = Codec(self.data_blocks, self.parity_blocks, self._device)
+        return self._codec
+
+    def shard_size(self) -> int:
+        """erasure.go:96-98"""
+        return ceil_frac(self.block_size, self.data_blocks)
+
+    def encode_data(self, data: bytes) -> List[Optional[bytes]]:
+        """erasure.go:51-65 EncodeData: Split + Encode."""
+        n = self.data_blocks + self.parity_blocks
+        if len(data) == 0:
+            return [None] * n
+        flat = self.encoder().encode_block(data)
+        S = len(flat) // n
+        return [flat[i * S:(i + 1) * S] for i in range(n)]
+
+    def _reconstruct(self, shards: List[Optional[bytes]], data_only: bool) -> None:
+        n = self.data_blocks + self.parity_blocks
+        if len(shards) != n:
+            raise RsmiError(ErrTooFewShards)  # upstream: len(shards) != totalShards
+        lens = [len(s) if s else 0 for s in shards]
+        rc, S = check_shards(lens, nil_ok=True)
+        _check(rc)
+        present = [bool(x) for x in lens]
+        np_ = sum(present)
+        dp = sum(present[: self.data_blocks])
+        if np_ == n or (data_only and dp == self.data_blocks):
+            return
+        flat = bytearray(n * S)
+        for i, s in enumerate(shards):
+            if s:
+                flat[i * S:(i + 1) * S] = s
+        self.encoder().reconstruct(flat, S, present, data_only)
+        for i in range(n):
+            if not present[i] and (i < self.data_blocks or not data_only):
+                shards[i] = bytes(flat[i * S:(i + 1) * S])
+
+    def decode_data_blocks(self, data: List[Optional[bytes]]) -> None:
+        """erasure.go:70-83 DecodeDataBlocks (the isZero loop breaks after the first empty
+        shard, so only 'nothing missing' short-circuits; then ReconstructData)."""
+        is_zero = 0
+        for b in data:
+            if not b:
+                is_zero += 1
+                break
+        if is_zero == 0 or is_zero == len(data):
+            return
+        self._reconstruct(data, data_only=True)
+
+    def decode_data_and_parity_blocks(self, data: List[Optional[bytes]]) -> None:
+        """erasure.go:87-93 DecodeDataAndParityBlocks -> Reconstruct."""
+        self._reconstruct(data, data_only=False)
+
+
+def NewErasure(data_blocks: int, parity_blocks: int, block_size: int, device: int = 0) -> Erasure:
+    return Erasure(data_blocks, parity_blocks, block_size, device)
+
+
+def device_count() -> int:
+    return lib().rsmi_device_count()

@@ -1,0 +1,137 @@
+/*
+ * rsmi.h -- C-ABI of the MI355X Reed-Solomon engine (librsmi.so).
+ *
+ * This is the drop-in seam under filedag-storage's Dag Node: every entry point replaces
+ * one call that dag/node/dagnode makes into github.com/klauspost/reedsolomon v1.11.0
+ * (go.mod:31).  Plain pointers and sizes only -- no Go, torch or HIP types -- so a cgo
+ * file binds it directly.  All functions are thread-safe; one context
+ * may be shared by every goroutine of a DagNode (node.go:358 Put, :220 Get, the repair
+ * worker at :159 and data_recovery.go:16 RepairDataNode all run concurrently).
+ *
+ * Buffer ownership: the caller owns every buffer; the library never retains a caller
+ * pointer after a call returns (cgo pointer rules).  The *_dev entry points take device
+ * pointers and a hipStream_t passed as void*; they are stream-ordered and do not sync.
+ *
+ * Status codes map 1:1 onto the upstream sentinels (erasure.go:19,23 return two of them
+ * directly; the rest surface through Split/Encode/Reconstruct at erasure.go:55,60,82,88).
+ * There is no CPU fallback: a device failure is RSMI_ERR_DEVICE / RSMI_ERR_NO_DEVICE.
+ */
+#ifndef RSMI_H
+#define RSMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSMI_ABI_VERSION 1
+
+typedef struct rsmi_ctx rsmi_ctx;
+
+enum rsmi_status {
+    RSMI_OK = 0,
+    RSMI_ERR_SHORT_DATA = 1,     /* reedsolomon.ErrShortData    (Split of 0 bytes)          */
+    RSMI_ERR_TOO_FEW_SHARDS = 2, /* reedsolomon.ErrTooFewShards (< k shards present)        */
+    RSMI_ERR_SHARD_NO_DATA = 3,  /* reedsolomon.ErrShardNoData  (every shard empty)         */
+    RSMI_ERR_SHARD_SIZE = 4,     /* reedsolomon.ErrShardSize    (unequal non-empty shards)  */
+    RSMI_ERR_INV_SHARD_NUM = 5,  /* reedsolomon.ErrInvShardNum  (k<=0 || m<=0), erasure.go:19 */
+    RSMI_ERR_MAX_SHARD_NUM = 6,  /* reedsolomon.ErrMaxShardNum  (k+m>256),     erasure.go:23 */
+    RSMI_ERR_SINGULAR = 7,       /* matrix not invertible (cannot happen for valid patterns) */
+    RSMI_ERR_INVALID_ARG = 8,    /* NULL pointer, stride smaller than a shard, ...          */
+    RSMI_ERR_DEVICE = 100,       /* a HIP call failed                                       */
+    RSMI_ERR_NO_DEVICE = 101     /* no usable gfx950 device / kernels not loadable          */
+};
+
+/* ------------------------------------------------------------------ lifecycle */
+
+/* Replaces reedsolomon.New(k, m, WithAutoGoroutines(S)) inside NewErasure
+ * (dag/node/dagnode/erasure.go:16-47).  Validates like erasure.go:18-24, builds and caches
+ * the n x k systematic matrix.  Device resources are created lazily on first compute call,
+ * so opening a context works (and reports argument errors) on a host without a GPU. */
+int rsmi_open(int k, int m, int device, rsmi_ctx** out);
+void rsmi_close(rsmi_ctx* ctx);
+
+int rsmi_device_count(void);
+const char* rsmi_status_string(int status);
+int rsmi_abi_version(void);
+
+/* ------------------------------------------------------------------ host-only helpers */
+
+/* Erasure.ShardSize (erasure.go:96-98) = ceilFrac(B, k) (utils.go:6-21). */
+size_t rsmi_shard_size(size_t block_size, int k);
+
+/* The cached (k+m) x k encode matrix, row-major. */
+int rsmi_encode_matrix(const rsmi_ctx* ctx, uint8_t* out);
+
+/* Upstream checkShards/shardSize: lens[i]==0 marks shard i missing.  nil_ok=0 is the
+ * Encode check, nil_ok=1 the Reconstruct check.  *S_out receives the common size. */
+int rsmi_check_shards(int n, const size_t* lens, int nil_ok, size_t* S_out);
+
+/* The k x k data-decode matrix the reconstruct path uses for this erasure pattern
+ * (inverse of the rows of the first k present shards, upstream reconstruct()); the k
+ * survivor indices are written to used_rows.  present: n flags. */
+int rsmi_decode_matrix(const rsmi_ctx* ctx, const uint8_t* present, uint8_t* out, int* used_rows);
+
+/* ------------------------------------------------------------------ one block, host memory */
+
+/* Erasure.EncodeData (erasure.go:51-65): Split + Encode of one raw block of B bytes into
+ * (k+m)*S contiguous bytes, S = rsmi_shard_size(B, k); data rows zero-padded like Split.
+ * B == 0 -> RSMI_ERR_SHORT_DATA (the Go wrapper short-circuits it before calling). */
+int rsmi_encode_block(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out);
+
+/* Encoder.Encode on pre-split shards: data = k*S contiguous, parity = m*S contiguous. */
+int rsmi_encode(rsmi_ctx* ctx, const uint8_t* data, uint8_t* parity, size_t S);
+
+/* Encoder.ReconstructData (data_only=1, erasure.go:82) / Encoder.Reconstruct (data_only=0,
+ * erasure.go:88) on n*S contiguous bytes.  present: n flags; missing rows are overwritten,
+ * present rows are only read.  Nothing missing -> RSMI_OK without touching the device. */
+int rsmi_reconstruct(rsmi_ctx* ctx, uint8_t* shards, size_t S, const uint8_t* present, int data_only);
+
+/* ------------------------------------------------------------------ batches, host memory */
+
+/* nblocks independent blocks: data block b at data + b*data_block_stride (k rows of S
+ * bytes), parity block b at parity + b*parity_block_stride (m rows of S bytes).
+ * Copies are overlapped with compute over several HIP streams; pass memory from
+ * rsmi_host_alloc for full PCIe rate. */
+int rsmi_encode_batch_host(rsmi_ctx* ctx, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                           size_t parity_block_stride, size_t S, size_t nblocks);
+
+/* One erasure pattern for every block (RepairDataNode shape, data_recovery.go:16-112):
+ * block b at shards + b*block_stride holds n rows of S bytes. */
+int rsmi_reconstruct_batch_host(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                const uint8_t* present, int data_only);
+
+void* rsmi_host_alloc(size_t bytes);
+void rsmi_host_free(void* p);
+
+/* ------------------------------------------------------------------ batches, device memory */
+
+/* Device-resident encode.  Row c of data block b is at
+ *   d_data + b*data_block_stride + c*data_shard_stride
+ * and parity row j at d_parity + b*parity_block_stride + j*parity_shard_stride.
+ * Fast path: every base/stride a multiple of 16 and each shard stride >= S rounded up to
+ * 16 (the rows' padding bytes may be read, are never written).  Any other layout runs a
+ * byte-granular kernel.  stream: hipStream_t (NULL = default stream). */
+int rsmi_encode_batch_dev(rsmi_ctx* ctx, const uint8_t* d_data, size_t data_shard_stride,
+                          size_t data_block_stride, uint8_t* d_parity, size_t parity_shard_stride,
+                          size_t parity_block_stride, size_t S, size_t nblocks, void* stream);
+
+/* Device-resident in-place reconstruct, one erasure pattern for all blocks.  Row i of
+ * block b at d_shards + b*block_stride + i*shard_stride. */
+int rsmi_reconstruct_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t shard_stride, size_t block_stride,
+                               size_t S, size_t nblocks, const uint8_t* present, int data_only, void* stream);
+
+/* ------------------------------------------------------------------ tuning / introspection */
+
+/* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (0|1),
+ * "waves_per_cu" (grid cap).  Returns RSMI_ERR_INVALID_ARG for unknown keys. */
+int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
+/* Name of the kernel the last device launch on this context used ("" if none). */
+const char* rsmi_last_kernel(const rsmi_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSMI_H */

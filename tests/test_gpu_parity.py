@@ -1,0 +1,264 @@
+"""HIP path vs the CPU oracle, bit-exact (GPU tests; call through the C-ABI).
+
+Sizes follow SURVEY.md 8(d) / Appendix B.3: every (k, m) in BASELINE.json's configs plus
+a few others, block sizes {1, k-1, k, k+1, 6, 262143, 262144, 262145, ~1 MiB leaf}, and
+the loss patterns {each single shard, first two data, last two parity, data+parity}.
+Full-size configs are checked through size-independent properties (encode -> erase ->
+reconstruct round trips) plus oracle spot checks.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+torch = pytest.importorskip("torch")
+rsmi = pytest.importorskip("rsmi")
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [(2, 1), (4, 2), (10, 4), (16, 4), (5, 5), (3, 2), (6, 3), (8, 4), (12, 4), (1, 1), (20, 4), (17, 3)]
+
+
+def _rng_bytes(seed, n):
+    return orc.splitmix64_bytes(0xF11EDA6 ^ seed, n)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available() or rsmi.device_count() == 0:
+        pytest.skip("no GPU")
+
+
+def test_encode_matrix_matches_oracle():
+    for k, m in CONFIGS:
+        with rsmi.Codec(k, m) as c:
+            got = np.frombuffer(c.encode_matrix(), dtype=np.uint8).reshape(k + m, k)
+            assert np.array_equal(got, orc.build_matrix(k, m)), (k, m)
+
+
+@pytest.mark.parametrize("k,m", CONFIGS)
+def test_encode_block_grid(k, m):
+    sizes = sorted({1, max(1, k - 1), k, k + 1, 6, 4095, 65537, 262143, 262144, 262145})
+    with rsmi.Codec(k, m) as c:
+        for B in sizes:
+            block = _rng_bytes(B, B).tobytes()
+            got = np.frombuffer(c.encode_block(block), dtype=np.uint8).reshape(k + m, -1)
+            want = orc.split(k, m, block)
+            want[k:] = orc.encode(k, m, want[:k])
+            assert np.array_equal(got, want), (k, m, B, c.last_kernel())
+
+
+def test_reference_fixture_123456():
+    """node_test.go:33 RS(2,1) "123456": shards "123", "456", parity 3b 3c 39."""
+    e = rsmi.NewErasure(2, 1, 6)
+    shards = e.encode_data(b"123456")
+    assert shards == [b"123", b"456", bytes([0x3B, 0x3C, 0x39])]
+    # TestDagNode: Get after losing any one shard returns the block
+    for lost in range(3):
+        sh = list(shards)
+        sh[lost] = None
+        e.decode_data_blocks(sh)
+        assert b"".join(sh[:2])[:6] == b"123456"
+
+
+def test_kat_one_encode_5_5():
+    """upstream TestOneEncode: RS(5,5) with 2-byte shards."""
+    with rsmi.Codec(5, 5) as c:
+        data = bytearray([0, 1, 4, 5, 2, 3, 6, 7, 8, 9])
+        par = bytearray(10)
+        c.encode(data, par, 2)
+        assert list(par) == [12, 13, 10, 11, 14, 15, 90, 91, 94, 95]
+
+
+def _patterns(k, m):
+    n = k + m
+    pats = [[i] for i in range(n)]
+    pats.append([0, 1] if k >= 2 else [0])
+    pats.append([n - 2, n - 1] if m >= 2 else [n - 1])
+    pats.append([0, n - 1])
+    if m >= 2:
+        pats.append(list(range(k - 1, k - 1 + m)))  # m losses spanning data and parity
+    return [p for p in pats if len(p) <= m]
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (4, 2), (10, 4), (16, 4), (5, 5), (6, 3), (20, 4)])
+@pytest.mark.parametrize("S", [1, 7, 4099, 26215])
+def test_reconstruct_patterns(k, m, S):
+    n = k + m
+    data = _rng_bytes(k * 1000 + S, k * S).reshape(k, S)
+    full = np.zeros((n, S), dtype=np.uint8)
+    full[:k] = data
+    full[k:] = orc.encode(k, m, data)
+    with rsmi.Codec(k, m) as c:
+        for lost in _patterns(k, m):
+            present = [i not in lost for i in range(n)]
+            for data_only in (True, False):
+                buf = full.copy()
+                buf[lost] = 0xA5  # garbage in the missing rows
+                flat = bytearray(buf.tobytes())
+                c.reconstruct(flat, S, present, data_only)
+                got = np.frombuffer(bytes(flat), dtype=np.uint8).reshape(n, S)
+                rc, want = orc.reconstruct(k, m, buf, present, data_only)
+                assert rc == 0
+                assert np.array_equal(got, want), (k, m, S, lost, data_only)
+                if not data_only:
+                    assert np.array_equal(got, full)
+                else:
+                    assert np.array_equal(got[:k], full[:k])
+
+
+def test_reconstruct_errors():
+    with rsmi.Codec(4, 2) as c:
+        S = 16
+        flat = bytearray(6 * S)
+        with pytest.raises(rsmi.RsmiError) as ei:
+            c.reconstruct(flat, S, [True, True, True, False, False, False], False)
+        assert ei.value.code == rsmi.ErrTooFewShards
+        # nothing missing: no-op
+        c.reconstruct(flat, S, [True] * 6, False)
+        # data_only with all data present: no-op even if parity is missing
+        c.reconstruct(flat, S, [True] * 4 + [False, False], True)
+
+
+def _dev_layout(k, m, S, nblocks, pad):
+    rs = (S + pad - 1) // pad * pad
+    return rs, k * rs, m * rs
+
+
+@pytest.mark.parametrize("k,m,S,nblocks", [(4, 2, 65536, 64), (10, 4, 26215, 96), (16, 4, 4097, 33),
+                                           (2, 1, 131072, 8), (10, 4, 104858, 9), (3, 2, 17, 129)])
+@pytest.mark.parametrize("opts", [{}, {"chunks_per_lane": 2}, {"nontemporal": 1},
+                                  {"chunks_per_lane": 2, "nontemporal": 1}])
+def test_encode_batch_dev_vs_oracle(k, m, S, nblocks, opts):
+    rs, dbs, pbs = _dev_layout(k, m, S, nblocks, 256)
+    host = np.zeros((nblocks, k, rs), dtype=np.uint8)
+    for b in range(nblocks):
+        host[b, :, :S] = _rng_bytes(b, k * S).reshape(k, S)
+    d_in = torch.from_numpy(host.reshape(-1)).cuda()
+    d_out = torch.full((nblocks * pbs,), 0x5A, dtype=torch.uint8, device="cuda")
+    with rsmi.Codec(k, m) as c:
+        for key, val in opts.items():
+            c.set_option(key, val)
+        c.encode_batch_dev(d_in.data_ptr(), rs, dbs, d_out.data_ptr(), rs, pbs, S, nblocks,
+                           torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert "rs_fast_kernel" in c.last_kernel()
+    got = d_out.cpu().numpy().reshape(nblocks, m, rs)
+    want = orc.encode_fast(k, m, np.ascontiguousarray(host[:, :, :S]))
+    assert np.array_equal(got[:, :, :S], want)
+    # bytes at and past S in every parity row are never written
+    assert (got[:, :, S:] == 0x5A).all()
+
+
+@pytest.mark.parametrize("k,m,S,nblocks", [(10, 4, 26215, 5), (4, 2, 1001, 7), (20, 4, 333, 3)])
+def test_encode_batch_dev_unaligned_generic(k, m, S, nblocks):
+    """Contiguous k*S layout with odd S (the Split layout itself): byte-granular kernel."""
+    host = _rng_bytes(77, nblocks * k * S).reshape(nblocks, k, S)
+    d_in = torch.from_numpy(host.reshape(-1).copy()).cuda()
+    d_out = torch.zeros(nblocks * m * S, dtype=torch.uint8, device="cuda")
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_dev(d_in.data_ptr(), S, k * S, d_out.data_ptr(), S, m * S, S, nblocks, 0)
+        torch.cuda.synchronize()
+        assert "generic" in c.last_kernel()
+    got = d_out.cpu().numpy().reshape(nblocks, m, S)
+    assert np.array_equal(got, orc.encode_fast(k, m, host))
+
+
+@pytest.mark.parametrize("k,m,S,nblocks,lost,data_only",
+                         [(10, 4, 26215, 64, [0], True), (16, 4, 262144 // 16, 8, [0, 9], False),
+                          (4, 2, 65536, 16, [1, 4], False), (10, 4, 26215, 16, [3, 11, 12, 13], False),
+                          (2, 1, 131072, 4, [1], False)])
+def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only):
+    n = k + m
+    rs = (S + 255) // 256 * 256
+    full = np.zeros((nblocks, n, rs), dtype=np.uint8)
+    for b in range(nblocks):
+        d = _rng_bytes(b + 5, k * S).reshape(k, S)
+        full[b, :k, :S] = d
+    full[:, k:, :S] = orc.encode_fast(k, m, np.ascontiguousarray(full[:, :k, :S]))
+    erased = full.copy()
+    erased[:, lost, :] = 0
+    d = torch.from_numpy(erased.reshape(-1).copy()).cuda()
+    present = [i not in lost for i in range(n)]
+    with rsmi.Codec(k, m) as c:
+        c.reconstruct_batch_dev(d.data_ptr(), rs, n * rs, S, nblocks, present, data_only,
+                                torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    got = d.cpu().numpy().reshape(nblocks, n, rs)
+    rows = [i for i in lost if i < k or not data_only]
+    assert np.array_equal(got[:, rows, :S], full[:, rows, :S])
+    untouched = [i for i in lost if i not in rows]
+    assert (got[:, untouched, :] == 0).all()
+
+
+def test_batch_host_matches_dev():
+    k, m, S, nb = 10, 4, 26215, 300
+    data = _rng_bytes(9, nb * k * S).reshape(nb, k, S)
+    par = np.zeros((nb, m, S), dtype=np.uint8)
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_host_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb)
+        assert np.array_equal(par, orc.encode_fast(k, m, data))
+        full = np.concatenate([data, par], axis=1).copy()
+        sh = full.copy()
+        sh[:, [0, 12]] = 0
+        present = [i not in (0, 12) for i in range(k + m)]
+        c.reconstruct_batch_host_ptr(sh.ctypes.data, (k + m) * S, S, nb, present, False)
+        assert np.array_equal(sh, full)
+
+
+def test_full_size_roundtrip_rs10_4():
+    """BASELINE config 3 at full size: 4096 x 256 KiB, encode, lose data shard 0,
+    ReconstructData, compare with the original bytes; oracle spot check on 8 blocks."""
+    k, m, nb = 10, 4, 4096
+    B = 256 * 1024
+    S = (B + k - 1) // k
+    rs = (S + 255) // 256 * 256
+    n = k + m
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    shards = torch.randint(0, 256, (nb, n, rs), dtype=torch.uint8, device="cuda", generator=g)
+    shards[:, :, S:] = 0
+    # block tail padding (k*S - B = 6 bytes of the last data row) is zero like Split
+    shards[:, k - 1, S - (k * S - B):S] = 0
+    with rsmi.Codec(k, m) as c:
+        stream = torch.cuda.current_stream().cuda_stream
+        base = shards.data_ptr()
+        c.encode_batch_dev(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, stream)
+        torch.cuda.synchronize()
+        orig = shards.clone()
+        shards[:, 0, :] = 0
+        c.reconstruct_batch_dev(base, rs, n * rs, S, nb, [i != 0 for i in range(n)], True, stream)
+        torch.cuda.synchronize()
+    assert torch.equal(shards, orig)
+    idx = [0, 1, 777, 2048, 4095, 3, 1000, 4000]
+    host = orig[idx].cpu().numpy()
+    want = orc.encode_fast(k, m, np.ascontiguousarray(host[:, :k, :S]))
+    assert np.array_equal(host[:, k:, :S], want)
+
+
+def test_concurrent_contexts_threads():
+    """One context shared by several threads (DagNode goroutines share one Erasure)."""
+    import threading
+
+    k, m = 10, 4
+    errs = []
+    with rsmi.Codec(k, m) as c:
+        def worker(seed):
+            try:
+                for it in range(5):
+                    blk = _rng_bytes(seed * 100 + it, 5000 + seed).tobytes()
+                    got = np.frombuffer(c.encode_block(blk), dtype=np.uint8).reshape(k + m, -1)
+                    want = orc.split(k, m, blk)
+                    want[k:] = orc.encode(k, m, want[:k])
+                    assert np.array_equal(got, want)
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errs, errs
