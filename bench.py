@@ -139,7 +139,7 @@ def main():
     k, m, n = a.k, a.m, a.k + a.m
     B = a.block_kib * 1024
     S = (B + k - 1) // k
-    rs = (S + 255) // 256 * 256  # 256-B row pitch in HBM
+    rs = rsmi.recommended_pitch(S)  # power-of-two shard slots in HBM (DESIGN.md "Layout")
     bs = n * rs
     nb = a.blocks
     lost = [int(x) for x in a.lost.split(",") if x != ""]

@@ -42,8 +42,18 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
     else return *p;
 }
 
-// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row.
-template <int K, int MT, int D, bool NT>
+// Default rows in flight per lane for the software pipeline.
+// Narrow outputs (MT <= 2) keep every input row in flight (registers are cheap there,
+// measured +2.6% on RS(10,4) 1-row reconstruct); wide outputs keep a ring of 6 (D=1) or 3.
+template <int K, int MT, int D>
+constexpr int default_prefetch() {
+    constexpr int cap = MT <= 2 ? 16 : (D == 1 ? 6 : 3);
+    return K < cap ? K : cap;
+}
+
+// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row, NT nontemporal memory
+// ops, PF rows in flight per lane (0 = default_prefetch).
+template <int K, int MT, int D, bool NT, int PF = 0, bool PAIR = true>
 __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -64,7 +74,7 @@ __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const Rs
     uint32_t t = blockIdx.x * kWavesPerWG + wid;
     if (t >= ntiles) return;
 
-    constexpr int P = K < (D == 1 ? 6 : 3) ? K : (D == 1 ? 6 : 3);  // rows in flight per lane
+    constexpr int P = PF == 0 ? default_prefetch<K, MT, D>() : (PF < K ? PF : K);  // rows in flight per lane
     uint64_t in_off[K], out_off[MT];
 #pragma unroll
     for (int c = 0; c < K; c++) in_off[c] = uint64_t(plan->in_row[c]) * in_rs;
@@ -98,11 +108,9 @@ __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const Rs
 #pragma unroll
         for (int c = 0; c < P; c++) load_col(c, v[c]);
 
-        uint32_t acc[MT][4 * D];
-#pragma unroll
-        for (int j = 0; j < MT; j++)
-#pragma unroll
-            for (int w = 0; w < 4 * D; w++) acc[j][w] = 0;
+        // acc ^= p1^p2^p3 per column, folded two columns at a time with 3-input XORs:
+        // even columns leave p3 pending, odd columns retire it (1.5 VALU per column).
+        uint32_t acc[MT][4 * D], pend[MT][4 * D];
 
         // Opaque per-tile table base: stops LICM from hoisting all K*20 table words out
         // of the tile loop (which would pin ~200 VGPRs and drop occupancy to 1 wave).
@@ -133,8 +141,24 @@ __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const Rs
                         const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
                         const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
                         uint32_t& a = acc[j][d * 4 + w];
-                        a = xor3(a, p1, p2);
-                        a ^= p3;
+                        uint32_t& q = pend[j][d * 4 + w];
+                        if constexpr (!PAIR) {
+                            a = c == 0 ? p1 ^ p2 ^ p3 : xor3(a, p1, p2) ^ p3;
+                        } else if (c == 0 && K == 1) {
+                            a = xor3(p1, p2, p3);
+                        } else if (c == 0) {
+                            a = p1 ^ p2;
+                            q = p3;
+                        } else if (c & 1) {
+                            a = xor3(a, p1, p2);
+                            a = xor3(a, p3, q);
+                        } else if (c == K - 1) {
+                            a = xor3(a, p1, p2);
+                            a ^= p3;
+                        } else {
+                            a = xor3(a, p1, p2);
+                            q = p3;
+                        }
                     }
                 }
             if (c + P < K) load_col(c + P, v[slot]);
@@ -239,9 +263,9 @@ __global__ __launch_bounds__(kWG) void rs_generic_kernel(const RsPlanDev* __rest
 }
 
 // ------------------------------------------------------------------ dispatch table
-template <int K, int MT, int D, bool NT>
+template <int K, int MT, int D, bool NT, int PF = 0, bool PAIR = true>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR>);
 }
 
 template <int K, int D, bool NT>
@@ -264,6 +288,25 @@ static void fill_d(FastKernelTable& t) {
     fill_k<10, D, NT>(t);
     fill_k<12, D, NT>(t);
     fill_k<16, D, NT>(t);
+}
+
+// A/B variants of the RS(10,4) encode / 1-row reconstruct shapes (rsmi_set_option "prefetch")
+const ExpKernelTable& exp_kernels() {
+    static const ExpKernelTable t = [] {
+        ExpKernelTable x{};
+        x.fn[0][0] = fast_ptr<10, 4, 1, true, 4>();
+        x.fn[0][1] = fast_ptr<10, 4, 1, true, 8>();
+        x.fn[0][2] = fast_ptr<10, 4, 1, true, 10>();
+        x.fn[1][0] = fast_ptr<10, 1, 1, true, 4>();
+        x.fn[1][1] = fast_ptr<10, 1, 1, true, 8>();
+        x.fn[1][2] = fast_ptr<10, 1, 1, true, 10>();
+        x.fn[0][3] = fast_ptr<10, 4, 1, true, 6, false>();
+        x.fn[0][4] = fast_ptr<10, 4, 1, true, 10, false>();
+        x.fn[1][3] = fast_ptr<10, 1, 1, true, 6, false>();
+        x.fn[1][4] = fast_ptr<10, 1, 1, true, 10, false>();
+        return x;
+    }();
+    return t;
 }
 
 const FastKernelTable& fast_kernels() {

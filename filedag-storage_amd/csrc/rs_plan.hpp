@@ -26,7 +26,14 @@ struct FastKernelTable {
     void* fn[17][kMaxMT + 1][3][2];
 };
 
+// Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1, NT=1);
+// v 0/1/2 = 4/8/10 rows in flight (paired XOR), v 3/4 = 6/10 rows, unpaired XOR.
+struct ExpKernelTable {
+    void* fn[2][5];
+};
+
 const FastKernelTable& fast_kernels();
+const ExpKernelTable& exp_kernels();
 void* generic_kernel();
 
 }  // namespace rsmi

@@ -57,6 +57,7 @@ def lib() -> ctypes.CDLL:
         "rsmi_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "rsmi_abi_version": (ctypes.c_int, []),
         "rsmi_shard_size": (c_size, [c_size, ctypes.c_int]),
+        "rsmi_recommended_pitch": (c_size, [c_size]),
         "rsmi_encode_matrix": (ctypes.c_int, [ctypes.c_void_p, u8p]),
         "rsmi_check_shards": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_size), ctypes.c_int, ctypes.POINTER(c_size)]),
         "rsmi_decode_matrix": (ctypes.c_int, [ctypes.c_void_p, u8p, u8p, ctypes.POINTER(ctypes.c_int)]),
@@ -274,6 +275,10 @@ class Erasure:
 
 def NewErasure(data_blocks: int, parity_blocks: int, block_size: int, device: int = 0) -> Erasure:
     return Erasure(data_blocks, parity_blocks, block_size, device)
+
+
+def recommended_pitch(S: int) -> int:
+    return lib().rsmi_recommended_pitch(S)
 
 
 def device_count() -> int:

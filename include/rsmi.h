@@ -62,6 +62,11 @@ int rsmi_abi_version(void);
 /* Erasure.ShardSize (erasure.go:96-98) = ceilFrac(B, k) (utils.go:6-21). */
 size_t rsmi_shard_size(size_t block_size, int k);
 
+/* Device row pitch for shards of S bytes that the fast kernels stream best: the next
+ * power of two (HBM channel spreading), or S rounded up to 4 KiB when that would waste
+ * more than half a shard.  The host-staged entry points use it internally. */
+size_t rsmi_recommended_pitch(size_t S);
+
 /* The cached (k+m) x k encode matrix, row-major. */
 int rsmi_encode_matrix(const rsmi_ctx* ctx, uint8_t* out);
 
@@ -125,8 +130,9 @@ int rsmi_reconstruct_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t shard_st
 
 /* ------------------------------------------------------------------ tuning / introspection */
 
-/* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (0|1),
- * "waves_per_cu" (grid cap).  Returns RSMI_ERR_INVALID_ARG for unknown keys. */
+/* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (0|1,
+ * default 1), "waves_per_cu" (grid cap, 0 = occupancy), "prefetch" (experimental RS(10,4)
+ * variants).  Returns RSMI_ERR_INVALID_ARG for unknown keys or values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */
 const char* rsmi_last_kernel(const rsmi_ctx* ctx);

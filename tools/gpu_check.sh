@@ -1,9 +1,10 @@
 #!/bin/bash
-# One GPU session: tests, smoke, bench, rocprofv3 kernel trace.  Each step has its own
-# time limit; the chain stops at the first failure.
+# One GPU session: tests, smoke, bench, rocprofv3 kernel trace + PMC passes.  Each step
+# has its own time limit; the chain stops at the first failure.
 set -o pipefail
-mkdir -p gpurun_out
 cd "$(dirname "$0")/.."
+R=$(pwd)
+mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEP=${1:-all}
 if [[ $STEP == all || $STEP == tests ]]; then
@@ -12,10 +13,13 @@ if [[ $STEP == all || $STEP == tests ]]; then
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
   timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
-  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-seconds 10 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
+  timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 > "$OLDPWD/gpurun_out/prof_bench.json" 2> "$OLDPWD/gpurun_out/prof.err") || { echo "rocprof failed"; tail -20 gpurun_out/prof.err; exit 1; }
-  find gpurun_out/prof -name "*stats*" | head
+  rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err") || { echo "rocprof failed"; tail -20 gpurun_out/prof.err; exit 1; }
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_fetch.log" 2>&1) || { echo "pmc fetch failed"; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_write.log" 2>&1) || { echo "pmc write failed"; tail -20 gpurun_out/pmc_write.log; exit 1; }
+  find gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.csv" | head -20
 fi

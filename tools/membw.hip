@@ -1,0 +1,85 @@
+// membw.hip -- diagnostic ceilings for the RS kernels (not part of the product).
+//   membw_copy<U,NT>:  out[i] = in[i], U x 16 B per lane in flight, grid-stride
+//   membw_rows<K,M,NT>: the exact row/tile access pattern of rs_fast_kernel (K rows read,
+//                    M rows written, 1 KiB per wave-instruction) with the GF math replaced
+//                    by a plain XOR -- the memory ceiling for that pattern.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void membw_copy(const u32x4* __restrict__ in, u32x4* __restrict__ out, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    uint64_t i = uint64_t(blockIdx.x) * 256 * U + threadIdx.x;
+    for (; i + (U - 1) * 256 < n; i += stride * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = ld<NT>(in + i + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; u++) st<NT>(out + i + u * 256, v[u]);
+    }
+}
+
+template <int K, int M, bool NT>
+__global__ __launch_bounds__(256) void membw_rows(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                  uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                  uint32_t tpb, uint32_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        const uint32_t ch = tib * 64 + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) acc ^= ld<NT>(reinterpret_cast<const u32x4*>(ib + c * rs) + chl);
+        if (ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < M; j++) st<NT>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+        }
+    }
+}
+
+extern "C" {
+int membw_copy_launch(int U, int NT, const void* in, void* out, uint64_t bytes, int grid, void* stream) {
+    auto st = (hipStream_t)stream;
+    const u32x4* i = (const u32x4*)in;
+    u32x4* o = (u32x4*)out;
+    const uint64_t n = bytes / 16;
+#define C(u, nt) \
+    if (U == u && NT == nt) membw_copy<u, nt><<<grid, 256, 0, st>>>(i, o, n); else
+    C(1, 0) C(1, 1) C(2, 0) C(2, 1) C(4, 0) C(4, 1) return -1;
+#undef C
+    return hipGetLastError();
+}
+
+int membw_rows_launch(int K, int M, int NT, const void* in, void* out, uint64_t in_bs, uint64_t rs, uint64_t out_bs,
+                      uint32_t S, uint64_t nblocks, int grid, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+#define R(k, m, nt) \
+    if (K == k && M == m && NT == nt) membw_rows<k, m, nt><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles); else
+    R(10, 4, 0) R(10, 4, 1) R(10, 1, 0) R(10, 1, 1) R(16, 4, 0) R(16, 4, 1) R(4, 2, 0) R(4, 2, 1) R(1, 1, 0) R(1, 1, 1) return -1;
+#undef R
+    return hipGetLastError();
+}
+}
