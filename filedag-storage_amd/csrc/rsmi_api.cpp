@@ -371,7 +371,7 @@ size_t rsmi_recommended_pitch(size_t S) {
     // power-of-two row pitch spreads a block's concurrent row streams evenly over the
     // HBM channels (+13% measured at S=26215); fall back to 4 KiB granules when the
     // padding would exceed half a shard
-    if (p <= S + S / 2) return p;
+    if (p <= S + S / 2 || p <= 4096) return p;
     return round_up(S, 4096);
 }
 
@@ -494,8 +494,9 @@ int rsmi_encode(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
 }
 
 int rsmi_encode_block(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out) {
-    if (!c || !shards_out || (B && !block)) return RSMI_ERR_INVALID_ARG;
-    if (B == 0) return RSMI_ERR_SHORT_DATA;  // upstream Split
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;  // upstream Split checks this first
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
     const size_t S = rsmi_shard_size(B, c->k);
     std::memcpy(shards_out, block, B);
     std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding

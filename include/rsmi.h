@@ -63,8 +63,9 @@ int rsmi_abi_version(void);
 size_t rsmi_shard_size(size_t block_size, int k);
 
 /* Device row pitch for shards of S bytes that the fast kernels stream best: the next
- * power of two (HBM channel spreading), or S rounded up to 4 KiB when that would waste
- * more than half a shard.  The host-staged entry points use it internally. */
+ * power of two (HBM channel spreading; always taken up to 4 KiB), or S rounded up to
+ * 4 KiB when a power of two would waste more than half a shard.  The host-staged entry
+ * points use it internally. */
 size_t rsmi_recommended_pitch(size_t S);
 
 /* The cached (k+m) x k encode matrix, row-major. */

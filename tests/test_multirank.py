@@ -1,0 +1,63 @@
+"""world_size-2 gloo rehearsal of the multi-GPU path on CPU.
+
+bench.py runs one process per GPU with no data-path collective: each rank codes its own
+blocks and only the timing barrier / max-over-ranks reduction crosses ranks.  Here two
+CPU ranks take their block ranges (rsmi.multi.partition_blocks), code them with the
+oracle as a stand-in for their GPU (test-only), and rank 0 checks that the union is
+byte-identical to one process coding the whole batch, and that bench.max_over_ranks
+reduces the way the bench reports it."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    import oracle_lib as orc
+    from rsmi import multi
+
+    w, r, _ = bench.dist_setup()
+    assert (w, r) == (world, rank)
+    k, m, S, nb = 4, 2, 1000, 13
+    data = orc.splitmix64_bytes(0xF11EDA6, nb * k * S).reshape(nb, k, S)
+    start, count = multi.partition_blocks(nb, world, rank)
+    par = orc.encode_fast(k, m, np.ascontiguousarray(data[start:start + count]), threads=1)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (start, count, par))
+    bench.barrier(world)
+    el = bench.max_over_ranks(0.5 + rank, world)
+    if rank == 0:
+        full = np.concatenate([g[2] for g in sorted(gathered, key=lambda g: g[0])], axis=0)
+        ref = orc.encode_fast(k, m, data, threads=1)
+        np.save(os.path.join(out_dir, "ok.npy"), np.array([np.array_equal(full, ref), el == 0.5 + world - 1,
+                                                          sum(g[1] for g in gathered) == nb]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_partition_and_timing(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ok = np.load(os.path.join(tmp_path, "ok.npy"))
+    assert ok.all(), ok
