@@ -262,6 +262,43 @@ __global__ __launch_bounds__(kWG) void rs_generic_kernel(const RsPlanDev* __rest
     }
 }
 
+// Strided byte-row copy on the device (any src/dst alignment): rows x width bytes from
+// src (row pitch spitch) to dst (row pitch dpitch).  Host staging uses it to turn the
+// contiguous Split layout (pitch S, often odd) into the 16-B-aligned pitched layout and
+// back, so PCIe transfers stay linear (odd-width 2-D DMA runs at 3-9 GB/s on MI355X).
+// Each thread writes one naturally aligned destination dword; its 4 source bytes are
+// funnel-shifted out of the two aligned source dwords that cover them.  A row's first
+// and last dwords may be shared with a neighbouring row, so they are written bytewise.
+__global__ __launch_bounds__(kWG) void rs_repitch_kernel(const uint8_t* __restrict__ src, uint64_t spitch,
+                                                         uint8_t* __restrict__ dst, uint64_t dpitch, uint64_t width,
+                                                         uint64_t rows) {
+    const uint64_t dw_per_row = (width + 6) / 4 + 1;  // upper bound of dwords a row can touch
+    const uint64_t total = dw_per_row * rows;
+    for (uint64_t i = uint64_t(blockIdx.x) * kWG + threadIdx.x; i < total; i += uint64_t(gridDim.x) * kWG) {
+        const uint64_t r = i / dw_per_row, q = i - r * dw_per_row;
+        const uintptr_t drow = reinterpret_cast<uintptr_t>(dst + r * dpitch);
+        const uintptr_t a = (drow & ~uintptr_t(3)) + 4 * q;  // aligned destination dword
+        if (a >= drow + width) continue;
+        const uint8_t* srow = src + r * spitch;
+        const int64_t off = int64_t(a) - int64_t(drow);     // row offset of the dword's byte 0
+        if (off >= 0 && uint64_t(off) + 4 <= width) {
+            const uintptr_t sa = reinterpret_cast<uintptr_t>(srow) + uint64_t(off);
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(sa & ~uintptr_t(3));
+            const uint32_t sh = uint32_t(sa & 3);
+            const uint32_t lo = p[0];
+            const uint32_t hi = sh ? p[1] : 0u;  // a second dword only when straddling
+            *reinterpret_cast<uint32_t*>(a) = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        } else {
+            for (int b = 0; b < 4; b++) {
+                const int64_t o = off + b;
+                if (o >= 0 && uint64_t(o) < width) reinterpret_cast<uint8_t*>(a)[b] = srow[o];
+            }
+        }
+    }
+}
+
+void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
+
 // ------------------------------------------------------------------ dispatch table
 template <int K, int MT, int D, bool NT, int PF = 0, bool PAIR = true>
 static void* fast_ptr() {

@@ -35,5 +35,6 @@ struct ExpKernelTable {
 const FastKernelTable& fast_kernels();
 const ExpKernelTable& exp_kernels();
 void* generic_kernel();
+void* repitch_kernel();
 
 }  // namespace rsmi

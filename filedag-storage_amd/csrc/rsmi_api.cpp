@@ -45,7 +45,8 @@ struct Staging {
     hipStream_t stream = nullptr;
     uint8_t* d_in = nullptr;
     uint8_t* d_out = nullptr;
-    size_t in_cap = 0, out_cap = 0;
+    uint8_t* d_lin = nullptr;  // linear (pitch S) landing buffer for odd S
+    size_t in_cap = 0, out_cap = 0, lin_cap = 0;
 };
 
 }  // namespace
@@ -58,7 +59,10 @@ struct rsmi_ctx {
     int dev_status = RSMI_OK;
     int num_cu = 256;
     std::map<std::string, std::shared_ptr<Plan>> plans;
+    std::map<void*, int> occupancy;
     std::vector<Staging> staging;  // [0] single-block calls, [0..2] batch pipeline
+    uint8_t* h_stage = nullptr;    // pinned landing area for rebuilt rows (odd S)
+    size_t h_stage_cap = 0;
     // options
     int opt_d = 1;
     int opt_nt = 1;  // nontemporal loads/stores: +5-7% on every shape measured
@@ -237,9 +241,11 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
             const uint64_t tpb = (cpb + uint64_t(kWave * D) - 1) / uint64_t(kWave * D);
-            int occ = 0;
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
-            if (occ <= 0) occ = 1;
+            int& occ = c->occupancy[fn];  // queried once per kernel, not per launch
+            if (occ <= 0) {
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
+                if (occ <= 0) occ = 1;
+            }
             long wg_cap = long(c->num_cu) * occ;
             if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / (kWG / kWave));
             // split into launches whose tile count fits 32 bits
@@ -357,8 +363,10 @@ void rsmi_close(rsmi_ctx* c) {
                 if (s.stream) (void)hipStreamSynchronize(s.stream);
                 if (s.d_in) (void)hipFree(s.d_in);
                 if (s.d_out) (void)hipFree(s.d_out);
+                if (s.d_lin) (void)hipFree(s.d_lin);
                 if (s.stream) (void)hipStreamDestroy(s.stream);
             }
+            if (c->h_stage) (void)hipHostFree(c->h_stage);
         }
     }
     delete c;
@@ -368,10 +376,13 @@ size_t rsmi_recommended_pitch(size_t S) {
     if (S == 0) return 0;
     size_t p = 16;
     while (p < S) p <<= 1;
-    // power-of-two row pitch spreads a block's concurrent row streams evenly over the
-    // HBM channels (+13% measured at S=26215); fall back to 4 KiB granules when the
-    // padding would exceed half a shard
-    if (p <= S + S / 2 || p <= 4096) return p;
+    // Measured on MI355X (tools/pitchsweep*.py, DESIGN.md "Layout"): a power-of-two row
+    // pitch is +13% for S = 26215 (32 KiB) and best for S = 262144 (itself a power of
+    // two), but the worst choice for S = 104858 (128 KiB: -4% vs 4 KiB granules).  Use
+    // powers of two for shards up to 64 KiB (padding <= 50%) and exact powers; otherwise
+    // 4 KiB granules.
+    if (p == S || p <= 4096) return p;
+    if (S <= 65536 && p <= S + S / 2) return p;
     return round_up(S, 4096);
 }
 
@@ -509,9 +520,34 @@ int rsmi_reconstruct(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* pres
     return rsmi_reconstruct_batch_host(c, shards, size_t(c->n) * S, S, 1, present, data_only);
 }
 
+}  // extern "C"
+
 // ---------------------------------------------------------------- host memory, batches
 // Pipeline: chunks of blocks round-robin over 3 streams, each with its own device
-// buffers: H2D (2-D copy into 256-B row pitch) -> kernel -> D2H (2-D copy back).
+// buffers: H2D -> kernel -> D2H.  When S is a multiple of 8 the DMA engines move rows
+// straight between the contiguous host layout (pitch S) and the pitched device layout with
+// 2-D copies at full PCIe rate.  Odd-width 2-D copies crawl (3-9 GB/s measured,
+// tools/copyprobe.py), so for other S the PCIe copies stay linear and rs_repitch_kernel
+// re-lays rows out on the device (HBM-speed, ~1% of the PCIe time).
+namespace {
+
+bool dma_2d_ok(size_t S) { return S % 8 == 0; }
+
+int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width, size_t rows,
+            hipStream_t stream) {
+    if (!rows || !width) return RSMI_OK;
+    uint64_t sp = spitch, dp = dpitch, w = width, r = rows;
+    const uint64_t dwords = ((w + 6) / 4 + 1) * r;
+    const uint32_t grid = uint32_t(std::min<uint64_t>((dwords + kWG - 1) / kWG, 8192));
+    void* args[] = {&src, &sp, &dst, &dp, &w, &r};
+    HIP_TRY(hipLaunchKernel(repitch_kernel(), dim3(grid), dim3(kWG), args, 0, stream));
+    return RSMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                            size_t parity_block_stride, size_t S, size_t nblocks) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
@@ -525,8 +561,10 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
     std::shared_ptr<Plan> plan;
     rc = encode_plan(c, plan);
     if (rc) return rc;
+    const size_t k = size_t(c->k), m = size_t(c->m);
     const size_t Sp = rsmi_recommended_pitch(S);
-    const size_t in_bs = size_t(c->k) * Sp, out_bs = size_t(c->m) * Sp;
+    const size_t in_bs = k * Sp, out_bs = m * Sp;
+    const bool d2 = dma_2d_ok(S);
     const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (in_bs + out_bs));
     const int ns = nblocks > chunk ? 3 : 1;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
@@ -534,22 +572,42 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
         const size_t nb = std::min(chunk, nblocks - b0);
         if ((rc = reserve(st.d_in, st.in_cap, nb * in_bs))) return rc;
         if ((rc = reserve(st.d_out, st.out_cap, nb * out_bs))) return rc;
+        if (!d2 && (rc = reserve(st.d_lin, st.lin_cap, nb * k * S))) return rc;
         const uint8_t* src = data + b0 * data_block_stride;
         uint8_t* dst = parity + b0 * parity_block_stride;
-        if (data_block_stride == size_t(c->k) * S) {
-            HIP_TRY(hipMemcpy2DAsync(st.d_in, Sp, src, S, S, nb * c->k, hipMemcpyHostToDevice, st.stream));
-        } else {
+        // host -> device
+        if (d2 && data_block_stride == k * S) {
+            HIP_TRY(hipMemcpy2DAsync(st.d_in, Sp, src, S, S, nb * k, hipMemcpyHostToDevice, st.stream));
+        } else if (d2) {
             for (size_t b = 0; b < nb; b++)
-                HIP_TRY(hipMemcpy2DAsync(st.d_in + b * in_bs, Sp, src + b * data_block_stride, S, S, c->k,
+                HIP_TRY(hipMemcpy2DAsync(st.d_in + b * in_bs, Sp, src + b * data_block_stride, S, S, k,
                                          hipMemcpyHostToDevice, st.stream));
+        } else {
+            if (data_block_stride == k * S)
+                HIP_TRY(hipMemcpyAsync(st.d_lin, src, nb * k * S, hipMemcpyHostToDevice, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(st.d_lin + b * k * S, src + b * data_block_stride, k * S,
+                                           hipMemcpyHostToDevice, st.stream));
+            if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * k, st.stream))) return rc;
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
-        if (parity_block_stride == size_t(c->m) * S) {
-            HIP_TRY(hipMemcpy2DAsync(dst, S, st.d_out, Sp, S, nb * c->m, hipMemcpyDeviceToHost, st.stream));
-        } else {
+        // device -> host
+        if (d2 && parity_block_stride == m * S) {
+            HIP_TRY(hipMemcpy2DAsync(dst, S, st.d_out, Sp, S, nb * m, hipMemcpyDeviceToHost, st.stream));
+        } else if (d2) {
             for (size_t b = 0; b < nb; b++)
-                HIP_TRY(hipMemcpy2DAsync(dst + b * parity_block_stride, S, st.d_out + b * out_bs, Sp, S, c->m,
+                HIP_TRY(hipMemcpy2DAsync(dst + b * parity_block_stride, S, st.d_out + b * out_bs, Sp, S, m,
                                          hipMemcpyDeviceToHost, st.stream));
+        } else {
+            // reuse d_lin (its H2D contents are consumed by the repitch above, in stream order)
+            if ((rc = repitch(st.d_lin, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
+            if (parity_block_stride == m * S)
+                HIP_TRY(hipMemcpyAsync(dst, st.d_lin, nb * m * S, hipMemcpyDeviceToHost, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(dst + b * parity_block_stride, st.d_lin + b * m * S, m * S,
+                                           hipMemcpyDeviceToHost, st.stream));
         }
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
@@ -577,24 +635,67 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_strid
         if (present[i]) in_rows.push_back(i);
     for (int i = 0; i < c->n; i++)
         if (!present[i] && (i < c->k || !data_only)) out_rows.push_back(i);
+    const size_t n = size_t(c->n), nr = out_rows.size();
     const size_t Sp = rsmi_recommended_pitch(S);
-    const size_t bs = size_t(c->n) * Sp;
+    const size_t bs = n * Sp;
+    const bool d2 = dma_2d_ok(S);
     const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / bs);
     const int ns = nblocks > chunk ? 3 : 1;
+    if (!d2) {  // pinned landing area for the rebuilt rows, scattered on the host at the end
+        const size_t need = nblocks * nr * S;
+        if (c->h_stage_cap < need) {
+            if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
+            c->h_stage = nullptr;
+            c->h_stage_cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), need, hipHostMallocDefault));
+            c->h_stage_cap = need;
+        }
+    }
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
         if ((rc = reserve(st.d_in, st.in_cap, nb * bs))) return rc;
         uint8_t* h = shards + b0 * block_stride;
-        for (int r : in_rows)
-            HIP_TRY(hipMemcpy2DAsync(st.d_in + size_t(r) * Sp, bs, h + size_t(r) * S, block_stride, S, nb,
-                                     hipMemcpyHostToDevice, st.stream));
+        if (d2) {
+            for (int r : in_rows)
+                HIP_TRY(hipMemcpy2DAsync(st.d_in + size_t(r) * Sp, bs, h + size_t(r) * S, block_stride, S, nb,
+                                         hipMemcpyHostToDevice, st.stream));
+        } else {
+            // whole blocks move linearly (missing rows ride along as don't-care bytes)
+            if ((rc = reserve(st.d_lin, st.lin_cap, nb * n * S))) return rc;
+            if (block_stride == n * S)
+                HIP_TRY(hipMemcpyAsync(st.d_lin, h, nb * n * S, hipMemcpyHostToDevice, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(st.d_lin + b * n * S, h + b * block_stride, n * S, hipMemcpyHostToDevice,
+                                           st.stream));
+            if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * n, st.stream))) return rc;
+        }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, bs, st.d_in, Sp, bs, S, nb, st.stream))) return rc;
-        for (int r : out_rows)
-            HIP_TRY(hipMemcpy2DAsync(h + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S, nb,
-                                     hipMemcpyDeviceToHost, st.stream));
+        if (d2) {
+            for (int r : out_rows)
+                HIP_TRY(hipMemcpy2DAsync(h + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S, nb,
+                                         hipMemcpyDeviceToHost, st.stream));
+        } else {
+            // gather rebuilt rows compactly as [row][block][S], then one linear D2H
+            for (size_t j = 0; j < nr; j++)
+                if ((rc = repitch(st.d_lin + j * nb * S, S, st.d_in + size_t(out_rows[j]) * Sp, bs, S, nb,
+                                  st.stream)))
+                    return rc;
+            HIP_TRY(hipMemcpyAsync(c->h_stage + b0 * nr * S, st.d_lin, nb * nr * S, hipMemcpyDeviceToHost,
+                                   st.stream));
+        }
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
+    if (!d2) {
+        for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+            const size_t nb = std::min(chunk, nblocks - b0);
+            const uint8_t* hs = c->h_stage + b0 * nr * S;
+            for (size_t j = 0; j < nr; j++)
+                for (size_t b = 0; b < nb; b++)
+                    std::memcpy(shards + (b0 + b) * block_stride + size_t(out_rows[j]) * S, hs + (j * nb + b) * S, S);
+        }
+    }
     return RSMI_OK;
 }
 

@@ -47,6 +47,13 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"librsmi.so not built at {LIB_PATH}: run `python __graft_entry__.py build`")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7).
+    # Loaded first, it also satisfies librsmi's dependency; loaded after librsmi, a second
+    # runtime (ROCm's) would already own the device and torch would report no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     c_size = ctypes.c_size_t
     u8p = ctypes.c_void_p

@@ -62,10 +62,10 @@ int rsmi_abi_version(void);
 /* Erasure.ShardSize (erasure.go:96-98) = ceilFrac(B, k) (utils.go:6-21). */
 size_t rsmi_shard_size(size_t block_size, int k);
 
-/* Device row pitch for shards of S bytes that the fast kernels stream best: the next
- * power of two (HBM channel spreading; always taken up to 4 KiB), or S rounded up to
- * 4 KiB when a power of two would waste more than half a shard.  The host-staged entry
- * points use it internally. */
+/* Device row pitch for shards of S bytes that the fast kernels stream best on MI355X:
+ * the next power of two for shards up to 64 KiB (when it wastes at most half a shard) and
+ * for exact powers of two, otherwise S rounded up to 4 KiB (measured, DESIGN.md "Layout").
+ * The host-staged entry points use it internally. */
 size_t rsmi_recommended_pitch(size_t S);
 
 /* The cached (k+m) x k encode matrix, row-major. */

@@ -67,9 +67,10 @@ def test_shard_size(B, k):
 
 def test_recommended_pitch():
     p = rsmi.recommended_pitch
-    assert p(26215) == 32768 and p(65536) == 65536 and p(262144) == 262144 and p(104858) == 131072
+    assert p(26215) == 32768 and p(65536) == 65536 and p(262144) == 262144 and p(104858) == 106496
     assert p(17) == 32 and p(1) == 16
     assert p(40000) == 40960  # next pow2 (65536) would waste > S/2
+    assert p(1 << 22) == 1 << 22 and p(3000) == 4096
     for S in (1, 3, 17, 4097, 26215, 40000, 104858, 262145):
         assert p(S) >= S and p(S) % 16 == 0
 

@@ -283,3 +283,37 @@ def test_golden_vectors_gpu(k, m):
         sh = [bytes(want[i]) if present[i] else None for i in range(n)]
         e.decode_data_blocks(sh)
         assert all(sh[i] == bytes(want[i]) for i in range(k))
+
+
+@pytest.mark.parametrize("S", [26215, 26216, 4096, 1, 104858])
+@pytest.mark.parametrize("padded", [False, True])
+def test_batch_host_layouts(S, padded):
+    """Host batch entry points over odd/even S and contiguous vs padded host block strides
+    (linear-copy + device repitch path for odd S, 2-D DMA path otherwise)."""
+    k, m = 10, 4
+    n = k + m
+    nb = 7 if S > 50000 else 37
+    gap = 13 if padded else 0
+    dbs, pbs, sbs = k * S + gap, m * S + gap, n * S + gap
+    data = np.zeros(nb * dbs, dtype=np.uint8)
+    blocks = _rng_bytes(S + 3, nb * k * S).reshape(nb, k, S)
+    for b in range(nb):
+        data[b * dbs:b * dbs + k * S] = blocks[b].reshape(-1)
+    par = np.full(nb * pbs, 0x77, dtype=np.uint8)
+    want = orc.encode_fast(k, m, blocks)
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_host_ptr(data.ctypes.data, dbs, par.ctypes.data, pbs, S, nb)
+        for b in range(nb):
+            assert np.array_equal(par[b * pbs:b * pbs + m * S].reshape(m, S), want[b]), b
+            assert (par[b * pbs + m * S:(b + 1) * pbs] == 0x77).all()  # gaps untouched
+        sh = np.full(nb * sbs, 0x33, dtype=np.uint8)
+        for b in range(nb):
+            sh[b * sbs:b * sbs + k * S] = blocks[b].reshape(-1)
+            sh[b * sbs + k * S:b * sbs + n * S] = want[b].reshape(-1)
+        full = sh.copy()
+        lost = [2, 11]
+        for b in range(nb):
+            for r in lost:
+                sh[b * sbs + r * S:b * sbs + (r + 1) * S] = 0
+        c.reconstruct_batch_host_ptr(sh.ctypes.data, sbs, S, nb, [i not in lost for i in range(n)], False)
+        assert np.array_equal(sh, full)
