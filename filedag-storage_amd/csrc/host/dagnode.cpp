@@ -1,0 +1,508 @@
+// dagnode.cpp -- see dagnode.hpp.  Line references are to the reference's
+// dag/node/dagnode/node.go, data_recovery.go and error.go.
+#include "dagnode.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+
+namespace rsmi {
+namespace host {
+
+const char* const kErrReadQuorum = "Read failed. Insufficient number of nodes online";  // error.go:12
+const char* const kErrNodeNotFound = "node not found";                                   // error.go:9
+static const char* const kErrNodeAccessDenied = "node access denied";                     // error.go:18
+static const char* const kErrCanceled = "context canceled";
+
+// ------------------------------------------------------------------ quorum helpers
+namespace {
+
+// paralleltask.Wait (parallel_task.go:59-84) applied to results in arrival order.
+class QuorumWait {
+public:
+    QuorumWait(int success_quorum, int failure_quorum) : sq_(success_quorum), fq_(failure_quorum) {}
+    // returns true once the outcome is decided
+    bool add(const Status& s) {
+        if (decided_) return true;
+        if (s.ok()) {
+            if (++succ_ >= sq_) decided_ = true;
+        } else if (++fail_ >= fq_) {
+            result_ = s;  // "return last error"
+            decided_ = true;
+        }
+        return decided_;
+    }
+    bool decided() const { return decided_; }
+    // if every task finished without reaching either quorum, Wait would block forever in Go
+    // (all goroutines done); report it as the read/write quorum failure instead
+    Status result(const char* undecided) const { return decided_ ? result_ : Status::Error(undecided); }
+
+private:
+    int sq_, fq_, succ_ = 0, fail_ = 0;
+    bool decided_ = false;
+    Status result_;
+};
+
+}  // namespace
+
+Status reduce_quorum_errs(const std::vector<Status>& errs, int quorum, const char* quorum_err) {
+    std::vector<std::pair<std::string, int>> counts;  // first-occurrence order (Go: map order)
+    for (const auto& e : errs) {
+        if (e.err == kErrNodeNotFound || e.err == kErrNodeAccessDenied) continue;
+        auto it = std::find_if(counts.begin(), counts.end(), [&](auto& p) { return p.first == e.err; });
+        if (it == counts.end())
+            counts.push_back({e.err, 1});
+        else
+            it->second++;
+    }
+    int max = 0;
+    std::string max_err;
+    for (auto& p : counts) {
+        if (max < p.second) {
+            max = p.second;
+            max_err = p.first;
+        } else if (max == p.second && p.first.empty()) {
+            max_err.clear();  // prefer nil on ties (error.go:51-54)
+        }
+    }
+    if (max >= quorum) return Status{max_err};
+    return Status::Error(quorum_err);
+}
+
+Status find_meta_in_quorum(const std::vector<Meta>& metas, int quorum, Meta* out) {
+    if (quorum < 2) return Status::Error(kErrReadQuorum);  // node.go:493-495
+    // the reference hashes fmt.Sprint(BlockSize) with sha256; equal hashes <=> equal sizes
+    std::vector<std::pair<int32_t, int>> counts;
+    for (const auto& m : metas) {
+        auto it = std::find_if(counts.begin(), counts.end(), [&](auto& p) { return p.first == m.block_size; });
+        if (it == counts.end())
+            counts.push_back({m.block_size, 1});
+        else
+            it->second++;
+    }
+    int max = 0;
+    int32_t best = 0;
+    for (auto& p : counts)
+        if (p.second > max) {
+            max = p.second;
+            best = p.first;
+        }
+    if (max < quorum) return Status::Error(kErrReadQuorum);
+    out->block_size = best;
+    return Status::Ok();
+}
+
+// ------------------------------------------------------------------ construction
+Status DagNode::New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
+                    std::unique_ptr<DagNode>* out, int device) {
+    const size_t n = cfg.nodes.size();
+    if (n != size_t(cfg.data_blocks + cfg.parity_blocks) || n == 0 || clients.size() != n)
+        return Status::Error("dag node config is incorrect");  // node.go:55-57
+    std::unique_ptr<DagNode> d(new DagNode());
+    d->config_ = cfg;
+    d->device_ = device;
+    d->slots_.assign(kClusterSlots / 8, 0);
+    for (auto& c : clients) d->nodes_.push_back(StorageNode{c, false});
+    *out = std::move(d);
+    return Status::Ok();
+}
+
+DagNode::~DagNode() { Close(); }
+
+void DagNode::Close() {
+    {
+        std::lock_guard<std::mutex> g(q_mu_);
+        stop_ = true;
+    }
+    q_cv_.notify_all();
+    if (worker_.joinable()) worker_.join();
+}
+
+std::pair<int, int> DagNode::EntryQuorum() const {  // node.go:439-446
+    int write_quorum = config_.data_blocks;
+    if (config_.data_blocks == config_.parity_blocks) write_quorum++;
+    return {config_.data_blocks, write_quorum};
+}
+
+bool DagNode::GetDataNodeState(int i) const {
+    if (i < 0 || i >= int(nodes_.size())) throw std::out_of_range("input setIndex is illegal");  // log.Fatalf
+    return nodes_[i].state;
+}
+
+bool DagNode::AddSlot(uint64_t slot) {
+    if (slot >= uint64_t(kClusterSlots)) throw std::out_of_range("slot out of range");
+    const bool old = slots_[slot / 8] >> (slot % 8) & 1;
+    slots_[slot / 8] |= uint8_t(1u << (slot % 8));
+    if (!old) num_slots_++;
+    return old;
+}
+
+bool DagNode::ClearSlot(uint64_t slot) {
+    if (slot >= uint64_t(kClusterSlots)) throw std::out_of_range("slot out of range");
+    const bool old = slots_[slot / 8] >> (slot % 8) & 1;
+    slots_[slot / 8] &= uint8_t(~(1u << (slot % 8)));
+    if (old) num_slots_--;
+    return old;
+}
+
+bool DagNode::GetSlot(uint64_t slot) const {
+    if (slot >= uint64_t(kClusterSlots)) throw std::out_of_range("slot out of range");
+    return slots_[slot / 8] >> (slot % 8) & 1;
+}
+
+void DagNode::HealthCheckAll() {
+    for (auto& sn : nodes_) sn.state = sn.client->Healthy();
+}
+
+// ------------------------------------------------------------------ meta
+Bytes DagNode::encode_meta(int32_t size) {
+    Bytes b(4);
+    for (int i = 0; i < 4; i++) b[i] = uint8_t(uint32_t(size) >> (8 * i));  // binary.LittleEndian
+    return b;
+}
+
+Status DagNode::get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online) {
+    const size_t n = nodes_.size();
+    std::vector<Meta> metas(n);
+    std::vector<Status> errs(n);
+    for (size_t i = 0; i < n; i++) {  // readAllMeta (node.go:450-489)
+        Bytes mb;
+        Status s = nodes_[i].client->GetMeta(key, &mb);
+        if (!s.ok()) {
+            errs[i] = s;
+            continue;
+        }
+        if (mb.size() < 4) {
+            errs[i] = Status::Error("unexpected EOF");
+            continue;
+        }
+        metas[i].block_size = int32_t(uint32_t(mb[0]) | uint32_t(mb[1]) << 8 | uint32_t(mb[2]) << 16 |
+                                      uint32_t(mb[3]) << 24);
+    }
+    const int read_quorum = EntryQuorum().first;
+    Status r = reduce_quorum_errs(errs, read_quorum, kErrReadQuorum);
+    if (!r.ok()) return r;
+    Status f = find_meta_in_quorum(metas, read_quorum, meta);
+    if (!f.ok()) return f;
+    if (online) {
+        online->assign(n, nullptr);
+        for (size_t i = 0; i < n; i++)
+            if (metas[i].block_size == meta->block_size) (*online)[i] = &nodes_[i];
+    }
+    return Status::Ok();
+}
+
+Status DagNode::GetSize(const std::string& key, int* size) {
+    Meta meta;
+    Status s = get_meta_info(key, &meta, nullptr);
+    *size = meta.block_size;
+    return s;
+}
+
+Status DagNode::Has(const std::string& key, bool* has) {
+    int size;
+    Status s = GetSize(key, &size);
+    *has = s.ok();
+    return s;
+}
+
+// ------------------------------------------------------------------ write path
+Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:358-408
+    const Bytes meta = encode_meta(int32_t(block.size()));
+    Erasure enc;
+    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
+    if (!s.ok()) return s;
+    std::vector<Bytes> shards;
+    s = enc.EncodeData(block, &shards);
+    if (!s.ok()) return s;
+    const int wq = EntryQuorum().second;
+    QuorumWait w(wq, int(nodes_.size()) - wq + 1);
+    for (size_t i = 0; i < nodes_.size(); i++) w.add(nodes_[i].client->Put(key, meta, shards[i]));  // no cancel
+    return w.result("Write failed. Insufficient number of nodes online");
+}
+
+Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<Bytes>& blocks) {
+    if (keys.size() != blocks.size()) return Status::Error("keys and blocks differ in length");
+    const int k = config_.data_blocks, m = config_.parity_blocks, n = k + m;
+    std::vector<Status> results(blocks.size());
+    // group equal-size blocks: one GPU batch encode per size, then the per-block fan-out
+    std::map<size_t, std::vector<size_t>> groups;
+    for (size_t i = 0; i < blocks.size(); i++) groups[blocks[i].size()].push_back(i);
+    for (auto& g : groups) {
+        const size_t B = g.first;
+        if (B == 0 || g.second.size() == 1) {
+            for (size_t i : g.second) results[i] = Put(keys[i], blocks[i]);
+            continue;
+        }
+        int rc;
+        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
+        if (!ctx) {
+            for (size_t i : g.second) results[i] = rsmi_status(rc);
+            continue;
+        }
+        const size_t S = rsmi_shard_size(B, k), nb = g.second.size();
+        Bytes flat(nb * size_t(n) * S, 0);  // per block: k data rows (Split, zero-padded) + m parity rows
+        for (size_t j = 0; j < nb; j++) std::memcpy(flat.data() + j * n * S, blocks[g.second[j]].data(), B);
+        rc = rsmi_encode_batch_host(ctx, flat.data(), size_t(n) * S, flat.data() + size_t(k) * S, size_t(n) * S, S, nb);
+        if (rc) {
+            for (size_t i : g.second) results[i] = rsmi_status(rc);
+            continue;
+        }
+        const Bytes meta = encode_meta(int32_t(B));
+        const int wq = EntryQuorum().second;
+        for (size_t j = 0; j < nb; j++) {
+            QuorumWait w(wq, n - wq + 1);
+            const uint8_t* base = flat.data() + j * n * S;
+            for (int i = 0; i < n; i++)
+                w.add(nodes_[i].client->Put(keys[g.second[j]], meta, Bytes(base + size_t(i) * S, base + size_t(i + 1) * S)));
+            results[g.second[j]] = w.result("Write failed. Insufficient number of nodes online");
+        }
+    }
+    // node.go:411-416 returns the error of the last Put
+    return results.empty() ? Status::Ok() : results.back();
+}
+
+Status DagNode::DeleteBlock(const std::string& key) {  // node.go:191-208
+    const int wq = EntryQuorum().second;
+    QuorumWait w(wq, int(nodes_.size()) - wq + 1);
+    for (auto& sn : nodes_) w.add(sn.client->Delete(key));
+    return w.result("Write failed. Insufficient number of nodes online");
+}
+
+// ------------------------------------------------------------------ read path
+Status DagNode::Get(const std::string& key, Bytes* block) {  // node.go:220-326
+    Meta meta;
+    std::vector<StorageNode*> online;
+    Status s = get_meta_info(key, &meta, &online);
+    if (!s.ok()) return s;
+    const int n = int(nodes_.size()), rq = EntryQuorum().first;
+    std::vector<Bytes> shards(static_cast<size_t>(n));
+    std::vector<bool> repair(size_t(n), false);
+    bool need_repair = false;
+    QuorumWait w(rq, n - rq + 1);
+    for (int i = 0; i < n; i++) {
+        if (!online[i]) {
+            // runs even after the quorum is met: the goroutine returns before its first RPC
+            if (nodes_[i].state) {
+                repair[i] = true;
+                need_repair = true;
+            }
+            w.add(Status::Error("offline node"));
+            continue;
+        }
+        if (w.decided()) continue;  // cancelOther: later fetches are cancelled, no repair
+        Bytes m, data;
+        Status g = online[i]->client->Get(key, &m, &data);
+        if (!g.ok()) {
+            repair[i] = true;  // any non-cancel error (node.go:254-258)
+            need_repair = true;
+        } else {
+            shards[i] = std::move(data);
+        }
+        w.add(g);
+    }
+    s = w.result(kErrReadQuorum);
+    if (!s.ok()) return s;
+
+    Erasure enc;
+    s = Erasure::New(config_.data_blocks, config_.parity_blocks, meta.block_size, &enc, device_);
+    if (!s.ok()) return s;
+    s = enc.DecodeDataBlocks(shards);
+    if (!s.ok()) return s;
+
+    if (need_repair) {
+        std::vector<int> idx;
+        for (int i = 0; i < n; i++)
+            if (repair[i]) idx.push_back(i);
+        const int32_t bs = meta.block_size;
+        std::lock_guard<std::mutex> g(q_mu_);
+        if (repair_queue_.size() < kRepairQueueCap)  // else: "repair queue is full, discard this task"
+            repair_queue_.push_back([this, key, bs, shards, idx]() { (void)repair_block(key, bs, shards, idx); });
+        q_cv_.notify_one();
+    }
+
+    const size_t S = size_t(enc.ShardSize());
+    block->assign(size_t(config_.data_blocks) * S, 0);
+    for (int i = 0; i < config_.data_blocks; i++)
+        std::memcpy(block->data() + size_t(i) * S, shards[i].data(), std::min(S, shards[i].size()));
+    block->resize(size_t(meta.block_size));
+    return Status::Ok();
+}
+
+// ------------------------------------------------------------------ repair
+Status DagNode::repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,
+                             const std::vector<int>& indexes) {  // data_recovery.go:115-167
+    for (int i : indexes)
+        if (i >= int(nodes_.size())) return Status::Error("repair index greater than max index of nodes");
+    int available = 0;
+    for (auto& sh : shards) available += !sh.empty();
+    if (available < EntryQuorum().first) return Status::Error("repair index greater than max index of nodes");
+    Erasure enc;
+    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, block_size, &enc, device_);
+    if (!s.ok()) return s;
+    s = enc.DecodeDataAndParityBlocks(shards);
+    if (!s.ok()) return s;
+    const Bytes meta = encode_meta(block_size);
+    for (int i : indexes) {
+        s = nodes_[i].client->Put(key, meta, shards[i]);
+        if (!s.ok()) return s;
+    }
+    return Status::Ok();
+}
+
+size_t DagNode::RepairQueueLen() {
+    std::lock_guard<std::mutex> g(q_mu_);
+    return repair_queue_.size();
+}
+
+size_t DagNode::RunRepairTasks() {
+    size_t ran = 0;
+    for (;;) {
+        std::function<void()> task;
+        {
+            std::lock_guard<std::mutex> g(q_mu_);
+            if (repair_queue_.empty()) return ran;
+            task = std::move(repair_queue_.front());
+            repair_queue_.pop_front();
+        }
+        task();
+        ran++;
+    }
+}
+
+void DagNode::StartRepairWorker() {
+    if (worker_.joinable()) return;
+    worker_ = std::thread([this] {
+        for (;;) {
+            std::function<void()> task;
+            {
+                std::unique_lock<std::mutex> g(q_mu_);
+                q_cv_.wait(g, [this] { return stop_ || !repair_queue_.empty(); });
+                if (stop_) return;
+                task = std::move(repair_queue_.front());
+                repair_queue_.pop_front();
+            }
+            task();
+        }
+    });
+}
+
+// data_recovery.go:57-81: k shards from every node but the one under repair
+Status DagNode::fetch_for_repair(const std::string& key, int repair_index, std::vector<Bytes>* shards) {
+    const int n = int(nodes_.size()), rq = EntryQuorum().first;
+    shards->assign(size_t(n), Bytes());
+    QuorumWait w(rq, n - rq + 1);
+    for (int i = 0; i < n && !w.decided(); i++) {
+        if (i == repair_index) {
+            w.add(Status::Error("there is no data in this node"));
+            continue;
+        }
+        Bytes m, data;
+        Status g = nodes_[i].client->Get(key, &m, &data);
+        if (g.ok() && data.empty()) g = Status::Error("there is no data in this node");
+        if (g.ok()) (*shards)[i] = std::move(data);
+        w.add(g);
+    }
+    return w.result(kErrReadQuorum);
+}
+
+Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
+    if (from >= int(nodes_.size())) return Status::Error("index greater than max index of nodes");
+    if (to >= int(nodes_.size())) return Status::Error("repair index greater than max index of nodes");
+    std::vector<std::string> keys;
+    Status s = nodes_[from].client->AllKeys(&keys);
+    if (!s.ok()) return s;
+    for (const auto& key : keys) {
+        Bytes mb;
+        if (nodes_[to].client->GetMeta(key, &mb).ok()) continue;
+        int size;
+        if (!GetSize(key, &size).ok()) continue;
+        std::vector<Bytes> shards;
+        if (!fetch_for_repair(key, to, &shards).ok()) continue;
+        Erasure enc;
+        s = Erasure::New(config_.data_blocks, config_.parity_blocks, size, &enc, device_);
+        if (!s.ok()) return s;
+        s = enc.DecodeDataAndParityBlocks(shards);
+        if (!s.ok()) return s;
+        s = nodes_[to].client->Put(key, encode_meta(size), shards[to]);
+        if (!s.ok()) return s;
+    }
+    return Status::Ok();
+}
+
+Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* repaired) {
+    if (from >= int(nodes_.size())) return Status::Error("index greater than max index of nodes");
+    if (to >= int(nodes_.size())) return Status::Error("repair index greater than max index of nodes");
+    if (batch == 0) batch = 1;
+    const int k = config_.data_blocks, m = config_.parity_blocks, n = k + m;
+    std::vector<std::string> keys;
+    Status s = nodes_[from].client->AllKeys(&keys);
+    if (!s.ok()) return s;
+    size_t done = 0;
+    struct Pending {
+        std::string key;
+        std::vector<Bytes> shards;
+    };
+    // (block size, survivor pattern) -> pending keys
+    std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
+    auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
+        if (pend.empty()) return Status::Ok();
+        const int size = gk.first;
+        int rc;
+        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
+        if (!ctx) return rsmi_status(rc);
+        const size_t S = rsmi_shard_size(size_t(size), k), nb = pend.size();
+        std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
+        for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
+        required[to] = 1;
+        Bytes flat(nb * size_t(n) * S, 0);
+        for (size_t j = 0; j < nb; j++)
+            for (int i = 0; i < n; i++)
+                if (present[i]) std::memcpy(flat.data() + (j * n + i) * S, pend[j].shards[i].data(), S);
+        rc = rsmi_reconstruct_rows_batch_host(ctx, flat.data(), size_t(n) * S, S, nb, present.data(), required.data());
+        if (rc) return rsmi_status(rc);
+        const Bytes meta = encode_meta(size);
+        for (size_t j = 0; j < nb; j++) {
+            const uint8_t* row = flat.data() + (j * n + size_t(to)) * S;
+            Status ps = nodes_[to].client->Put(pend[j].key, meta, Bytes(row, row + S));
+            if (!ps.ok()) return ps;
+            done++;
+        }
+        pend.clear();
+        return Status::Ok();
+    };
+    for (const auto& key : keys) {
+        Bytes mb;
+        if (nodes_[to].client->GetMeta(key, &mb).ok()) continue;
+        int size;
+        if (!GetSize(key, &size).ok()) continue;
+        std::vector<Bytes> shards;
+        if (!fetch_for_repair(key, to, &shards).ok()) continue;
+        if (size <= 0) {  // empty block: the per-key path's error behaviour (ErrShardNoData)
+            Erasure enc;
+            s = Erasure::New(k, m, size, &enc, device_);
+            if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
+            if (!s.ok()) return s;
+            continue;
+        }
+        std::string pat(size_t(n), '0');
+        for (int i = 0; i < n; i++) pat[i] = shards[i].empty() ? '0' : '1';
+        auto gk = std::make_pair(size, pat);
+        auto& pend = groups[gk];
+        pend.push_back(Pending{key, std::move(shards)});
+        if (pend.size() >= batch) {
+            s = flush(gk, pend);
+            if (!s.ok()) return s;
+        }
+    }
+    for (auto& g : groups) {
+        s = flush(g.first, g.second);
+        if (!s.ok()) return s;
+    }
+    if (repaired) *repaired = done;
+    return Status::Ok();
+}
+
+}  // namespace host
+}  // namespace rsmi

@@ -1,0 +1,126 @@
+// dagnode.hpp -- C++ mirror of dag/node/dagnode's DagNode (the erasure set).
+//
+// Same public surface the Dag Pool calls: NewDagNode, Put, Get, GetSize,
+// Has, DeleteBlock, PutMany, the slot methods, GetConfig / GetDataNodeState, the
+// heartbeat and repair loops and RepairDataNode.  Semantics follow node.go and
+// data_recovery.go line by line where they are observable:
+//   * Meta{BlockSize int32} stored as 4 bytes little-endian with every shard (node.go:48-50,367-374);
+//   * write quorum k (k+1 when k == m), read quorum k (entryQuorum, node.go:439-446);
+//   * meta quorum via reduceQuorumErrs + findMetaInQuorum, including "quorum < 2 fails"
+//     (node.go:334-355, :491-533; error.go:30-82);
+//   * Get fetches shards with cancel-others after k successes, decodes the data shards,
+//     queues a read-repair for shards that failed on online nodes (queue of 10000, drops
+//     when full) and truncates to BlockSize (node.go:220-326);
+//   * repairBlock / RepairDataNode (data_recovery.go:16-167).
+// Fan-out is sequential over in-process datanodes; the success / failure quorum rules of
+// paralleltask.Wait (parallel_task.go:59-84) decide the outcome exactly as in Go, and the
+// Get fan-out returns after the first k successes in node order.
+//
+// Additions for the GPU engine (results identical to the per-block path):
+//   * PutMany batches equal-size blocks through one rsmi_encode_batch_host call;
+//   * RepairDataNodeBatched rebuilds only the repaired node's row for many keys at once
+//     with rsmi_reconstruct_rows_batch_host.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "datanode.hpp"
+#include "erasure.hpp"
+
+namespace rsmi {
+namespace host {
+
+struct DagNodeConfig {  // dag/config/config.go:24-29
+    std::string name;
+    std::vector<std::string> nodes;
+    int data_blocks = 0;
+    int parity_blocks = 0;
+};
+
+struct Meta {
+    int32_t block_size = 0;
+};
+
+extern const char* const kErrReadQuorum;   // error.go:12
+extern const char* const kErrNodeNotFound;  // error.go:9
+
+struct StorageNode {
+    std::shared_ptr<DataNodeClient> client;
+    bool state = false;  // set by the heartbeat (node.go:127-157)
+};
+
+class DagNode {
+public:
+    static constexpr int kClusterSlots = 16384;  // slotsmgr.ClusterSlots
+    static constexpr size_t kRepairQueueCap = 10000;
+
+    // node.go:53-73 (clients replace the gRPC dial of datanode.NewClient)
+    static Status New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
+                      std::unique_ptr<DagNode>* out, int device = 0);
+    ~DagNode();
+
+    Status Put(const std::string& key, const Bytes& block);
+    Status PutMany(const std::vector<std::string>& keys, const std::vector<Bytes>& blocks);
+    Status Get(const std::string& key, Bytes* block);
+    Status GetSize(const std::string& key, int* size);
+    Status Has(const std::string& key, bool* has);
+    Status DeleteBlock(const std::string& key);
+
+    Status RepairDataNode(int from_index, int repair_index);
+    // batched: keys needing repair are grouped by (block size, survivor pattern) and rebuilt
+    // `batch` at a time on the GPU
+    Status RepairDataNodeBatched(int from_index, int repair_index, size_t batch, size_t* repaired = nullptr);
+
+    // heartbeat: one health-check round (node.go:132-144); the ticker loop is the caller's
+    void HealthCheckAll();
+    // drain queued read-repairs synchronously; returns how many ran (RunRepairTask body)
+    size_t RunRepairTasks();
+    void StartRepairWorker();  // RunRepairTask goroutine
+    void Close();
+
+    bool AddSlot(uint64_t slot);
+    bool ClearSlot(uint64_t slot);
+    bool GetSlot(uint64_t slot) const;
+    int GetNumSlots() const { return num_slots_; }
+    const DagNodeConfig& GetConfig() const { return config_; }
+    bool GetDataNodeState(int set_index) const;
+    void SetDataNodeState(int set_index, bool v) { nodes_.at(set_index).state = v; }
+    std::pair<int, int> EntryQuorum() const;  // (read, write)
+    size_t RepairQueueLen();
+
+private:
+    Status get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online);
+    Status repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,
+                        const std::vector<int>& indexes);
+    Status fetch_for_repair(const std::string& key, int repair_index, std::vector<Bytes>* shards);
+    static Bytes encode_meta(int32_t size);
+
+    DagNodeConfig config_;
+    std::vector<StorageNode> nodes_;
+    std::vector<uint8_t> slots_;
+    int num_slots_ = 0;
+    int device_ = 0;
+
+    std::mutex q_mu_;
+    std::condition_variable q_cv_;
+    std::deque<std::function<void()>> repair_queue_;
+    std::thread worker_;
+    bool stop_ = false;
+};
+
+// reduceQuorumErrs (error.go:73-82): most frequent error (ignoring errNodeNotFound /
+// errNodeAccessDenied; an empty string is nil and wins ties) if it reaches quorum.
+Status reduce_quorum_errs(const std::vector<Status>& errs, int quorum, const char* quorum_err);
+// findMetaInQuorum (node.go:491-533)
+Status find_meta_in_quorum(const std::vector<Meta>& metas, int quorum, Meta* out);
+
+}  // namespace host
+}  // namespace rsmi

@@ -1,0 +1,94 @@
+// datanode.hpp -- the datanode shard store behind a DataNodeClient interface.
+//
+// Mirrors dag/node/datanode/server.go: a shard is stored as one entry
+//   | crc (4 B LE) | meta size (4 B LE) | data size (4 B LE) | meta | data |     (server.go:40-41)
+// whose crc is CRC-16 "IBM" over every byte after the crc field (server.go:70), checked on
+// Get/GetMeta (server.go:93-97, :115-119).  The KV engine below it (badger / mutcask,
+// server.go:183-238) is out of scope; an in-memory map stands in, with badger's rule
+// that keys must be non-empty.  DataNodeClient mirrors proto.DataNodeClient
+// (dag/proto/datanode.proto:9-17) so the DagNode talks to any implementation, and an
+// in-process client can be switched offline to exercise the quorum paths.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace rsmi {
+namespace host {
+
+using Bytes = std::vector<uint8_t>;
+
+// A Go-style error value: ok() when empty.
+struct Status {
+    std::string err;
+    bool ok() const { return err.empty(); }
+    static Status Ok() { return {}; }
+    static Status Error(std::string e) { return Status{std::move(e)}; }
+};
+
+// howeyc/crc16 Checksum(data, IBMTable) as restated in SURVEY.md 8(a) a10: reflected
+// polynomial 0xA001, register complemented on entry and exit (CRC-16/USB; check value
+// 0xB4C8).  The upstream source is absent, so this variant is parity-unpinned.
+uint16_t crc16_ibm(const uint8_t* p, size_t n, uint16_t crc = 0);
+
+constexpr int kHeaderSize = 12;  // server.go:37
+
+class DataNodeClient {
+public:
+    virtual ~DataNodeClient() = default;
+    virtual Status Put(const std::string& key, const Bytes& meta, const Bytes& data) = 0;
+    virtual Status Get(const std::string& key, Bytes* meta, Bytes* data) = 0;
+    virtual Status GetMeta(const std::string& key, Bytes* meta) = 0;
+    virtual Status Delete(const std::string& key) = 0;
+    virtual Status Size(const std::string& key, int64_t* size) = 0;
+    virtual Status AllKeys(std::vector<std::string>* keys) = 0;  // AllKeysChan
+    virtual bool Healthy() = 0;                                   // grpc.health Check
+    virtual std::string Address() const = 0;
+};
+
+// server.go's `server` over an in-memory KV.
+class DataNodeServer {
+public:
+    Status Put(const std::string& key, const Bytes& meta, const Bytes& data);
+    Status Get(const std::string& key, Bytes* meta, Bytes* data);
+    Status GetMeta(const std::string& key, Bytes* meta);
+    Status Delete(const std::string& key);
+    Status Size(const std::string& key, int64_t* size);
+    Status AllKeys(std::vector<std::string>* keys);
+    // test hooks
+    bool RawEntry(const std::string& key, Bytes* entry);
+    void CorruptByte(const std::string& key, size_t offset);
+    void Wipe();
+
+private:
+    std::mutex mu_;
+    std::map<std::string, Bytes> kv_;
+};
+
+// An in-process client; Offline(true) makes every call fail like a dead gRPC peer.
+class InProcDataNode : public DataNodeClient {
+public:
+    explicit InProcDataNode(std::string addr) : addr_(std::move(addr)) {}
+    Status Put(const std::string& key, const Bytes& meta, const Bytes& data) override;
+    Status Get(const std::string& key, Bytes* meta, Bytes* data) override;
+    Status GetMeta(const std::string& key, Bytes* meta) override;
+    Status Delete(const std::string& key) override;
+    Status Size(const std::string& key, int64_t* size) override;
+    Status AllKeys(std::vector<std::string>* keys) override;
+    bool Healthy() override { return !offline_; }
+    std::string Address() const override { return addr_; }
+    void SetOffline(bool v) { offline_ = v; }
+    DataNodeServer& server() { return server_; }
+
+private:
+    Status down() const;
+    std::string addr_;
+    bool offline_ = false;
+    DataNodeServer server_;
+};
+
+}  // namespace host
+}  // namespace rsmi

@@ -1,0 +1,124 @@
+// erasure.cpp -- see erasure.hpp.
+#include "erasure.hpp"
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace rsmi {
+namespace host {
+
+Status rsmi_status(int rc) {
+    switch (rc) {
+        case RSMI_OK: return Status::Ok();
+        case RSMI_ERR_SHORT_DATA: return Status::Error("not enough data to fill the number of requested shards");
+        case RSMI_ERR_TOO_FEW_SHARDS: return Status::Error("too few shards given");
+        case RSMI_ERR_SHARD_NO_DATA: return Status::Error("no shard data");
+        case RSMI_ERR_SHARD_SIZE: return Status::Error("shard sizes do not match");
+        case RSMI_ERR_INV_SHARD_NUM:
+            return Status::Error("cannot create Encoder with less than one data shard or less than zero parity shards");
+        case RSMI_ERR_MAX_SHARD_NUM: return Status::Error("cannot create Encoder with more than 256 data+parity shards");
+        default: return Status::Error(std::string("rsmi: ") + rsmi_status_string(rc));
+    }
+}
+
+int64_t ceil_frac(int64_t numerator, int64_t denominator) {
+    if (denominator == 0) return 0;
+    if (denominator < 0) {
+        numerator = -numerator;
+        denominator = -denominator;
+    }
+    int64_t c = numerator / denominator;
+    if (numerator > 0 && numerator % denominator != 0) c++;
+    return c;
+}
+
+rsmi_ctx* shared_context(int k, int m, int device, int* rc) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int>, rsmi_ctx*> cache;  // lives for the process
+    std::lock_guard<std::mutex> g(mu);
+    auto key = std::make_tuple(k, m, device);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+        *rc = RSMI_OK;
+        return it->second;
+    }
+    rsmi_ctx* c = nullptr;
+    *rc = rsmi_open(k, m, device, &c);
+    if (*rc == RSMI_OK) cache[key] = c;
+    return c;
+}
+
+Status Erasure::New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device) {
+    if (data_blocks <= 0 || parity_blocks <= 0) return rsmi_status(RSMI_ERR_INV_SHARD_NUM);
+    if (data_blocks + parity_blocks > 256) return rsmi_status(RSMI_ERR_MAX_SHARD_NUM);
+    out->data_blocks_ = data_blocks;
+    out->parity_blocks_ = parity_blocks;
+    out->block_size_ = block_size;
+    out->device_ = device;
+    return Status::Ok();
+}
+
+Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const {
+    const int n = data_blocks_ + parity_blocks_;
+    shards->assign(size_t(n), Bytes());
+    if (data.empty()) return Status::Ok();  // erasure.go:52-54
+    int rc;
+    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    if (!c) return rsmi_status(rc);
+    const size_t S = rsmi_shard_size(data.size(), data_blocks_);
+    Bytes flat(size_t(n) * S);
+    rc = rsmi_encode_block(c, data.data(), data.size(), flat.data());
+    if (rc) return rsmi_status(rc);
+    for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    return Status::Ok();
+}
+
+Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
+    const int n = data_blocks_ + parity_blocks_;
+    if (int(shards.size()) != n) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);
+    std::vector<size_t> lens(static_cast<size_t>(n));
+    std::vector<uint8_t> present(static_cast<size_t>(n));
+    for (int i = 0; i < n; i++) {
+        lens[i] = shards[i].size();
+        present[i] = shards[i].empty() ? 0 : 1;
+    }
+    size_t S = 0;
+    int rc = rsmi_check_shards(n, lens.data(), 1, &S);
+    if (rc) return rsmi_status(rc);
+    int np = 0, dp = 0;
+    for (int i = 0; i < n; i++)
+        if (present[i]) {
+            np++;
+            if (i < data_blocks_) dp++;
+        }
+    if (np == n || (data_only && dp == data_blocks_)) return Status::Ok();
+    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    if (!c) return rsmi_status(rc);
+    Bytes flat(size_t(n) * S);  // [][]byte -> one contiguous buffer for the C-ABI
+    for (int i = 0; i < n; i++)
+        if (present[i]) std::memcpy(flat.data() + size_t(i) * S, shards[i].data(), S);
+    rc = rsmi_reconstruct(c, flat.data(), S, present.data(), data_only ? 1 : 0);
+    if (rc) return rsmi_status(rc);
+    for (int i = 0; i < n; i++)
+        if (!present[i] && (i < data_blocks_ || !data_only))
+            shards[i].assign(flat.begin() + size_t(i) * S, flat.begin() + size_t(i + 1) * S);
+    return Status::Ok();
+}
+
+Status Erasure::DecodeDataBlocks(std::vector<Bytes>& shards) const {
+    size_t is_zero = 0;
+    for (auto& b : shards)
+        if (b.empty()) {
+            is_zero++;
+            break;  // erasure.go:72-77: counts at most one
+        }
+    if (is_zero == 0 || is_zero == shards.size()) return Status::Ok();
+    return reconstruct(shards, true);
+}
+
+Status Erasure::DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const { return reconstruct(shards, false); }
+
+}  // namespace host
+}  // namespace rsmi

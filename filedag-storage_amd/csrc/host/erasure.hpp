@@ -1,0 +1,45 @@
+// erasure.hpp -- C++ mirror of dag/node/dagnode/erasure.go over the rsmi C-ABI.
+//
+// Same method set and semantics as the Go type: NewErasure validation (erasure.go:16-24),
+// EncodeData = Split + Encode with the empty-block short-circuit (:51-65),
+// DecodeDataBlocks with the isZero/break quirk (:70-83), DecodeDataAndParityBlocks
+// (:87-93), ShardSize = ceilFrac(B, k) (:96-98).  A shard is a byte vector; an empty
+// vector is a missing shard (Go: nil / zero-length slice).  Every coded byte comes from
+// the gfx950 kernels behind include/rsmi.h; there is no CPU fallback.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../../include/rsmi.h"
+#include "datanode.hpp"
+
+namespace rsmi {
+namespace host {
+
+// upstream sentinel texts (reedsolomon.Err*), so callers can match on them
+Status rsmi_status(int rc);
+int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
+
+// Process-wide context per (k, m, device): NewErasure runs per block in the reference
+// (node.go:277,376) but the matrix / device plans are built once.
+rsmi_ctx* shared_context(int k, int m, int device, int* rc);
+
+class Erasure {
+public:
+    static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);
+    Status EncodeData(const Bytes& data, std::vector<Bytes>* shards) const;
+    Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
+    Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;
+    int64_t ShardSize() const { return ceil_frac(block_size_, data_blocks_); }
+    int data_blocks() const { return data_blocks_; }
+    int parity_blocks() const { return parity_blocks_; }
+
+private:
+    Status reconstruct(std::vector<Bytes>& shards, bool data_only) const;
+    int data_blocks_ = 0, parity_blocks_ = 0, device_ = 0;
+    int64_t block_size_ = 0;
+};
+
+}  // namespace host
+}  // namespace rsmi

@@ -174,9 +174,10 @@ int decode_rows(const rsmi_ctx* c, const uint8_t* present, Matrix& dec, std::vec
     return RSMI_OK;
 }
 
-int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, int data_only, std::shared_ptr<Plan>& out) {
-    std::string key = data_only ? "D" : "R";
-    for (int i = 0; i < c->n; i++) key.push_back(present[i] ? '1' : '0');
+// want[i]: rebuild row i (only rows that are missing are ever written)
+int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, const uint8_t* want, std::shared_ptr<Plan>& out) {
+    std::string key = "R";
+    for (int i = 0; i < c->n; i++) key.push_back(char('0' + (present[i] ? 1 : 0) + (want[i] ? 2 : 0)));
     auto it = c->plans.find(key);
     if (it != c->plans.end()) {
         out = it->second;
@@ -189,25 +190,30 @@ int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, int data_only, std::sh
     std::vector<int> out_rows;
     std::vector<uint8_t> rows;
     for (int i = 0; i < c->k; i++)
-        if (!present[i]) {
+        if (!present[i] && want[i]) {
             out_rows.push_back(i);
             rows.insert(rows.end(), dec.row(i), dec.row(i) + c->k);
         }
-    if (!data_only) {
-        for (int i = c->k; i < c->n; i++)
-            if (!present[i]) {
-                Matrix r(1, c->k);
-                std::memcpy(r.v.data(), c->M.row(i), size_t(c->k));
-                Matrix p = mat_mul(r, dec);
-                out_rows.push_back(i);
-                rows.insert(rows.end(), p.v.begin(), p.v.end());
-            }
-    }
+    for (int i = c->k; i < c->n; i++)
+        if (!present[i] && want[i]) {
+            Matrix r(1, c->k);
+            std::memcpy(r.v.data(), c->M.row(i), size_t(c->k));
+            Matrix p = mat_mul(r, dec);
+            out_rows.push_back(i);
+            rows.insert(rows.end(), p.v.begin(), p.v.end());
+        }
     Matrix coef(int(out_rows.size()), c->k);
     std::memcpy(coef.v.data(), rows.data(), rows.size());
     rc = make_plan(c, coef, used, out_rows, out);
     if (rc == RSMI_OK) c->plans[key] = out;
     return rc;
+}
+
+// want mask of upstream ReconstructData (missing data rows) / Reconstruct (all missing)
+std::vector<uint8_t> want_mask(const rsmi_ctx* c, const uint8_t* present, int data_only) {
+    std::vector<uint8_t> w(size_t(c->n), 0);
+    for (int i = 0; i < c->n; i++) w[i] = !present[i] && (i < c->k || !data_only);
+    return w;
 }
 
 const char* kernel_label(int K, int MT, int D, int NT, bool fast) {
@@ -297,12 +303,15 @@ int count_present(const rsmi_ctx* c, const uint8_t* present, int& np, int& dp) {
     return RSMI_OK;
 }
 
-// quick-return / too-few checks shared by every reconstruct entry point
-// returns 1 when there is nothing to do, 0 when work is needed, or an error
-int reconstruct_precheck(const rsmi_ctx* c, const uint8_t* present, int data_only) {
+// quick-return / too-few checks shared by every reconstruct entry point (upstream
+// reconstruct(): nothing requested missing -> no-op, then fewer than k present -> error).
+// returns 1 when there is nothing to do, 0 when work is needed, or -error
+int reconstruct_precheck(const rsmi_ctx* c, const uint8_t* present, const uint8_t* want) {
     int np, dp;
     count_present(c, present, np, dp);
-    if (np == c->n || (data_only && dp == c->k)) return 1;
+    bool any = false;
+    for (int i = 0; i < c->n; i++) any |= !present[i] && want[i];
+    if (!any) return 1;
     if (np < c->k) return -RSMI_ERR_TOO_FEW_SHARDS;
     return 0;
 }
@@ -478,12 +487,12 @@ int rsmi_encode_batch_dev(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_
     }
 }
 
-int rsmi_reconstruct_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride, size_t S,
-                               size_t nblocks, const uint8_t* present, int data_only, void* stream) {
-    if (!c || !d_shards || !present) return RSMI_ERR_INVALID_ARG;
+static int reconstruct_dev_impl(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride, size_t S,
+                                size_t nblocks, const uint8_t* present, const uint8_t* want, void* stream) {
+    if (!c || !d_shards || !present || !want) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (shard_stride < S) return RSMI_ERR_INVALID_ARG;
-    int pre = reconstruct_precheck(c, present, data_only);
+    int pre = reconstruct_precheck(c, present, want);
     if (pre < 0) return -pre;
     if (pre == 1) return RSMI_OK;
     std::shared_ptr<Plan> plan;
@@ -491,10 +500,23 @@ int rsmi_reconstruct_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stri
     int rc = ensure_device(c);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    rc = reconstruct_plan(c, present, data_only, plan);
+    rc = reconstruct_plan(c, present, want, plan);
     if (rc) return rc;
     return launch_plan(c, *plan, d_shards, shard_stride, block_stride, d_shards, shard_stride, block_stride, S, nblocks,
                        static_cast<hipStream_t>(stream));
+}
+
+int rsmi_reconstruct_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride, size_t S,
+                               size_t nblocks, const uint8_t* present, int data_only, void* stream) {
+    if (!c || !present) return RSMI_ERR_INVALID_ARG;
+    const std::vector<uint8_t> w = want_mask(c, present, data_only);
+    return reconstruct_dev_impl(c, d_shards, shard_stride, block_stride, S, nblocks, present, w.data(), stream);
+}
+
+int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride,
+                                    size_t S, size_t nblocks, const uint8_t* present, const uint8_t* required,
+                                    void* stream) {
+    return reconstruct_dev_impl(c, d_shards, shard_stride, block_stride, S, nblocks, present, required, stream);
 }
 
 // ---------------------------------------------------------------- host memory, one block
@@ -614,12 +636,12 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
     return RSMI_OK;
 }
 
-int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                const uint8_t* present, int data_only) {
-    if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
+static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                 const uint8_t* present, const uint8_t* want) {
+    if (!c || !shards || !present || !want) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (block_stride < size_t(c->n) * S) return RSMI_ERR_INVALID_ARG;
-    int pre = reconstruct_precheck(c, present, data_only);
+    int pre = reconstruct_precheck(c, present, want);
     if (pre < 0) return -pre;
     if (pre == 1 || nblocks == 0) return RSMI_OK;
     std::lock_guard<std::mutex> g(c->mu);
@@ -627,14 +649,14 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_strid
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
     std::shared_ptr<Plan> plan;
-    rc = reconstruct_plan(c, present, data_only, plan);
+    rc = reconstruct_plan(c, present, want, plan);
     if (rc) return rc;
     // rows to ship: the k survivors in; the missing rows the plan writes, out
     std::vector<int> in_rows, out_rows;
     for (int i = 0; i < c->n && int(in_rows.size()) < c->k; i++)
         if (present[i]) in_rows.push_back(i);
     for (int i = 0; i < c->n; i++)
-        if (!present[i] && (i < c->k || !data_only)) out_rows.push_back(i);
+        if (!present[i] && want[i]) out_rows.push_back(i);
     const size_t n = size_t(c->n), nr = out_rows.size();
     const size_t Sp = rsmi_recommended_pitch(S);
     const size_t bs = n * Sp;
@@ -697,6 +719,18 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_strid
         }
     }
     return RSMI_OK;
+}
+
+int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                const uint8_t* present, int data_only) {
+    if (!c || !present) return RSMI_ERR_INVALID_ARG;
+    const std::vector<uint8_t> w = want_mask(c, present, data_only);
+    return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, w.data());
+}
+
+int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                     const uint8_t* present, const uint8_t* required) {
+    return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required);
 }
 
 }  // extern "C"

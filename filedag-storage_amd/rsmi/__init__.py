@@ -73,6 +73,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_reconstruct": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_int]),
         "rsmi_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
         "rsmi_reconstruct_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p, ctypes.c_int]),
+        "rsmi_reconstruct_rows_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p, u8p]),
+        "rsmi_reconstruct_rows_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, u8p, ctypes.c_void_p]),
         "rsmi_host_alloc": (ctypes.c_void_p, [c_size]),
         "rsmi_host_free": (None, [ctypes.c_void_p]),
         "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
@@ -188,11 +190,25 @@ class Codec:
         _check(lib().rsmi_reconstruct_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                  1 if data_only else 0))
 
+    def reconstruct_rows_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
+                                        required: Sequence[bool]) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        q = bytearray(1 if x else 0 for x in required)
+        _check(lib().rsmi_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                      ctypes.addressof(_buf(q))))
+
     # -- device memory (raw pointers, e.g. torch tensor.data_ptr()); stream = hipStream_t
     def encode_batch_dev(self, d_data: int, data_rs: int, data_bs: int, d_parity: int, parity_rs: int,
                          parity_bs: int, S: int, nblocks: int, stream: int = 0) -> None:
         _check(lib().rsmi_encode_batch_dev(self._h, d_data, data_rs, data_bs, d_parity, parity_rs, parity_bs, S,
                                            nblocks, stream or None))
+
+    def reconstruct_rows_batch_dev(self, d_shards: int, rs: int, bs: int, S: int, nblocks: int,
+                                   present: Sequence[bool], required: Sequence[bool], stream: int = 0) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        q = bytearray(1 if x else 0 for x in required)
+        _check(lib().rsmi_reconstruct_rows_batch_dev(self._h, d_shards, rs, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                     ctypes.addressof(_buf(q)), stream or None))
 
     def reconstruct_batch_dev(self, d_shards: int, rs: int, bs: int, S: int, nblocks: int,
                               present: Sequence[bool], data_only: bool, stream: int = 0) -> None:

@@ -109,6 +109,12 @@ int rsmi_encode_batch_host(rsmi_ctx* ctx, const uint8_t* data, size_t data_block
 int rsmi_reconstruct_batch_host(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                 const uint8_t* present, int data_only);
 
+/* Rebuild only the rows flagged in required[] (n flags; rows that are present are left
+ * alone) -- RepairDataNode needs one row per key (data_recovery.go:88,102-106), not every
+ * missing one.  Same layout and errors as rsmi_reconstruct_batch_host. */
+int rsmi_reconstruct_rows_batch_host(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                     const uint8_t* present, const uint8_t* required);
+
 void* rsmi_host_alloc(size_t bytes);
 void rsmi_host_free(void* p);
 
@@ -128,6 +134,11 @@ int rsmi_encode_batch_dev(rsmi_ctx* ctx, const uint8_t* d_data, size_t data_shar
  * block b at d_shards + b*block_stride + i*shard_stride. */
 int rsmi_reconstruct_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t shard_stride, size_t block_stride,
                                size_t S, size_t nblocks, const uint8_t* present, int data_only, void* stream);
+
+/* Device-resident form of rsmi_reconstruct_rows_batch_host. */
+int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t shard_stride, size_t block_stride,
+                                    size_t S, size_t nblocks, const uint8_t* present, const uint8_t* required,
+                                    void* stream);
 
 /* ------------------------------------------------------------------ tuning / introspection */
 

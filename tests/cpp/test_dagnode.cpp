@@ -1,0 +1,356 @@
+// test_dagnode.cpp -- the Dag Node / datanode host mirror, in the shape of the reference's
+// own Go tests (dag/node/dagnode/node_test.go, dag/node/datanode/server_test.go).
+//
+//   test_dagnode cpu   datanode framing/CRC, quorum helpers, slots, config checks (no GPU)
+//   test_dagnode gpu   TestDagNode "123456" round trip, RS(10,4) failure/quorum matrix,
+//                      read-repair, RepairDataNode (per key and batched), PutMany batch;
+//                      every stored shard is compared with the CPU oracle (test-only).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../filedag-storage_amd/csrc/host/dagnode.hpp"
+#include "../../oracle/rs_oracle.h"
+
+using namespace rsmi::host;
+
+static int g_fail = 0, g_checks = 0;
+#define CHECK(cond)                                                                  \
+    do {                                                                             \
+        g_checks++;                                                                  \
+        if (!(cond)) {                                                               \
+            g_fail++;                                                                \
+            std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+        }                                                                            \
+    } while (0)
+#define CHECK_OK(st)                                                                              \
+    do {                                                                                          \
+        Status _s = (st);                                                                         \
+        g_checks++;                                                                               \
+        if (!_s.ok()) {                                                                           \
+            g_fail++;                                                                             \
+            std::fprintf(stderr, "%s:%d: unexpected error: %s\n", __FILE__, __LINE__, _s.err.c_str()); \
+        }                                                                                         \
+    } while (0)
+
+static Bytes str(const char* s) { return Bytes(s, s + std::strlen(s)); }
+
+static Bytes rand_bytes(std::mt19937_64& r, size_t n) {
+    Bytes b(n);
+    for (auto& x : b) x = uint8_t(r());
+    return b;
+}
+
+struct Cluster {
+    std::vector<std::shared_ptr<InProcDataNode>> dn;
+    std::unique_ptr<DagNode> node;
+    Cluster(int k, int m) {
+        DagNodeConfig cfg;
+        cfg.name = "dag_node1";
+        cfg.data_blocks = k;
+        cfg.parity_blocks = m;
+        std::vector<std::shared_ptr<DataNodeClient>> clients;
+        for (int i = 0; i < k + m; i++) {
+            cfg.nodes.push_back("127.0.0.1:" + std::to_string(9011 + i));
+            dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back()));
+            clients.push_back(dn.back());
+        }
+        Status s = DagNode::New(cfg, clients, &node);
+        if (!s.ok()) {
+            std::fprintf(stderr, "NewDagNode: %s\n", s.err.c_str());
+            std::exit(2);
+        }
+        node->HealthCheckAll();
+    }
+};
+
+// oracle shards of a block: (k+m) rows of S bytes
+static std::vector<Bytes> oracle_shards(int k, int m, const Bytes& block) {
+    const size_t S = rs_oracle_shard_size(block.size(), k);
+    Bytes flat(size_t(k + m) * S);
+    rs_oracle_split(k, m, block.data(), block.size(), flat.data());
+    rs_oracle_encode(k, m, flat.data(), S);
+    std::vector<Bytes> out;
+    for (int i = 0; i < k + m; i++) out.emplace_back(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    return out;
+}
+
+static Bytes stored_shard(InProcDataNode& d, const std::string& key) {
+    Bytes meta, data;
+    if (!d.server().Get(key, &meta, &data).ok()) return Bytes();
+    return data;
+}
+
+// ------------------------------------------------------------------ CPU-only tests
+static void test_datanode_server() {
+    DataNodeServer s;
+    // server_test.go:14-22 (badger): empty key rejected
+    CHECK(!s.Put("", Bytes(), str("123")).ok());
+    CHECK_OK(s.Put("1234567", Bytes(), str("\b\x02\x12\a1234567\x18\a")));
+    CHECK_OK(s.Put("@#", Bytes(), str("@#$$&*^@*")));
+    Bytes meta = {6, 0, 0, 0}, data = str("123456"), m2, d2;
+    CHECK_OK(s.Put("key", meta, data));
+    CHECK_OK(s.Get("key", &m2, &d2));
+    CHECK(m2 == meta && d2 == data);
+    int64_t sz = 0;
+    CHECK_OK(s.Size("key", &sz));
+    CHECK(sz == kHeaderSize + 4 + 6);  // HeaderSize + len(meta) + len(data) (server_test.go:147-152)
+    Bytes e;
+    CHECK(s.RawEntry("key", &e));
+    // | crc | metaSize | dataSize | meta | data |, crc over bytes [4:], little endian
+    CHECK(e.size() == 22 && e[4] == 4 && e[8] == 6);
+    const uint16_t crc = crc16_ibm(e.data() + 4, e.size() - 4);
+    CHECK(e[0] == (crc & 0xFF) && e[1] == (crc >> 8) && e[2] == 0 && e[3] == 0);
+    // corruption is caught by the crc check on Get and GetMeta (server.go:93-97)
+    s.CorruptByte("key", 15);
+    Status g = s.Get("key", &m2, &d2);
+    CHECK(!g.ok() && g.err == "checking crc failed");
+    CHECK(!s.GetMeta("key", &m2).ok());
+    CHECK_OK(s.Delete("key"));
+    CHECK(!s.Get("key", &m2, &d2).ok());
+    CHECK(!s.Size("key", &sz).ok());
+    std::vector<std::string> keys;
+    CHECK_OK(s.AllKeys(&keys));
+    CHECK(keys.size() == 2);
+    // CRC-16/USB check value of the restated IBM-table variant
+    const char* cv = "123456789";
+    CHECK(crc16_ibm(reinterpret_cast<const uint8_t*>(cv), 9) == 0xB4C8);
+}
+
+static void test_quorum_helpers() {
+    // reduceQuorumErrs
+    std::vector<Status> errs = {Status(), Status(), Status::Error("x"), Status::Error(kErrNodeNotFound)};
+    CHECK(reduce_quorum_errs(errs, 2, kErrReadQuorum).ok());
+    CHECK(reduce_quorum_errs(errs, 3, kErrReadQuorum).err == kErrReadQuorum);
+    errs = {Status::Error("Key not found"), Status::Error("Key not found"), Status::Error("Key not found")};
+    CHECK(reduce_quorum_errs(errs, 2, kErrReadQuorum).err == "Key not found");
+    errs = {Status::Error("a"), Status(), Status::Error("a"), Status()};
+    CHECK(reduce_quorum_errs(errs, 2, kErrReadQuorum).ok());  // nil wins ties
+    // findMetaInQuorum
+    Meta out;
+    CHECK(find_meta_in_quorum({{6}, {6}, {6}}, 1, &out).err == kErrReadQuorum);  // quorum < 2 fails
+    CHECK(find_meta_in_quorum({{6}, {6}, {0}}, 2, &out).ok() && out.block_size == 6);
+    CHECK(!find_meta_in_quorum({{6}, {7}, {0}}, 2, &out).ok());
+}
+
+static void test_config_and_slots() {
+    DagNodeConfig cfg;
+    cfg.data_blocks = 2;
+    cfg.parity_blocks = 1;
+    cfg.nodes = {"a", "b"};
+    std::unique_ptr<DagNode> d;
+    std::vector<std::shared_ptr<DataNodeClient>> c = {std::make_shared<InProcDataNode>("a"),
+                                                      std::make_shared<InProcDataNode>("b")};
+    CHECK(DagNode::New(cfg, c, &d).err == "dag node config is incorrect");  // node.go:55-57
+    cfg.nodes.push_back("c");
+    c.push_back(std::make_shared<InProcDataNode>("c"));
+    CHECK_OK(DagNode::New(cfg, c, &d));
+    CHECK(d->EntryQuorum() == std::make_pair(2, 2));
+    CHECK(d->AddSlot(5) == false && d->AddSlot(5) == true && d->GetNumSlots() == 1);
+    CHECK(d->GetSlot(5) && !d->GetSlot(6));
+    CHECK(d->ClearSlot(5) == true && d->GetNumSlots() == 0);
+    CHECK(!d->GetDataNodeState(0));
+    d->HealthCheckAll();
+    CHECK(d->GetDataNodeState(0));
+    cfg.data_blocks = cfg.parity_blocks = 2;
+    cfg.nodes.push_back("d");
+    c.push_back(std::make_shared<InProcDataNode>("d"));
+    CHECK_OK(DagNode::New(cfg, c, &d));
+    CHECK(d->EntryQuorum() == std::make_pair(2, 3));  // k == m -> write quorum k+1
+    // Get of an absent key on a healthy cluster surfaces the KV's error
+    Bytes b;
+    Status s = d->Get("nope", &b);
+    CHECK(!s.ok() && s.err == "Key not found");
+}
+
+// ------------------------------------------------------------------ GPU tests
+static void test_dagnode_123456() {  // node_test.go:18-65, RS(2,1) over 3 datanodes
+    Cluster c(2, 1);
+    const Bytes block = str("123456");
+    CHECK_OK(c.node->Put("QmTestBlock", block));
+    Bytes got;
+    CHECK_OK(c.node->Get("QmTestBlock", &got));
+    CHECK(got == block);
+    int size = 0;
+    CHECK_OK(c.node->GetSize("QmTestBlock", &size));
+    CHECK(size == 6);
+    // the shards on the datanodes: "123", "456", parity 3b 3c 39
+    CHECK(stored_shard(*c.dn[0], "QmTestBlock") == str("123"));
+    CHECK(stored_shard(*c.dn[1], "QmTestBlock") == str("456"));
+    CHECK((stored_shard(*c.dn[2], "QmTestBlock") == Bytes{0x3b, 0x3c, 0x39}));
+    int64_t sz;
+    CHECK_OK(c.dn[0]->Size("QmTestBlock", &sz));
+    CHECK(sz == kHeaderSize + 4 + 3);
+    // any single datanode down: still readable (read quorum 2), reconstruct on the GPU
+    for (int down = 0; down < 3; down++) {
+        c.dn[down]->SetOffline(true);
+        got.clear();
+        CHECK_OK(c.node->Get("QmTestBlock", &got));
+        CHECK(got == block);
+        c.dn[down]->SetOffline(false);
+    }
+    CHECK_OK(c.node->DeleteBlock("QmTestBlock"));
+    bool has = true;
+    c.node->Has("QmTestBlock", &has);
+    CHECK(!has);
+}
+
+static void test_rs10_4_failures() {
+    const int k = 10, m = 4, n = k + m;
+    Cluster c(k, m);
+    std::mt19937_64 r(0xF11EDA6);
+    const size_t sizes[] = {1, 6, 9, 10, 11, 4099, 65536, 262143, 262144, 262145, 1048590};
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) {
+        keys.push_back("bafy-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, sizes[i]));
+        CHECK_OK(c.node->Put(keys.back(), blocks.back()));
+        // every stored shard equals the oracle's
+        auto want = oracle_shards(k, m, blocks.back());
+        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], keys.back()) == want[j]);
+    }
+    // up to m datanodes down: every block still reads back
+    const int downs[][4] = {{0, -1, -1, -1}, {0, 1, 2, 3}, {10, 11, 12, 13}, {0, 5, 11, 13}, {9, 3, 12, -1}};
+    for (auto& d : downs) {
+        for (int x : d)
+            if (x >= 0) c.dn[x]->SetOffline(true);
+        for (size_t i = 0; i < keys.size(); i++) {
+            Bytes got;
+            CHECK_OK(c.node->Get(keys[i], &got));
+            CHECK(got == blocks[i]);
+        }
+        for (int x : d)
+            if (x >= 0) c.dn[x]->SetOffline(false);
+    }
+    // m+1 down: read quorum lost
+    for (int x = 0; x < m + 1; x++) c.dn[x]->SetOffline(true);
+    Bytes got;
+    CHECK(!c.node->Get(keys[0], &got).ok());
+    // write quorum is k: with m+1 down a Put fails, with m down it succeeds
+    CHECK(!c.node->Put("w1", blocks[3]).ok());
+    c.dn[m]->SetOffline(false);
+    CHECK_OK(c.node->Put("w2", blocks[3]));
+    for (int x = 0; x < m; x++) c.dn[x]->SetOffline(false);
+    CHECK_OK(c.node->Get("w2", &got));
+    CHECK(got == blocks[3]);
+}
+
+static void test_read_repair() {
+    const int k = 10, m = 4;
+    Cluster c(k, m);
+    std::mt19937_64 r(7);
+    const Bytes block = rand_bytes(r, 262144);
+    CHECK_OK(c.node->Put("blk", block));
+    auto want = oracle_shards(k, m, block);
+    // a datanode loses two shards of the block (data 3 and parity 12)
+    c.dn[3]->server().Delete("blk");
+    c.dn[12]->server().Delete("blk");
+    Bytes got;
+    CHECK_OK(c.node->Get("blk", &got));
+    CHECK(got == block);
+    CHECK(c.node->RepairQueueLen() == 1);  // node.go:289-308
+    CHECK(c.node->RunRepairTasks() == 1);
+    CHECK(stored_shard(*c.dn[3], "blk") == want[3]);
+    CHECK(stored_shard(*c.dn[12], "blk") == want[12]);
+    // a corrupted shard fails its CRC, is treated as a failed read and repaired
+    c.dn[5]->server().CorruptByte("blk", 100);
+    CHECK_OK(c.node->Get("blk", &got));
+    CHECK(got == block);
+    CHECK(c.node->RunRepairTasks() == 1);
+    CHECK(stored_shard(*c.dn[5], "blk") == want[5]);
+    // background worker variant
+    c.dn[0]->server().Delete("blk");
+    c.node->StartRepairWorker();
+    CHECK_OK(c.node->Get("blk", &got));
+    for (int i = 0; i < 200 && stored_shard(*c.dn[0], "blk").empty(); i++) {
+        struct timespec ts = {0, 10 * 1000 * 1000};
+        nanosleep(&ts, nullptr);
+    }
+    CHECK(stored_shard(*c.dn[0], "blk") == want[0]);
+    c.node->Close();
+}
+
+static void test_repair_datanode(bool batched) {
+    const int k = 10, m = 4, n = k + m;
+    Cluster c(k, m);
+    std::mt19937_64 r(batched ? 11 : 13);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < 40; i++) {
+        keys.push_back("key-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, i % 3 == 0 ? 262144 : (i % 3 == 1 ? 1000 + i : 65536)));
+        CHECK_OK(c.node->Put(keys.back(), blocks.back()));
+    }
+    // datanode 6 is replaced by an empty one; one more node is down during the repair
+    c.dn[6]->server().Wipe();
+    c.dn[2]->SetOffline(true);
+    size_t repaired = 0;
+    if (batched)
+        CHECK_OK(c.node->RepairDataNodeBatched(0, 6, 16, &repaired));
+    else
+        CHECK_OK(c.node->RepairDataNode(0, 6));
+    if (batched) CHECK(repaired == keys.size());
+    c.dn[2]->SetOffline(false);
+    for (size_t i = 0; i < keys.size(); i++) {
+        auto want = oracle_shards(k, m, blocks[i]);
+        CHECK(stored_shard(*c.dn[6], keys[i]) == want[6]);
+    }
+    // bad indexes (data_recovery.go:17-22)
+    CHECK(c.node->RepairDataNode(n, 0).err == "index greater than max index of nodes");
+    CHECK(c.node->RepairDataNode(0, n).err == "repair index greater than max index of nodes");
+}
+
+static void test_putmany_batch() {
+    const int k = 4, m = 2;
+    Cluster c(k, m);
+    std::mt19937_64 r(5);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < 64; i++) {
+        keys.push_back("pm-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, i % 2 ? 262144 : 4097));
+    }
+    blocks[7].clear();  // an empty block travels the per-block path
+    CHECK_OK(c.node->PutMany(keys, blocks));
+    for (size_t i = 0; i < keys.size(); i++) {
+        if (blocks[i].empty()) continue;
+        auto want = oracle_shards(k, m, blocks[i]);
+        for (int j = 0; j < k + m; j++) CHECK(stored_shard(*c.dn[j], keys[i]) == want[j]);
+        Bytes got;
+        CHECK_OK(c.node->Get(keys[i], &got));
+        CHECK(got == blocks[i]);
+    }
+    // empty block: Put succeeds, Get fails with ErrShardNoData
+    Bytes got;
+    Status s = c.node->Get(keys[7], &got);
+    CHECK(!s.ok() && s.err == "no shard data");
+    int size = -1;
+    CHECK_OK(c.node->GetSize(keys[7], &size));
+    CHECK(size == 0);
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (rs_oracle_selftest() != 0) {
+        std::fprintf(stderr, "oracle selftest failed\n");
+        return 2;
+    }
+    test_datanode_server();
+    test_quorum_helpers();
+    test_config_and_slots();
+    if (mode == "gpu") {
+        test_dagnode_123456();
+        test_rs10_4_failures();
+        test_read_repair();
+        test_repair_datanode(false);
+        test_repair_datanode(true);
+        test_putmany_batch();
+    }
+    std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
+    return g_fail ? 1 : 0;
+}
