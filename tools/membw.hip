@@ -56,7 +56,69 @@ __global__ __launch_bounds__(256) void membw_rows(const uint8_t* __restrict__ in
     }
 }
 
+// Tile-shape / order study: W chunks of 16 B per lane per row; ORDER 0 = block-major
+// tiles (rs_fast_kernel), 1 = tile-major (consecutive waves on different blocks, same
+// offset), 2 = block-major with XCD-grouped wave ids (each XCD label walks its own range).
+template <int K, int M, int W, int ORDER>
+__global__ __launch_bounds__(256) void membw_rows2(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                   uint32_t tpb, uint32_t ntiles, uint32_t nblocks) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    uint32_t wg = blockIdx.x;
+    if (ORDER == 2) wg = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+    for (uint32_t t = wg * 4 + wid; t < ntiles; t += nw) {
+        uint32_t blk, tib;
+        if (ORDER == 1) {
+            tib = t / nblocks;
+            blk = t - tib * nblocks;
+        } else {
+            blk = t / tpb;
+            tib = t - blk * tpb;
+        }
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        u32x4 acc[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) acc[w] = u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++)
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                uint32_t ch = tib * 64 * W + 64 * w + lane;
+                ch = ch < cpb ? ch : cpb - 1;
+                acc[w] ^= ld<true>(reinterpret_cast<const u32x4*>(ib + c * rs) + ch);
+            }
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const uint32_t ch = tib * 64 * W + 64 * w + lane;
+            if (ch < cpb) {
+#pragma unroll
+                for (int j = 0; j < M; j++) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc[w] + j);
+            }
+        }
+    }
+}
+
 extern "C" {
+int membw_rows2_launch(int K, int M, int W, int ORDER, const void* in, void* out, uint64_t in_bs, uint64_t rs,
+                       uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 64 * W - 1) / (64 * W);
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+    const uint32_t nb = uint32_t(nblocks);
+#define R2(k, m, w, ord) \
+    if (K == k && M == m && W == w && ORDER == ord) membw_rows2<k, m, w, ord><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles, nb); else
+#define R2O(k, m, w) R2(k, m, w, 0) R2(k, m, w, 1) R2(k, m, w, 2)
+    R2O(10, 4, 1) R2O(10, 4, 2) R2O(10, 4, 4) R2O(10, 1, 1) R2O(10, 1, 2) R2O(10, 1, 4) return -1;
+#undef R2O
+#undef R2
+    return hipGetLastError();
+}
+
 int membw_copy_launch(int U, int NT, const void* in, void* out, uint64_t bytes, int grid, void* stream) {
     auto st = (hipStream_t)stream;
     const u32x4* i = (const u32x4*)in;

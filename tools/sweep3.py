@@ -32,8 +32,10 @@ def main():
     V = {}
     V["xor10x4"] = (lambda: L.membw_rows_launch(10, 4, 1, b, b + 10 * p, n * p, p, n * p, S, nb, 2048, sh), enc)
     V["xor10x1"] = (lambda: L.membw_rows_launch(10, 1, 1, b + p, b, n * p, p, n * p, S, nb, 2048, sh), rec)
-    for pf in (0, 4, 8, 10, 106, 110):
-        for wpc in (0, 12, 16, 24):
+    pfs = [int(x) for x in os.environ.get("PFS", "0,4,8,10,106,110").split(",")]
+    wpcs = [int(x) for x in os.environ.get("WPCS", "0,12,16,24").split(",")]
+    for pf in pfs:
+        for wpc in wpcs:
             def fe(pf=pf, wpc=wpc):
                 c.set_option("prefetch", pf)
                 c.set_option("waves_per_cu", wpc)
