@@ -271,63 +271,149 @@ Status DagNode::DeleteBlock(const std::string& key) {  // node.go:191-208
 }
 
 // ------------------------------------------------------------------ read path
-Status DagNode::Get(const std::string& key, Bytes* block) {  // node.go:220-326
-    Meta meta;
+Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:220-275
     std::vector<StorageNode*> online;
-    Status s = get_meta_info(key, &meta, &online);
+    Status s = get_meta_info(key, &f->meta, &online);
     if (!s.ok()) return s;
     const int n = int(nodes_.size()), rq = EntryQuorum().first;
-    std::vector<Bytes> shards(static_cast<size_t>(n));
-    std::vector<bool> repair(size_t(n), false);
-    bool need_repair = false;
+    f->shards.assign(static_cast<size_t>(n), Bytes());
+    f->repair.clear();
     QuorumWait w(rq, n - rq + 1);
     for (int i = 0; i < n; i++) {
         if (!online[i]) {
             // runs even after the quorum is met: the goroutine returns before its first RPC
-            if (nodes_[i].state) {
-                repair[i] = true;
-                need_repair = true;
-            }
+            if (nodes_[i].state) f->repair.push_back(i);
             w.add(Status::Error("offline node"));
             continue;
         }
         if (w.decided()) continue;  // cancelOther: later fetches are cancelled, no repair
         Bytes m, data;
         Status g = online[i]->client->Get(key, &m, &data);
-        if (!g.ok()) {
-            repair[i] = true;  // any non-cancel error (node.go:254-258)
-            need_repair = true;
-        } else {
-            shards[i] = std::move(data);
-        }
+        if (!g.ok())
+            f->repair.push_back(i);  // any non-cancel error (node.go:254-258)
+        else
+            f->shards[i] = std::move(data);
         w.add(g);
     }
-    s = w.result(kErrReadQuorum);
-    if (!s.ok()) return s;
+    std::sort(f->repair.begin(), f->repair.end());
+    return w.result(kErrReadQuorum);
+}
 
+Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  // node.go:277-326
     Erasure enc;
-    s = Erasure::New(config_.data_blocks, config_.parity_blocks, meta.block_size, &enc, device_);
+    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, f.meta.block_size, &enc, device_);
     if (!s.ok()) return s;
-    s = enc.DecodeDataBlocks(shards);
+    s = enc.DecodeDataBlocks(f.shards);
     if (!s.ok()) return s;
-
-    if (need_repair) {
-        std::vector<int> idx;
-        for (int i = 0; i < n; i++)
-            if (repair[i]) idx.push_back(i);
-        const int32_t bs = meta.block_size;
+    if (!f.repair.empty()) {
+        const int32_t bs = f.meta.block_size;
         std::lock_guard<std::mutex> g(q_mu_);
-        if (repair_queue_.size() < kRepairQueueCap)  // else: "repair queue is full, discard this task"
+        if (repair_queue_.size() < kRepairQueueCap) {  // else: "repair queue is full, discard this task"
+            std::vector<Bytes> shards = f.shards;
+            std::vector<int> idx = f.repair;
             repair_queue_.push_back([this, key, bs, shards, idx]() { (void)repair_block(key, bs, shards, idx); });
+        }
         q_cv_.notify_one();
     }
-
     const size_t S = size_t(enc.ShardSize());
     block->assign(size_t(config_.data_blocks) * S, 0);
     for (int i = 0; i < config_.data_blocks; i++)
-        std::memcpy(block->data() + size_t(i) * S, shards[i].data(), std::min(S, shards[i].size()));
-    block->resize(size_t(meta.block_size));
+        std::memcpy(block->data() + size_t(i) * S, f.shards[i].data(), std::min(S, f.shards[i].size()));
+    block->resize(size_t(f.meta.block_size));
     return Status::Ok();
+}
+
+Status DagNode::Get(const std::string& key, Bytes* block) {
+    Fetched f;
+    Status s = fetch_for_get(key, &f);
+    if (!s.ok()) return s;
+    return finish_get(key, f, block);
+}
+
+void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* blocks, std::vector<Status>* statuses,
+                      size_t batch) {
+    const int k = config_.data_blocks, m = config_.parity_blocks, n = k + m;
+    if (batch == 0) batch = 1;
+    blocks->assign(keys.size(), Bytes());
+    statuses->assign(keys.size(), Status());
+    std::vector<Fetched> fs(keys.size());
+    // (block size, survivor pattern) -> indexes of keys whose data shards need decoding
+    std::map<std::pair<int32_t, std::string>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < keys.size(); i++) {
+        (*statuses)[i] = fetch_for_get(keys[i], &fs[i]);
+        if (!(*statuses)[i].ok()) continue;
+        bool data_missing = false;
+        for (int c = 0; c < k; c++) data_missing |= fs[i].shards[c].empty();
+        bool any = false;
+        for (auto& sh : fs[i].shards) any |= !sh.empty();
+        if (!data_missing || !any || fs[i].meta.block_size <= 0) continue;  // per-key path decides
+        std::string pat(static_cast<size_t>(n), '0');
+        for (int c = 0; c < n; c++) pat[c] = fs[i].shards[c].empty() ? '0' : '1';
+        groups[{fs[i].meta.block_size, pat}].push_back(i);
+    }
+    for (auto& g : groups) {
+        const size_t S = rsmi_shard_size(size_t(g.first.first), k);
+        std::vector<uint8_t> present(static_cast<size_t>(n));
+        for (int c = 0; c < n; c++) present[c] = uint8_t(g.first.second[c] == '1');
+        bool sizes_ok = true;  // every present shard must have the common size (else per-key errors)
+        for (size_t i : g.second)
+            for (int c = 0; c < n; c++) sizes_ok &= !present[c] || fs[i].shards[c].size() == S;
+        if (!sizes_ok) continue;
+        int rc;
+        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
+        if (!ctx) continue;  // finish_get reports the device error per key
+        for (size_t b0 = 0; b0 < g.second.size(); b0 += batch) {
+            const size_t nb = std::min(batch, g.second.size() - b0);
+            Bytes flat(nb * size_t(n) * S, 0);
+            for (size_t j = 0; j < nb; j++)
+                for (int c = 0; c < n; c++)
+                    if (present[c]) std::memcpy(flat.data() + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
+            if (rsmi_reconstruct_batch_host(ctx, flat.data(), size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
+                continue;  // leave these keys to the per-key path
+            for (size_t j = 0; j < nb; j++)
+                for (int c = 0; c < k; c++)
+                    if (!present[c]) {
+                        const uint8_t* row = flat.data() + (j * n + c) * S;
+                        fs[g.second[b0 + j]].shards[c].assign(row, row + S);
+                    }
+        }
+    }
+    for (size_t i = 0; i < keys.size(); i++)
+        if ((*statuses)[i].ok()) (*statuses)[i] = finish_get(keys[i], fs[i], &(*blocks)[i]);
+}
+
+void MigrateBlocks(DagNode& from, DagNode& to, const std::vector<std::string>& keys, std::vector<Status>* statuses,
+                   size_t batch) {
+    statuses->assign(keys.size(), Status());
+    for (size_t b0 = 0; b0 < keys.size(); b0 += std::max<size_t>(batch, 1)) {
+        const size_t nb = std::min(std::max<size_t>(batch, 1), keys.size() - b0);
+        std::vector<std::string> ks(keys.begin() + b0, keys.begin() + b0 + nb);
+        std::vector<Bytes> blocks;
+        std::vector<Status> st;
+        from.GetMany(ks, &blocks, &st, batch);
+        std::vector<std::string> put_keys;
+        std::vector<Bytes> put_blocks;
+        std::vector<size_t> put_idx;
+        for (size_t j = 0; j < nb; j++) {
+            if (!st[j].ok()) {
+                // cluster.go:252-255: a block missing on `from` counts as migrated
+                (*statuses)[b0 + j] = st[j].err == "Key not found" ? Status::Ok() : st[j];
+                continue;
+            }
+            put_keys.push_back(ks[j]);
+            put_blocks.push_back(std::move(blocks[j]));
+            put_idx.push_back(b0 + j);
+        }
+        // PutMany reports only the last error, so verify each key landed with a meta read
+        to.PutMany(put_keys, put_blocks);
+        for (size_t j = 0; j < put_keys.size(); j++) {
+            int size = -1;
+            Status s = to.GetSize(put_keys[j], &size);
+            if (s.ok() && size != int(put_blocks[j].size())) s = Status::Error("migrated block size mismatch");
+            (*statuses)[put_idx[j]] = s;
+            if (s.ok()) (void)from.DeleteBlock(put_keys[j]);  // cluster.go:265-267: warn only
+        }
+    }
 }
 
 // ------------------------------------------------------------------ repair

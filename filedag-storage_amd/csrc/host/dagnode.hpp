@@ -19,7 +19,9 @@
 // Additions for the GPU engine (results identical to the per-block path):
 //   * PutMany batches equal-size blocks through one rsmi_encode_batch_host call;
 //   * RepairDataNodeBatched rebuilds only the repaired node's row for many keys at once
-//     with rsmi_reconstruct_rows_batch_host.
+//     with rsmi_reconstruct_rows_batch_host;
+//   * GetMany decodes the blocks that need it in GPU batches (8(f) rank 3);
+//   * MigrateBlocks moves blocks between erasure sets as batched decode + encode (rank 4).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -74,6 +76,12 @@ public:
     Status Has(const std::string& key, bool* has);
     Status DeleteBlock(const std::string& key);
 
+    // Get for many keys: blocks whose data shards all arrived are assembled directly, the
+    // rest are decoded on the GPU in batches grouped by (block size, survivor pattern)
+    // (SURVEY.md 8(f) rank 3).  statuses[i] is what Get(keys[i]) would return.
+    void GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* blocks, std::vector<Status>* statuses,
+                 size_t batch = 256);
+
     Status RepairDataNode(int from_index, int repair_index);
     // batched: keys needing repair are grouped by (block size, survivor pattern) and rebuilt
     // `batch` at a time on the GPU
@@ -97,6 +105,13 @@ public:
     size_t RepairQueueLen();
 
 private:
+    struct Fetched {
+        Meta meta;
+        std::vector<Bytes> shards;
+        std::vector<int> repair;
+    };
+    Status fetch_for_get(const std::string& key, Fetched* f);
+    Status finish_get(const std::string& key, Fetched& f, Bytes* block);
     Status get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online);
     Status repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,
                         const std::vector<int>& indexes);
@@ -115,6 +130,14 @@ private:
     std::thread worker_;
     bool stop_ = false;
 };
+
+// Slot-migration data move (dag/pool/poolservice/cluster.go:244-270, per key: from.Get ->
+// to.Put -> from.DeleteBlock) with both coding steps batched on the GPU: GetMany on the
+// source erasure set, PutMany on the destination (the two sets may use different (k, m)).
+// statuses[i]: ok when key i now lives on `to`; a key absent on `from` counts as migrated
+// (format.IsNotFound); delete failures on `from` only warn in the reference and are ignored.
+void MigrateBlocks(DagNode& from, DagNode& to, const std::vector<std::string>& keys, std::vector<Status>* statuses,
+                   size_t batch = 256);
 
 // reduceQuorumErrs (error.go:73-82): most frequent error (ignoring errNodeNotFound /
 // errNodeAccessDenied; an empty string is nil and wins ties) if it reaches quorum.

@@ -3,7 +3,8 @@
 //
 //   test_dagnode cpu   datanode framing/CRC, quorum helpers, slots, config checks (no GPU)
 //   test_dagnode gpu   TestDagNode "123456" round trip, RS(10,4) failure/quorum matrix,
-//                      read-repair, RepairDataNode (per key and batched), PutMany batch;
+//                      read-repair, RepairDataNode (per key and batched), PutMany batch,
+//                      GetMany (batched degraded reads), RS(10,4) -> RS(4,2) migration;
 //                      every stored shard is compared with the CPU oracle (test-only).
 #include <cstdio>
 #include <cstdlib>
@@ -334,6 +335,69 @@ static void test_putmany_batch() {
     CHECK(size == 0);
 }
 
+static void test_getmany() {
+    const int k = 10, m = 4;
+    Cluster c(k, m);
+    std::mt19937_64 r(21);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < 60; i++) {
+        keys.push_back("gm-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, i % 4 == 0 ? 262144 : (i % 4 == 1 ? 6 : (i % 4 == 2 ? 65537 : 1048590))));
+        CHECK_OK(c.node->Put(keys.back(), blocks.back()));
+    }
+    // shards lost in different patterns: node 1 down, some keys missing a data shard on
+    // node 4, one key missing more than m shards (unreadable), one absent key
+    c.dn[1]->SetOffline(true);
+    for (int i = 0; i < 60; i += 3) c.dn[4]->server().Delete(keys[i]);
+    for (int j = 5; j <= 9; j++) c.dn[j]->server().Delete(keys[7]);
+    keys.push_back("absent");
+    std::vector<Bytes> got;
+    std::vector<Status> st;
+    c.node->GetMany(keys, &got, &st, 8);
+    for (size_t i = 0; i < 60; i++) {
+        if (i == 7) {
+            CHECK(!st[i].ok());
+            continue;
+        }
+        CHECK_OK(st[i]);
+        CHECK(got[i] == blocks[i]);
+        Bytes one;  // same answer as the per-key Get
+        CHECK_OK(c.node->Get(keys[i], &one));
+        CHECK(one == blocks[i]);
+    }
+    CHECK(!st[60].ok() && st[60].err == "Key not found");
+    CHECK(c.node->RepairQueueLen() > 0);  // read-repairs queued exactly as Get does
+}
+
+static void test_migrate() {
+    Cluster from(10, 4), to(4, 2);
+    std::mt19937_64 r(99);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < 24; i++) {
+        keys.push_back("mig-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, i % 2 ? 262144 : 777));
+        CHECK_OK(from.node->Put(keys.back(), blocks.back()));
+    }
+    from.dn[0]->SetOffline(true);  // the source set is degraded during the move
+    keys.push_back("never-stored");
+    std::vector<Status> st;
+    MigrateBlocks(*from.node, *to.node, keys, &st, 5);
+    from.dn[0]->SetOffline(false);
+    for (size_t i = 0; i < keys.size(); i++) CHECK_OK(st[i]);
+    for (size_t i = 0; i < blocks.size(); i++) {
+        Bytes got;
+        CHECK_OK(to.node->Get(keys[i], &got));
+        CHECK(got == blocks[i]);
+        auto want = oracle_shards(4, 2, blocks[i]);
+        for (int j = 0; j < 6; j++) CHECK(stored_shard(*to.dn[j], keys[i]) == want[j]);
+        bool has = true;
+        from.node->Has(keys[i], &has);
+        CHECK(!has);  // deleted from the source after the move
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (rs_oracle_selftest() != 0) {
@@ -350,6 +414,8 @@ int main(int argc, char** argv) {
         test_repair_datanode(false);
         test_repair_datanode(true);
         test_putmany_batch();
+        test_getmany();
+        test_migrate();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
     return g_fail ? 1 : 0;
