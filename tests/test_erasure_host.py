@@ -102,3 +102,19 @@ def test_key_gpu_stable_and_balanced():
         assert g == multi.key_gpu(k, 8)
         counts[g] += 1
     assert min(counts) > 300
+
+
+def test_datanode_crc_slice_by_8_matches_byte_serial():
+    """The datanode entry CRC (slice-by-8, csrc/host/datanode.cpp) equals the byte-serial
+    restatement of howeyc/crc16 Checksum(IBMTable) on every length class."""
+    import ctypes
+    import random
+
+    L = ctypes.CDLL(rsmi.LIB_PATH)
+    f = L._ZN4rsmi4host9crc16_ibmEPKhmt
+    f.restype = ctypes.c_uint16
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint16]
+    r = random.Random(5)
+    for n in [0, 1, 7, 8, 9, 15, 16, 17, 100, 1000, 4099, 26215]:
+        b = bytes(r.randrange(256) for _ in range(n))
+        assert f(b, n, 0) == multi.crc16_ibm(b), n

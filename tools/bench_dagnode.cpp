@@ -1,0 +1,82 @@
+// bench_dagnode.cpp -- end-to-end rates of the Dag Node mirror over in-process datanodes
+// (host memory in, framed+CRC'd shard entries out): per-block vs GPU-batched Put, Get with
+// a lost data shard, and RepairDataNode.  Diagnostic; numbers recorded in DESIGN.md.
+#include <chrono>
+#include <cstdio>
+#include <random>
+
+#include "../filedag-storage_amd/csrc/host/dagnode.hpp"
+
+using namespace rsmi::host;
+using clk = std::chrono::steady_clock;
+
+static double secs(clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); }
+
+int main(int argc, char** argv) {
+    const int k = argc > 1 ? atoi(argv[1]) : 10, m = argc > 2 ? atoi(argv[2]) : 4;
+    const size_t B = argc > 3 ? size_t(atol(argv[3])) : 262144;
+    const int N = argc > 4 ? atoi(argv[4]) : 512;
+    DagNodeConfig cfg;
+    cfg.data_blocks = k;
+    cfg.parity_blocks = m;
+    std::vector<std::shared_ptr<InProcDataNode>> dn;
+    std::vector<std::shared_ptr<DataNodeClient>> cl;
+    for (int i = 0; i < k + m; i++) {
+        cfg.nodes.push_back("n" + std::to_string(i));
+        dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back()));
+        cl.push_back(dn.back());
+    }
+    std::unique_ptr<DagNode> d;
+    if (!DagNode::New(cfg, cl, &d).ok()) return 2;
+    d->HealthCheckAll();
+    std::mt19937_64 r(1);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < N; i++) {
+        keys.push_back("k" + std::to_string(i));
+        Bytes b(B);
+        for (auto& x : b) x = uint8_t(r());
+        blocks.push_back(std::move(b));
+    }
+    const double gib = double(N) * B / (1 << 30);
+    d->Put("warm", blocks[0]);
+    auto t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Put(keys[i], blocks[i]);
+    const double put1 = secs(t0);
+    t0 = clk::now();
+    d->PutMany(keys, blocks);
+    const double putb = secs(t0);
+    // CRC + framing alone (the datanode's byte-serial CPU loop), for context
+    t0 = clk::now();
+    volatile uint16_t sink = 0;
+    for (int i = 0; i < N; i++) sink ^= crc16_ibm(blocks[i].data(), blocks[i].size());
+    const double crc = secs(t0);
+    dn[0]->SetOffline(true);  // a data shard is lost on every Get
+    Bytes got;
+    t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Get(keys[i], &got);
+    const double get1 = secs(t0);
+    std::vector<Bytes> gm;
+    std::vector<Status> st;
+    t0 = clk::now();
+    d->GetMany(keys, &gm, &st, 256);
+    const double getb = secs(t0);
+    dn[0]->SetOffline(false);
+    d->RunRepairTasks();
+    dn[3]->server().Wipe();
+    t0 = clk::now();
+    d->RepairDataNode(0, 3);
+    const double rep1 = secs(t0);
+    dn[3]->server().Wipe();
+    size_t rep = 0;
+    t0 = clk::now();
+    d->RepairDataNodeBatched(0, 3, 256, &rep);
+    const double repb = secs(t0);
+    std::printf("RS(%d,%d) %d blocks x %zu B (%.2f GiB payload), in-process datanodes\n", k, m, N, B, gib);
+    std::printf("Put per block      %8.2f GiB/s\nPutMany (batched)  %8.2f GiB/s\n", gib / put1, gib / putb);
+    std::printf("Get, 1 lost shard  %8.2f GiB/s\nGetMany (batched)  %8.2f GiB/s\n", gib / get1, gib / getb);
+    std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
+                gib / rep1, gib / repb, rep);
+    std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes)\n", gib / crc);
+    return 0;
+}
