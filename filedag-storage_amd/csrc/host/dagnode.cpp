@@ -229,6 +229,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
     // group equal-size blocks: one GPU batch encode per size, then the per-block fan-out
     std::map<size_t, std::vector<size_t>> groups;
     for (size_t i = 0; i < blocks.size(); i++) groups[blocks[i].size()].push_back(i);
+    PinnedBuf staging;
     for (auto& g : groups) {
         const size_t B = g.first;
         if (B == 0 || g.second.size() == 1) {
@@ -242,9 +243,17 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             continue;
         }
         const size_t S = rsmi_shard_size(B, k), nb = g.second.size();
-        Bytes flat(nb * size_t(n) * S, 0);  // per block: k data rows (Split, zero-padded) + m parity rows
-        for (size_t j = 0; j < nb; j++) std::memcpy(flat.data() + j * n * S, blocks[g.second[j]].data(), B);
-        rc = rsmi_encode_batch_host(ctx, flat.data(), size_t(n) * S, flat.data() + size_t(k) * S, size_t(n) * S, S, nb);
+        // per block: k data rows (Split, zero-padded) + m parity rows
+        uint8_t* flat = staging.reserve(nb * size_t(n) * S);
+        if (!flat) {
+            for (size_t i : g.second) results[i] = Status::Error("out of host memory");
+            continue;
+        }
+        for (size_t j = 0; j < nb; j++) {
+            std::memcpy(flat + j * n * S, blocks[g.second[j]].data(), B);
+            std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
+        }
+        rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
         if (rc) {
             for (size_t i : g.second) results[i] = rsmi_status(rc);
             continue;
@@ -253,7 +262,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         const int wq = EntryQuorum().second;
         for (size_t j = 0; j < nb; j++) {
             QuorumWait w(wq, n - wq + 1);
-            const uint8_t* base = flat.data() + j * n * S;
+            const uint8_t* base = flat + j * n * S;
             for (int i = 0; i < n; i++)
                 w.add(nodes_[i].client->Put(keys[g.second[j]], meta, Bytes(base + size_t(i) * S, base + size_t(i + 1) * S)));
             results[g.second[j]] = w.result("Write failed. Insufficient number of nodes online");
@@ -351,6 +360,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
         for (int c = 0; c < n; c++) pat[c] = fs[i].shards[c].empty() ? '0' : '1';
         groups[{fs[i].meta.block_size, pat}].push_back(i);
     }
+    PinnedBuf staging;
     for (auto& g : groups) {
         const size_t S = rsmi_shard_size(size_t(g.first.first), k);
         std::vector<uint8_t> present(static_cast<size_t>(n));
@@ -364,16 +374,17 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
         if (!ctx) continue;  // finish_get reports the device error per key
         for (size_t b0 = 0; b0 < g.second.size(); b0 += batch) {
             const size_t nb = std::min(batch, g.second.size() - b0);
-            Bytes flat(nb * size_t(n) * S, 0);
+            uint8_t* flat = staging.reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
+            if (!flat) continue;
             for (size_t j = 0; j < nb; j++)
                 for (int c = 0; c < n; c++)
-                    if (present[c]) std::memcpy(flat.data() + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
-            if (rsmi_reconstruct_batch_host(ctx, flat.data(), size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
+                    if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
+            if (rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
                 continue;  // leave these keys to the per-key path
             for (size_t j = 0; j < nb; j++)
                 for (int c = 0; c < k; c++)
                     if (!present[c]) {
-                        const uint8_t* row = flat.data() + (j * n + c) * S;
+                        const uint8_t* row = flat + (j * n + c) * S;
                         fs[g.second[b0 + j]].shards[c].assign(row, row + S);
                     }
         }
@@ -532,6 +543,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     };
     // (block size, survivor pattern) -> pending keys
     std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
+    PinnedBuf staging;
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
@@ -542,15 +554,16 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
         required[to] = 1;
-        Bytes flat(nb * size_t(n) * S, 0);
+        uint8_t* flat = staging.reserve(nb * size_t(n) * S);
+        if (!flat) return Status::Error("out of host memory");
         for (size_t j = 0; j < nb; j++)
             for (int i = 0; i < n; i++)
-                if (present[i]) std::memcpy(flat.data() + (j * n + i) * S, pend[j].shards[i].data(), S);
-        rc = rsmi_reconstruct_rows_batch_host(ctx, flat.data(), size_t(n) * S, S, nb, present.data(), required.data());
+                if (present[i]) std::memcpy(flat + (j * n + i) * S, pend[j].shards[i].data(), S);
+        rc = rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), required.data());
         if (rc) return rsmi_status(rc);
         const Bytes meta = encode_meta(size);
         for (size_t j = 0; j < nb; j++) {
-            const uint8_t* row = flat.data() + (j * n + size_t(to)) * S;
+            const uint8_t* row = flat + (j * n + size_t(to)) * S;
             Status ps = nodes_[to].client->Put(pend[j].key, meta, Bytes(row, row + S));
             if (!ps.ok()) return ps;
             done++;

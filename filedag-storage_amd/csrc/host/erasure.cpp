@@ -4,6 +4,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <new>
 #include <tuple>
 
 namespace rsmi {
@@ -32,6 +33,27 @@ int64_t ceil_frac(int64_t numerator, int64_t denominator) {
     int64_t c = numerator / denominator;
     if (numerator > 0 && numerator % denominator != 0) c++;
     return c;
+}
+
+uint8_t* PinnedBuf::reserve(size_t bytes) {
+    if (bytes <= cap_ && p_) return p_;
+    release();
+    const size_t want = bytes ? bytes : 1;
+    p_ = static_cast<uint8_t*>(rsmi_host_alloc(want));
+    pinned_ = p_ != nullptr;
+    if (!p_) p_ = new (std::nothrow) uint8_t[want];
+    cap_ = p_ ? want : 0;
+    return p_;
+}
+
+void PinnedBuf::release() {
+    if (p_) {
+        if (pinned_) rsmi_host_free(p_);
+        else delete[] p_;
+    }
+    p_ = nullptr;
+    cap_ = 0;
+    pinned_ = false;
 }
 
 rsmi_ctx* shared_context(int k, int m, int device, int* rc) {

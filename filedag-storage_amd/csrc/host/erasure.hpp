@@ -25,6 +25,26 @@ int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
 // (node.go:277,376) but the matrix / device plans are built once.
 rsmi_ctx* shared_context(int k, int m, int device, int* rc);
 
+// Host staging for the batch calls: page-locked (rsmi_host_alloc) so the batch copies run
+// as DMA at full PCIe rate instead of bouncing through the runtime's own pinned pool.
+// Grown on demand and reused; contents are not cleared.  If page-locking fails (no
+// device) it holds ordinary memory and the rsmi call itself reports the device error.
+class PinnedBuf {
+public:
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { release(); }
+    uint8_t* reserve(size_t bytes);
+    uint8_t* data() const { return p_; }
+
+private:
+    void release();
+    uint8_t* p_ = nullptr;
+    size_t cap_ = 0;
+    bool pinned_ = false;
+};
+
 class Erasure {
 public:
     static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);

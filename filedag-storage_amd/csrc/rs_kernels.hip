@@ -51,10 +51,12 @@ constexpr int default_prefetch() {
     return K < cap ? K : cap;
 }
 
-// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row, NT nontemporal memory
-// ops, PF rows in flight per lane (0 = default_prefetch).
-template <int K, int MT, int D, bool NT, int PF = 0, bool PAIR = true>
-__global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
+// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row, NT cache policy (0 = default
+// loads and stores, 1 = nontemporal loads and stores, 2 = nontemporal loads, default stores),
+// PF rows in flight per lane (0 = default_prefetch), WPS waves per SIMD the register
+// allocation must allow.
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd>
+__global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
@@ -98,7 +100,8 @@ __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const Rs
         }
         auto load_col = [&](int c, u32x4 (&dst)[D]) {
 #pragma unroll
-            for (int d = 0; d < D; d++) dst[d] = ld16<NT>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
+            for (int d = 0; d < D; d++)
+                dst[d] = ld16<NT != 0>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
         };
 
         // Software pipeline over the K input rows: a ring of P rows in flight, one
@@ -184,7 +187,7 @@ __global__ __launch_bounds__(kWG, kMinWavesPerSimd) void rs_fast_kernel(const Rs
 #pragma unroll
                     for (int j = 0; j < MT; j++) {
                         u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
-                        if constexpr (NT)
+                        if constexpr (NT == 1)
                             __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
                         else
                             *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
@@ -300,12 +303,12 @@ __global__ __launch_bounds__(kWG) void rs_repitch_kernel(const uint8_t* __restri
 void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 
 // ------------------------------------------------------------------ dispatch table
-template <int K, int MT, int D, bool NT, int PF = 0, bool PAIR = true>
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS>);
 }
 
-template <int K, int D, bool NT>
+template <int K, int D, int NT>
 static void fill_k(FastKernelTable& t) {
     t.fn[K][1][D][NT] = fast_ptr<K, 1, D, NT>();
     t.fn[K][2][D][NT] = fast_ptr<K, 2, D, NT>();
@@ -313,7 +316,7 @@ static void fill_k(FastKernelTable& t) {
     t.fn[K][4][D][NT] = fast_ptr<K, 4, D, NT>();
 }
 
-template <int D, bool NT>
+template <int D, int NT>
 static void fill_d(FastKernelTable& t) {
     fill_k<1, D, NT>(t);
     fill_k<2, D, NT>(t);
@@ -331,16 +334,12 @@ static void fill_d(FastKernelTable& t) {
 const ExpKernelTable& exp_kernels() {
     static const ExpKernelTable t = [] {
         ExpKernelTable x{};
-        x.fn[0][0] = fast_ptr<10, 4, 1, true, 4>();
-        x.fn[0][1] = fast_ptr<10, 4, 1, true, 8>();
-        x.fn[0][2] = fast_ptr<10, 4, 1, true, 10>();
-        x.fn[1][0] = fast_ptr<10, 1, 1, true, 4>();
-        x.fn[1][1] = fast_ptr<10, 1, 1, true, 8>();
-        x.fn[1][2] = fast_ptr<10, 1, 1, true, 10>();
-        x.fn[0][3] = fast_ptr<10, 4, 1, true, 6, false>();
-        x.fn[0][4] = fast_ptr<10, 4, 1, true, 10, false>();
-        x.fn[1][3] = fast_ptr<10, 1, 1, true, 6, false>();
-        x.fn[1][4] = fast_ptr<10, 1, 1, true, 10, false>();
+        x.fn[0][0] = fast_ptr<10, 4, 1, 1, 4>();
+        x.fn[0][1] = fast_ptr<10, 4, 1, 1, 8>();
+        x.fn[0][2] = fast_ptr<10, 4, 1, 1, 10>();
+        x.fn[1][0] = fast_ptr<10, 1, 1, 1, 4>();
+        x.fn[1][1] = fast_ptr<10, 1, 1, 1, 8>();
+        x.fn[1][2] = fast_ptr<10, 1, 1, 1, 10>();
         return x;
     }();
     return t;
@@ -349,10 +348,12 @@ const ExpKernelTable& exp_kernels() {
 const FastKernelTable& fast_kernels() {
     static const FastKernelTable t = [] {
         FastKernelTable x{};
-        fill_d<1, false>(x);
-        fill_d<2, false>(x);
-        fill_d<1, true>(x);
-        fill_d<2, true>(x);
+        fill_d<1, 0>(x);
+        fill_d<2, 0>(x);
+        fill_d<1, 1>(x);
+        fill_d<2, 1>(x);
+        fill_d<1, 2>(x);
+        fill_d<2, 2>(x);
         return x;
     }();
     return t;

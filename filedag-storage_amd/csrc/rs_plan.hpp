@@ -21,15 +21,16 @@ struct RsPlanDev {
     uint32_t tbl[kMaxK * kColDwords];
 };
 
-// Instantiated fast kernels: fn[K][MT][D][NT] (null when K has no instantiation).
+// Instantiated fast kernels: fn[K][MT][D][NT] (null when K has no instantiation); NT is
+// the cache policy (0 default, 1 nontemporal loads + stores, 2 nontemporal loads only).
 struct FastKernelTable {
-    void* fn[17][kMaxMT + 1][3][2];
+    void* fn[17][kMaxMT + 1][3][3];
 };
 
 // Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1, NT=1);
-// v 0/1/2 = 4/8/10 rows in flight (paired XOR), v 3/4 = 6/10 rows, unpaired XOR.
+// v 0/1/2 = 4/8/10 rows in flight.
 struct ExpKernelTable {
-    void* fn[2][5];
+    void* fn[2][3];
 };
 
 const FastKernelTable& fast_kernels();

@@ -65,7 +65,7 @@ struct rsmi_ctx {
     size_t h_stage_cap = 0;
     // options
     int opt_d = 1;
-    int opt_nt = 1;  // nontemporal loads/stores: +5-7% on every shape measured
+    int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
     long opt_waves_per_cu = 0;
     int opt_prefetch = 0;
     std::string last_kernel;
@@ -225,6 +225,13 @@ const char* kernel_label(int K, int MT, int D, int NT, bool fast) {
     return buf;
 }
 
+// Cache policy per tile shape (tools/ntsweep.py, profiles/r01/ntsweep.txt): nontemporal
+// loads are +5-15 % on every shape; nontemporal stores win while a tile writes a large
+// share of its traffic (RS(10,4) encode +9 %, RS(4,2) encode +10 %, RS(2,1) +6 %) and lose
+// once the tile reads at least 4 rows per row written (RS(10,4) 1-row reconstruct -5 %,
+// 2-row -3 %, RS(16,4) 2-row -4 %, RS(4,2) 1-row -5 %; RS(16,4) encode is a tie).
+int auto_cache_policy(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
+
 // Launch every tile of a plan over nblocks blocks.
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream) {
@@ -233,14 +240,13 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                          in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (uint64_t(1) << 31);
     const int D = c->opt_d;
-    const int NT = c->opt_nt;
     for (const DevTile& t : plan.tiles) {
+        const int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
         void* fn = nullptr;
         if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
         int pf_label = 0;
         if (fn && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
-            const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : c->opt_prefetch == 10 ? 2
-                         : c->opt_prefetch == 106 ? 3 : 4;
+            const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][pi];
             pf_label = c->opt_prefetch;
         }
@@ -440,10 +446,11 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         if (value != 1 && value != 2) return RSMI_ERR_INVALID_ARG;
         c->opt_d = int(value);
     } else if (!std::strcmp(key, "nontemporal")) {
-        c->opt_nt = value ? 1 : 0;
+        if (value < -1 || value > 2) return RSMI_ERR_INVALID_ARG;
+        c->opt_nt = int(value);
     } else if (!std::strcmp(key, "prefetch")) {
-        // 4/8/10 = rows in flight with paired XOR; 106/110 = 6/10 rows, unpaired (A/B only)
-        if (value != 0 && value != 4 && value != 8 && value != 10 && value != 106 && value != 110)
+        // 4/8/10 = rows in flight (A/B only; RS(10,4) encode and 1-row reconstruct, NT=1)
+        if (value != 0 && value != 4 && value != 8 && value != 10)
             return RSMI_ERR_INVALID_ARG;
         c->opt_prefetch = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {

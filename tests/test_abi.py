@@ -149,3 +149,7 @@ def test_null_arguments():
         assert L.rsmi_set_option(c._h, b"no_such_knob", 1) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"chunks_per_lane", 3) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"chunks_per_lane", 2) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"nontemporal", 3) == rsmi.ErrInvalidArg
+        for v in (-1, 0, 1, 2):
+            assert L.rsmi_set_option(c._h, b"nontemporal", v) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"prefetch", 505) == rsmi.ErrInvalidArg

@@ -131,7 +131,8 @@ def _dev_layout(k, m, S, nblocks, pad):
                                            (2, 1, 131072, 8), (10, 4, 104858, 9), (3, 2, 17, 129)])
 @pytest.mark.parametrize("opts", [{}, {"chunks_per_lane": 2}, {"nontemporal": 0},
                                   {"chunks_per_lane": 2, "nontemporal": 0}, {"prefetch": 4}, {"prefetch": 8},
-                                  {"prefetch": 10}, {"prefetch": 106}, {"prefetch": 110}])
+                                  {"prefetch": 10}, {"nontemporal": 1}, {"nontemporal": 2},
+                                  {"nontemporal": 2, "chunks_per_lane": 2}])
 def test_encode_batch_dev_vs_oracle(k, m, S, nblocks, opts):
     rs, dbs, pbs = _dev_layout(k, m, S, nblocks, 256)
     host = np.zeros((nblocks, k, rs), dtype=np.uint8)
@@ -171,8 +172,8 @@ def test_encode_batch_dev_unaligned_generic(k, m, S, nblocks):
                          [(10, 4, 26215, 64, [0], True), (16, 4, 262144 // 16, 8, [0, 9], False),
                           (4, 2, 65536, 16, [1, 4], False), (10, 4, 26215, 16, [3, 11, 12, 13], False),
                           (2, 1, 131072, 4, [1], False)])
-@pytest.mark.parametrize("pf", [0, 10])
-def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only, pf):
+@pytest.mark.parametrize("opts", [{}, {"prefetch": 10}, {"nontemporal": 0}, {"nontemporal": 1}, {"nontemporal": 2}])
+def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only, opts):
     n = k + m
     rs = (S + 255) // 256 * 256
     full = np.zeros((nblocks, n, rs), dtype=np.uint8)
@@ -185,7 +186,8 @@ def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only, pf):
     d = torch.from_numpy(erased.reshape(-1).copy()).cuda()
     present = [i not in lost for i in range(n)]
     with rsmi.Codec(k, m) as c:
-        c.set_option("prefetch", pf)
+        for key, val in opts.items():
+            c.set_option(key, val)
         c.reconstruct_batch_dev(d.data_ptr(), rs, n * rs, S, nblocks, present, data_only,
                                 torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()

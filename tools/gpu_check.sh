@@ -16,9 +16,16 @@ if [[ $STEP == all || $STEP == bench ]]; then
   timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
 fi
+if [[ $STEP == all || $STEP == dagnode ]]; then
+  make -C tools > /dev/null && \
+  timeout -k 10 300 tools/build/bench_dagnode 10 4 262144 512 > gpurun_out/dagnode_rs10_4.txt 2>&1 && \
+  timeout -k 10 300 tools/build/bench_dagnode 16 4 4194304 64 > gpurun_out/dagnode_rs16_4.txt 2>&1 || { echo "dagnode bench failed"; exit 1; }
+  cat gpurun_out/dagnode_rs10_4.txt gpurun_out/dagnode_rs16_4.txt
+fi
 if [[ $STEP == all || $STEP == prof ]]; then
   rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --cpu-seconds 0 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err") || { echo "rocprof failed"; tail -20 gpurun_out/prof.err; exit 1; }
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --cpu-seconds 0 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err") || { echo "rocprof failed"; tail -20 gpurun_out/prof.err; exit 1; }
+  python tools/trace_window.py gpurun_out/prof/bench_kernel_trace.csv gpurun_out/prof_bench.json | tee gpurun_out/prof_window.txt
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_fetch.log" 2>&1) || { echo "pmc fetch failed"; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
   (cd /tmp && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_write.log" 2>&1) || { echo "pmc write failed"; tail -20 gpurun_out/pmc_write.log; exit 1; }
   find gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.csv" | head -20

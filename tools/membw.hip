@@ -101,6 +101,150 @@ __global__ __launch_bounds__(256) void membw_rows2(const uint8_t* __restrict__ i
     }
 }
 
+// Read-only / write-only halves of the rows pattern (the DRAM's own read and write
+// ceilings for this access shape).  RO stores only when a lane's XOR hits a magic value
+// (never, for random data), so the loads stay live.
+template <int K>
+__global__ __launch_bounds__(256) void membw_rows_ro(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                     uint64_t in_bs, uint64_t rs, uint32_t cpb, uint32_t tpb,
+                                                     uint32_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        uint32_t ch = tib * 64 + lane;
+        ch = ch < cpb ? ch : cpb - 1;
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) acc ^= ld<true>(reinterpret_cast<const u32x4*>(ib + c * rs) + ch);
+        if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) *reinterpret_cast<u32x4*>(out) = acc;
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void membw_rows_wo(uint8_t* __restrict__ out, uint64_t rs, uint64_t out_bs,
+                                                     uint32_t cpb, uint32_t tpb, uint32_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        const uint32_t ch = tib * 64 + lane;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        const u32x4 v = {t, lane, blk, tib};
+        if (ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < M; j++) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, v + j);
+        }
+    }
+}
+
+// The rows pattern with the K row reads staged by LDS-DMA (global_load_lds_dwordx4, nt),
+// double-buffered per wave: the next tile's K loads are in flight while this tile is
+// XORed out of LDS and stored.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+template <int K, int M>
+__global__ __launch_bounds__(256) void membw_rows_lds(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                      uint32_t tpb, uint32_t ntiles) {
+    __shared__ u32x4 lds[4][2][K][64];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    auto issue = [&](uint32_t t, int b) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        uint32_t ch = tib * 64 + lane;
+        ch = ch < cpb ? ch : cpb - 1;
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+#pragma unroll
+        for (int c = 0; c < K; c++)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ib + c * rs + uint64_t(ch) * 16), (lds_ptr_t)&lds[wid][b][c][0],
+                                             16, 0, 2);
+    };
+    uint32_t t = blockIdx.x * 4 + wid;
+    int b = 0;
+    if (t < ntiles) issue(t, 0);
+    for (; t < ntiles; t += nw, b ^= 1) {
+        if (t + nw < ntiles) {
+            issue(t + nw, b ^ 1);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        const uint32_t ch = tib * 64 + lane;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) acc ^= lds[wid][b][c][lane];
+        if (ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < M; j++) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+        }
+    }
+}
+
+extern "C" int membw_half_launch(int kind, int K, int M, const void* in, void* out, uint64_t in_bs, uint64_t rs,
+                                 uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {
+    // kind 0 = read-only (K rows), 1 = write-only (M rows), 2 = LDS-DMA rows (K read, M written)
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+    if (kind == 0 && K == 10) membw_rows_ro<10><<<grid, 256, 0, st>>>(i, o, in_bs, rs, cpb, tpb, ntiles);
+    else if (kind == 0 && K == 16) membw_rows_ro<16><<<grid, 256, 0, st>>>(i, o, in_bs, rs, cpb, tpb, ntiles);
+    else if (kind == 1 && M == 4) membw_rows_wo<4><<<grid, 256, 0, st>>>(o, rs, out_bs, cpb, tpb, ntiles);
+    else if (kind == 1 && M == 1) membw_rows_wo<1><<<grid, 256, 0, st>>>(o, rs, out_bs, cpb, tpb, ntiles);
+    else if (kind == 2 && K == 10 && M == 4) membw_rows_lds<10, 4><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles);
+    else if (kind == 2 && K == 10 && M == 1) membw_rows_lds<10, 1><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles);
+    else return -1;
+    return hipGetLastError();
+}
+
+// Load and store cache policies split: NTL nontemporal loads, NTS nontemporal stores.
+template <int K, int M, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void membw_rows_pol(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                      uint32_t tpb, uint32_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        const uint32_t ch = tib * 64 + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) acc ^= ld<NTL>(reinterpret_cast<const u32x4*>(ib + c * rs) + chl);
+        if (ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < M; j++) st<NTS>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+        }
+    }
+}
+
+extern "C" int membw_pol_launch(int K, int M, int ntl, int nts, const void* in, void* out, uint64_t in_bs, uint64_t rs,
+                                uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+#define P(k, m, a, b) \
+    if (K == k && M == m && ntl == a && nts == b) membw_rows_pol<k, m, a, b><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles); else
+#define P4(k, m) P(k, m, 0, 0) P(k, m, 0, 1) P(k, m, 1, 0) P(k, m, 1, 1)
+    P4(10, 4) P4(10, 1) return -1;
+#undef P4
+#undef P
+    return hipGetLastError();
+}
+
 extern "C" {
 int membw_rows2_launch(int K, int M, int W, int ORDER, const void* in, void* out, uint64_t in_bs, uint64_t rs,
                        uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {

@@ -32,7 +32,7 @@ def main():
     V = {}
     V["xor10x4"] = (lambda: L.membw_rows_launch(10, 4, 1, b, b + 10 * p, n * p, p, n * p, S, nb, 2048, sh), enc)
     V["xor10x1"] = (lambda: L.membw_rows_launch(10, 1, 1, b + p, b, n * p, p, n * p, S, nb, 2048, sh), rec)
-    pfs = [int(x) for x in os.environ.get("PFS", "0,4,8,10,106,110").split(",")]
+    pfs = [int(x) for x in os.environ.get("PFS", "0,4,8,10,505,504").split(",")]
     wpcs = [int(x) for x in os.environ.get("WPCS", "0,12,16,24").split(",")]
     for pf in pfs:
         for wpc in wpcs:
