@@ -229,7 +229,6 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
     // group equal-size blocks: one GPU batch encode per size, then the per-block fan-out
     std::map<size_t, std::vector<size_t>> groups;
     for (size_t i = 0; i < blocks.size(); i++) groups[blocks[i].size()].push_back(i);
-    PinnedBuf staging;
     for (auto& g : groups) {
         const size_t B = g.first;
         if (B == 0 || g.second.size() == 1) {
@@ -242,30 +241,35 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             for (size_t i : g.second) results[i] = rsmi_status(rc);
             continue;
         }
-        const size_t S = rsmi_shard_size(B, k), nb = g.second.size();
-        // per block: k data rows (Split, zero-padded) + m parity rows
-        uint8_t* flat = staging.reserve(nb * size_t(n) * S);
-        if (!flat) {
-            for (size_t i : g.second) results[i] = Status::Error("out of host memory");
-            continue;
-        }
-        for (size_t j = 0; j < nb; j++) {
-            std::memcpy(flat + j * n * S, blocks[g.second[j]].data(), B);
-            std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
-        }
-        rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
-        if (rc) {
-            for (size_t i : g.second) results[i] = rsmi_status(rc);
-            continue;
-        }
+        const size_t S = rsmi_shard_size(B, k);
+        const size_t chunk = staging_blocks(size_t(n) * S);
         const Bytes meta = encode_meta(int32_t(B));
         const int wq = EntryQuorum().second;
-        for (size_t j = 0; j < nb; j++) {
-            QuorumWait w(wq, n - wq + 1);
-            const uint8_t* base = flat + j * n * S;
-            for (int i = 0; i < n; i++)
-                w.add(nodes_[i].client->Put(keys[g.second[j]], meta, Bytes(base + size_t(i) * S, base + size_t(i + 1) * S)));
-            results[g.second[j]] = w.result("Write failed. Insufficient number of nodes online");
+        for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
+            const size_t nb = std::min(chunk, g.second.size() - c0);
+            const size_t* idx = g.second.data() + c0;
+            // per block: k data rows (Split, zero-padded) + m parity rows
+            uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
+            if (!flat) {
+                for (size_t j = 0; j < nb; j++) results[idx[j]] = Status::Error("out of host memory");
+                continue;
+            }
+            for (size_t j = 0; j < nb; j++) {
+                std::memcpy(flat + j * n * S, blocks[idx[j]].data(), B);
+                std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
+            }
+            rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
+            if (rc) {
+                for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
+                continue;
+            }
+            for (size_t j = 0; j < nb; j++) {
+                QuorumWait w(wq, n - wq + 1);
+                const uint8_t* base = flat + j * n * S;
+                for (int i = 0; i < n; i++)
+                    w.add(nodes_[i].client->Put(keys[idx[j]], meta, Bytes(base + size_t(i) * S, base + size_t(i + 1) * S)));
+                results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
+            }
         }
     }
     // node.go:411-416 returns the error of the last Put
@@ -314,21 +318,22 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
     if (!s.ok()) return s;
     s = enc.DecodeDataBlocks(f.shards);
     if (!s.ok()) return s;
-    if (!f.repair.empty()) {
-        const int32_t bs = f.meta.block_size;
-        std::lock_guard<std::mutex> g(q_mu_);
-        if (repair_queue_.size() < kRepairQueueCap) {  // else: "repair queue is full, discard this task"
-            std::vector<Bytes> shards = f.shards;
-            std::vector<int> idx = f.repair;
-            repair_queue_.push_back([this, key, bs, shards, idx]() { (void)repair_block(key, bs, shards, idx); });
-        }
-        q_cv_.notify_one();
-    }
     const size_t S = size_t(enc.ShardSize());
     block->assign(size_t(config_.data_blocks) * S, 0);
     for (int i = 0; i < config_.data_blocks; i++)
         std::memcpy(block->data() + size_t(i) * S, f.shards[i].data(), std::min(S, f.shards[i].size()));
     block->resize(size_t(f.meta.block_size));
+    if (!f.repair.empty()) {  // the shards move into the task: `f` is spent after this
+        const int32_t bs = f.meta.block_size;
+        std::lock_guard<std::mutex> g(q_mu_);
+        if (repair_queue_.size() < kRepairQueueCap) {  // else: "repair queue is full, discard this task"
+            auto shards = std::make_shared<std::vector<Bytes>>(std::move(f.shards));
+            repair_queue_.push_back([this, key, bs, shards, idx = std::move(f.repair)]() {
+                (void)repair_block(key, bs, std::move(*shards), idx);
+            });
+        }
+        q_cv_.notify_one();
+    }
     return Status::Ok();
 }
 
@@ -345,52 +350,57 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
     if (batch == 0) batch = 1;
     blocks->assign(keys.size(), Bytes());
     statuses->assign(keys.size(), Status());
-    std::vector<Fetched> fs(keys.size());
-    // (block size, survivor pattern) -> indexes of keys whose data shards need decoding
-    std::map<std::pair<int32_t, std::string>, std::vector<size_t>> groups;
-    for (size_t i = 0; i < keys.size(); i++) {
-        (*statuses)[i] = fetch_for_get(keys[i], &fs[i]);
-        if (!(*statuses)[i].ok()) continue;
-        bool data_missing = false;
-        for (int c = 0; c < k; c++) data_missing |= fs[i].shards[c].empty();
-        bool any = false;
-        for (auto& sh : fs[i].shards) any |= !sh.empty();
-        if (!data_missing || !any || fs[i].meta.block_size <= 0) continue;  // per-key path decides
-        std::string pat(static_cast<size_t>(n), '0');
-        for (int c = 0; c < n; c++) pat[c] = fs[i].shards[c].empty() ? '0' : '1';
-        groups[{fs[i].meta.block_size, pat}].push_back(i);
-    }
-    PinnedBuf staging;
-    for (auto& g : groups) {
-        const size_t S = rsmi_shard_size(size_t(g.first.first), k);
-        std::vector<uint8_t> present(static_cast<size_t>(n));
-        for (int c = 0; c < n; c++) present[c] = uint8_t(g.first.second[c] == '1');
-        bool sizes_ok = true;  // every present shard must have the common size (else per-key errors)
-        for (size_t i : g.second)
-            for (int c = 0; c < n; c++) sizes_ok &= !present[c] || fs[i].shards[c].size() == S;
-        if (!sizes_ok) continue;
-        int rc;
-        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
-        if (!ctx) continue;  // finish_get reports the device error per key
-        for (size_t b0 = 0; b0 < g.second.size(); b0 += batch) {
-            const size_t nb = std::min(batch, g.second.size() - b0);
-            uint8_t* flat = staging.reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
-            if (!flat) continue;
-            for (size_t j = 0; j < nb; j++)
-                for (int c = 0; c < n; c++)
-                    if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
-            if (rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
-                continue;  // leave these keys to the per-key path
-            for (size_t j = 0; j < nb; j++)
-                for (int c = 0; c < k; c++)
-                    if (!present[c]) {
-                        const uint8_t* row = flat + (j * n + c) * S;
-                        fs[g.second[b0 + j]].shards[c].assign(row, row + S);
-                    }
+    // `batch` keys at a time: fetched shards are held only for the current chunk
+    for (size_t k0 = 0; k0 < keys.size(); k0 += batch) {
+        const size_t nk = std::min(batch, keys.size() - k0);
+        std::vector<Fetched> fs(nk);
+        // (block size, survivor pattern) -> chunk positions of keys whose data shards need decoding
+        std::map<std::pair<int32_t, std::string>, std::vector<size_t>> groups;
+        for (size_t q = 0; q < nk; q++) {
+            Status& st = (*statuses)[k0 + q];
+            st = fetch_for_get(keys[k0 + q], &fs[q]);
+            if (!st.ok()) continue;
+            bool data_missing = false;
+            for (int c = 0; c < k; c++) data_missing |= fs[q].shards[c].empty();
+            bool any = false;
+            for (auto& sh : fs[q].shards) any |= !sh.empty();
+            if (!data_missing || !any || fs[q].meta.block_size <= 0) continue;  // per-key path decides
+            std::string pat(static_cast<size_t>(n), '0');
+            for (int c = 0; c < n; c++) pat[c] = fs[q].shards[c].empty() ? '0' : '1';
+            groups[{fs[q].meta.block_size, pat}].push_back(q);
         }
+        for (auto& g : groups) {
+            const size_t S = rsmi_shard_size(size_t(g.first.first), k);
+            std::vector<uint8_t> present(static_cast<size_t>(n));
+            for (int c = 0; c < n; c++) present[c] = uint8_t(g.first.second[c] == '1');
+            bool sizes_ok = true;  // every present shard must have the common size (else per-key errors)
+            for (size_t q : g.second)
+                for (int c = 0; c < n; c++) sizes_ok &= !present[c] || fs[q].shards[c].size() == S;
+            if (!sizes_ok) continue;
+            int rc;
+            rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
+            if (!ctx) continue;  // finish_get reports the device error per key
+            const size_t chunk = staging_blocks(size_t(n) * S);
+            for (size_t b0 = 0; b0 < g.second.size(); b0 += chunk) {
+                const size_t nb = std::min(chunk, g.second.size() - b0);
+                uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
+                if (!flat) continue;
+                for (size_t j = 0; j < nb; j++)
+                    for (int c = 0; c < n; c++)
+                        if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
+                if (rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
+                    continue;  // leave these keys to the per-key path
+                for (size_t j = 0; j < nb; j++)
+                    for (int c = 0; c < k; c++)
+                        if (!present[c]) {
+                            const uint8_t* row = flat + (j * n + c) * S;
+                            fs[g.second[b0 + j]].shards[c].assign(row, row + S);
+                        }
+            }
+        }
+        for (size_t q = 0; q < nk; q++)
+            if ((*statuses)[k0 + q].ok()) (*statuses)[k0 + q] = finish_get(keys[k0 + q], fs[q], &(*blocks)[k0 + q]);
     }
-    for (size_t i = 0; i < keys.size(); i++)
-        if ((*statuses)[i].ok()) (*statuses)[i] = finish_get(keys[i], fs[i], &(*blocks)[i]);
 }
 
 void MigrateBlocks(DagNode& from, DagNode& to, const std::vector<std::string>& keys, std::vector<Status>* statuses,
@@ -543,7 +553,6 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     };
     // (block size, survivor pattern) -> pending keys
     std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
-    PinnedBuf staging;
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
@@ -554,7 +563,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
         required[to] = 1;
-        uint8_t* flat = staging.reserve(nb * size_t(n) * S);
+        uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
         if (!flat) return Status::Error("out of host memory");
         for (size_t j = 0; j < nb; j++)
             for (int i = 0; i < n; i++)
@@ -590,7 +599,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         auto gk = std::make_pair(size, pat);
         auto& pend = groups[gk];
         pend.push_back(Pending{key, std::move(shards)});
-        if (pend.size() >= batch) {
+        if (pend.size() >= std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(size), k)))) {
             s = flush(gk, pend);
             if (!s.ok()) return s;
         }

@@ -56,6 +56,11 @@ void PinnedBuf::release() {
     pinned_ = false;
 }
 
+PinnedBuf& thread_staging() {
+    static thread_local PinnedBuf buf;
+    return buf;
+}
+
 rsmi_ctx* shared_context(int k, int m, int device, int* rc) {
     static std::mutex mu;
     static std::map<std::tuple<int, int, int>, rsmi_ctx*> cache;  // lives for the process

@@ -45,6 +45,14 @@ private:
     bool pinned_ = false;
 };
 
+// Page-locking costs tens of ms per 100 MB, so the batch paths share one staging buffer per
+// thread, kept for the thread's life, and cut their batches to at most kStagingBytes.
+constexpr size_t kStagingBytes = size_t(64) << 20;
+PinnedBuf& thread_staging();
+inline size_t staging_blocks(size_t block_bytes) {
+    return block_bytes >= kStagingBytes ? 1 : kStagingBytes / block_bytes;
+}
+
 class Erasure {
 public:
     static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);
