@@ -140,9 +140,15 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                     const uint32_t s3 = (x >> 6) & 0x03030303u;
 #pragma unroll
                     for (int j = 0; j < MT; j++) {
+#ifndef RSMI_DIAG_NOMATH
                         const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
                         const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
                         const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
+#else  // diagnostic build (tools/Makefile, never the product): same loads, ring, table reads
+       // and stores, GF products replaced by one XOR per (output, input) dword
+                        const uint32_t p1 = x ^ u4get(T[0], j), p2 = u4get(T[1], j) ^ u4get(T[2], j) ^ s1,
+                                       p3 = u4get(T[3], j) ^ u4get(T[4], j) ^ s2 ^ s3;
+#endif
                         uint32_t& a = acc[j][d * 4 + w];
                         uint32_t& q = pend[j][d * 4 + w];
                         if constexpr (!PAIR) {

@@ -68,6 +68,7 @@ struct rsmi_ctx {
     int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
     long opt_waves_per_cu = 0;
     int opt_prefetch = 0;
+    int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     std::string last_kernel;
 };
 
@@ -453,6 +454,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         if (value != 0 && value != 4 && value != 8 && value != 10)
             return RSMI_ERR_INVALID_ARG;
         c->opt_prefetch = int(value);
+    } else if (!std::strcmp(key, "zero_copy")) {
+        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_zero_copy = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;
@@ -573,6 +577,30 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
     return RSMI_OK;
 }
 
+// Device-visible alias of the page-locked host range [p, p + len) (hipHostMalloc /
+// rsmi_host_alloc memory), or nullptr when the range is pageable memory.  On the odd-S
+// (linear copy) path, results bound for such a range are written by the repitch kernel
+// straight over PCIe: the copy engines were measured running the linear host->device and
+// device->host transfers one after the other, and taking the write-back off them lets it
+// overlap the next chunk's upload (tools/hostsweep.py: RS(10,4) 256 KiB reconstruct 28.5 ->
+// 35.4 GiB/s, encode 41.3 -> 42.8).  With 2-D DMA rows (S % 8 == 0) the engines already
+// overlap and kernel stores lose 2-12 %, so that path keeps its copies.
+uint8_t* host_alias(void* p, size_t len) {
+    auto alias = [](void* q) -> uint8_t* {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: not an error for the caller
+            return nullptr;
+        }
+        if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+        return static_cast<uint8_t*>(a.devicePointer) + (static_cast<uint8_t*>(q) - static_cast<uint8_t*>(a.hostPointer));
+    };
+    uint8_t* first = alias(p);
+    if (!first || len == 0) return first;
+    uint8_t* last = alias(static_cast<uint8_t*>(p) + len - 1);
+    return last == first + (len - 1) ? first : nullptr;  // one allocation end to end
+}
+
 }  // namespace
 
 extern "C" {
@@ -596,6 +624,10 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
     const bool d2 = dma_2d_ok(S);
     const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (in_bs + out_bs));
     const int ns = nblocks > chunk ? 3 : 1;
+    // odd S: parity straight into page-locked host memory when it is one contiguous
+    // [block][row][S] run (host_alias); 2-D DMA rows stay faster than kernel stores
+    uint8_t* zc = c->opt_zero_copy && !d2 && parity_block_stride == m * S ? host_alias(parity, nblocks * m * S)
+                                                                          : nullptr;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
@@ -622,7 +654,9 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
         // device -> host
-        if (d2 && parity_block_stride == m * S) {
+        if (zc) {
+            if ((rc = repitch(zc + b0 * m * S, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
+        } else if (d2 && parity_block_stride == m * S) {
             HIP_TRY(hipMemcpy2DAsync(dst, S, st.d_out, Sp, S, nb * m, hipMemcpyDeviceToHost, st.stream));
         } else if (d2) {
             for (size_t b = 0; b < nb; b++)
@@ -670,7 +704,10 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
     const bool d2 = dma_2d_ok(S);
     const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / bs);
     const int ns = nblocks > chunk ? 3 : 1;
-    if (!d2) {  // pinned landing area for the rebuilt rows, scattered on the host at the end
+    // odd S: rebuilt rows straight into page-locked host memory (see host_alias)
+    uint8_t* zc = c->opt_zero_copy && !d2 ? host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)
+                                          : nullptr;
+    if (!d2 && !zc) {  // pinned landing area for the rebuilt rows, scattered on the host at the end
         const size_t need = nblocks * nr * S;
         if (c->h_stage_cap < need) {
             if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
@@ -701,7 +738,12 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
             if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * n, st.stream))) return rc;
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, bs, st.d_in, Sp, bs, S, nb, st.stream))) return rc;
-        if (d2) {
+        if (zc) {
+            for (int r : out_rows)
+                if ((rc = repitch(zc + b0 * block_stride + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2) {
             for (int r : out_rows)
                 HIP_TRY(hipMemcpy2DAsync(h + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S, nb,
                                          hipMemcpyDeviceToHost, st.stream));
@@ -716,7 +758,7 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
         }
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
-    if (!d2) {
+    if (!d2 && !zc) {
         for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
             const size_t nb = std::min(chunk, nblocks - b0);
             const uint8_t* hs = c->h_stage + b0 * nr * S;

@@ -370,6 +370,34 @@ static void test_getmany() {
     CHECK(c.node->RepairQueueLen() > 0);  // read-repairs queued exactly as Get does
 }
 
+// Batches larger than one staging chunk (64 MiB: 12 blocks of RS(16,4) x 4 MiB): PutMany
+// encodes in 3 chunks, GetMany works 25 keys at a time and decodes each group in chunks.
+static void test_batches_span_staging_chunks() {
+    const int k = 16, m = 4;
+    Cluster c(k, m);
+    std::mt19937_64 r(77);
+    std::vector<std::string> keys;
+    std::vector<Bytes> blocks;
+    for (int i = 0; i < 30; i++) {
+        keys.push_back("big-" + std::to_string(i));
+        blocks.push_back(rand_bytes(r, 4194304));
+    }
+    CHECK_OK(c.node->PutMany(keys, blocks));
+    for (int i : {0, 11, 12, 23, 24, 29}) {  // chunk edges
+        auto want = oracle_shards(k, m, blocks[i]);
+        for (int j = 0; j < k + m; j++) CHECK(stored_shard(*c.dn[j], keys[i]) == want[j]);
+    }
+    c.dn[0]->SetOffline(true);
+    c.dn[9]->SetOffline(true);
+    std::vector<Bytes> got;
+    std::vector<Status> st;
+    c.node->GetMany(keys, &got, &st, 25);
+    for (size_t i = 0; i < keys.size(); i++) {
+        CHECK_OK(st[i]);
+        CHECK(got[i] == blocks[i]);
+    }
+}
+
 static void test_migrate() {
     Cluster from(10, 4), to(4, 2);
     std::mt19937_64 r(99);
@@ -415,6 +443,7 @@ int main(int argc, char** argv) {
         test_repair_datanode(true);
         test_putmany_batch();
         test_getmany();
+        test_batches_span_staging_chunks();
         test_migrate();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);

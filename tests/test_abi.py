@@ -153,3 +153,5 @@ def test_null_arguments():
         for v in (-1, 0, 1, 2):
             assert L.rsmi_set_option(c._h, b"nontemporal", v) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"prefetch", 505) == rsmi.ErrInvalidArg
+        assert L.rsmi_set_option(c._h, b"zero_copy", 0) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"zero_copy", 2) == rsmi.ErrInvalidArg

@@ -6,6 +6,7 @@ the loss patterns {each single shard, first two data, last two parity, data+pari
 Full-size configs are checked through size-independent properties (encode -> erase ->
 reconstruct round trips) plus oracle spot checks.
 """
+import ctypes
 import itertools
 
 import numpy as np
@@ -290,28 +291,62 @@ def test_golden_vectors_gpu(k, m):
         assert all(sh[i] == bytes(want[i]) for i in range(k))
 
 
+class _HostBufs:
+    """numpy arrays over pageable memory, or over page-locked rsmi_host_alloc memory (the
+    zero-copy write-back path of the host batch calls)."""
+
+    def __init__(self, pinned):
+        self.pinned, self.ptrs = pinned, []
+
+    def full(self, n, fill):
+        if not self.pinned:
+            return np.full(n, fill, dtype=np.uint8)
+        p = rsmi.lib().rsmi_host_alloc(n)
+        assert p
+        self.ptrs.append(p)
+        a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p))
+        a[:] = fill
+        return a
+
+    def free(self):
+        for p in self.ptrs:
+            rsmi.lib().rsmi_host_free(p)
+        self.ptrs = []
+
+
 @pytest.mark.parametrize("S", [26215, 26216, 4096, 1, 104858])
 @pytest.mark.parametrize("padded", [False, True])
-def test_batch_host_layouts(S, padded):
+@pytest.mark.parametrize("memory", ["pageable", "pinned", "pinned-no-zero-copy"])
+def test_batch_host_layouts(S, padded, memory):
     """Host batch entry points over odd/even S and contiguous vs padded host block strides
-    (linear-copy + device repitch path for odd S, 2-D DMA path otherwise)."""
+    (linear-copy + device repitch path for odd S, 2-D DMA path otherwise), from pageable
+    and page-locked host memory (results written back by kernel stores over PCIe)."""
+    bufs = _HostBufs(memory != "pageable")
+    try:
+        _batch_host_layouts(S, padded, bufs, memory != "pinned-no-zero-copy")
+    finally:
+        bufs.free()
+
+
+def _batch_host_layouts(S, padded, bufs, zero_copy):
     k, m = 10, 4
     n = k + m
     nb = 7 if S > 50000 else 37
     gap = 13 if padded else 0
     dbs, pbs, sbs = k * S + gap, m * S + gap, n * S + gap
-    data = np.zeros(nb * dbs, dtype=np.uint8)
+    data = bufs.full(nb * dbs, 0)
     blocks = _rng_bytes(S + 3, nb * k * S).reshape(nb, k, S)
     for b in range(nb):
         data[b * dbs:b * dbs + k * S] = blocks[b].reshape(-1)
-    par = np.full(nb * pbs, 0x77, dtype=np.uint8)
+    par = bufs.full(nb * pbs, 0x77)
     want = orc.encode_fast(k, m, blocks)
     with rsmi.Codec(k, m) as c:
+        c.set_option("zero_copy", 1 if zero_copy else 0)
         c.encode_batch_host_ptr(data.ctypes.data, dbs, par.ctypes.data, pbs, S, nb)
         for b in range(nb):
             assert np.array_equal(par[b * pbs:b * pbs + m * S].reshape(m, S), want[b]), b
             assert (par[b * pbs + m * S:(b + 1) * pbs] == 0x77).all()  # gaps untouched
-        sh = np.full(nb * sbs, 0x33, dtype=np.uint8)
+        sh = bufs.full(nb * sbs, 0x33)
         for b in range(nb):
             sh[b * sbs:b * sbs + k * S] = blocks[b].reshape(-1)
             sh[b * sbs + k * S:b * sbs + n * S] = want[b].reshape(-1)

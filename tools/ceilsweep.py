@@ -41,8 +41,8 @@ def main():
     for g in (512, 1024, 2048):
         V[f"lds 10r4w g{g}"] = (lambda g=g: L.membw_half_launch(2, 10, 4, b, b + k * p, n * p, p, n * p, S, nb, g, sh), nb * n * S)
         V[f"lds 10r1w g{g}"] = (lambda g=g: L.membw_half_launch(2, 10, 1, b + p, b, n * p, p, n * p, S, nb, g, sh), nb * 11 * S)
-    for ntl in (0, 1):
-        for nts in (0, 1):
+    for ntl, nts in ((0, 0), (0, 1), (1, 0), (1, 1), (1, 2), (1, 3)):
+        if True:
             V[f"pol 10r4w L{ntl}S{nts}"] = (lambda a=ntl, z=nts: L.membw_pol_launch(10, 4, a, z, b, b + k * p, n * p, p, n * p, S, nb, 2048, sh), nb * n * S)
             V[f"pol 10r1w L{ntl}S{nts}"] = (lambda a=ntl, z=nts: L.membw_pol_launch(10, 1, a, z, b + p, b, n * p, p, n * p, S, nb, 2048, sh), nb * 11 * S)
     V["xor 10r1w g2048"] = (lambda: L.membw_rows_launch(10, 1, 1, b + p, b, n * p, p, n * p, S, nb, 2048, sh), nb * 11 * S)

@@ -206,7 +206,9 @@ extern "C" int membw_half_launch(int kind, int K, int M, const void* in, void* o
 }
 
 // Load and store cache policies split: NTL nontemporal loads, NTS nontemporal stores.
-template <int K, int M, bool NTL, bool NTS>
+// NTS: 0 default stores, 1 nontemporal, 2 nontemporal for even output rows only, 3 for the
+// first output row only.
+template <int K, int M, bool NTL, int NTS>
 __global__ __launch_bounds__(256) void membw_rows_pol(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
                                                       uint32_t tpb, uint32_t ntiles) {
@@ -224,7 +226,11 @@ __global__ __launch_bounds__(256) void membw_rows_pol(const uint8_t* __restrict_
         for (int c = 0; c < K; c++) acc ^= ld<NTL>(reinterpret_cast<const u32x4*>(ib + c * rs) + chl);
         if (ch < cpb) {
 #pragma unroll
-            for (int j = 0; j < M; j++) st<NTS>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+            for (int j = 0; j < M; j++) {
+                const bool nt = NTS == 1 || (NTS == 2 && (j & 1) == 0) || (NTS == 3 && j == 0);
+                if (nt) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+                else st<false>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+            }
         }
     }
 }
@@ -238,7 +244,7 @@ extern "C" int membw_pol_launch(int K, int M, int ntl, int nts, const void* in, 
     uint8_t* o = (uint8_t*)out;
 #define P(k, m, a, b) \
     if (K == k && M == m && ntl == a && nts == b) membw_rows_pol<k, m, a, b><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles); else
-#define P4(k, m) P(k, m, 0, 0) P(k, m, 0, 1) P(k, m, 1, 0) P(k, m, 1, 1)
+#define P4(k, m) P(k, m, 0, 0) P(k, m, 0, 1) P(k, m, 1, 0) P(k, m, 1, 1) P(k, m, 1, 2) P(k, m, 1, 3)
     P4(10, 4) P4(10, 1) return -1;
 #undef P4
 #undef P

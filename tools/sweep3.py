@@ -13,6 +13,9 @@ sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
 from sweep import membw  # noqa: E402
 import rsmi  # noqa: E402
 
+if os.environ.get("RSMI_LIB"):  # e.g. the RSMI_DIAG_NOMATH build from `make -C tools diag`
+    rsmi.LIB_PATH = os.environ["RSMI_LIB"]
+
 
 def main():
     L = membw()
