@@ -455,7 +455,7 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
             return RSMI_ERR_INVALID_ARG;
         c->opt_prefetch = int(value);
     } else if (!std::strcmp(key, "zero_copy")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
@@ -582,9 +582,9 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
 // (linear copy) path, results bound for such a range are written by the repitch kernel
 // straight over PCIe: the copy engines were measured running the linear host->device and
 // device->host transfers one after the other, and taking the write-back off them lets it
-// overlap the next chunk's upload (tools/hostsweep.py: RS(10,4) 256 KiB reconstruct 28.5 ->
-// 35.4 GiB/s, encode 41.3 -> 42.8).  With 2-D DMA rows (S % 8 == 0) the engines already
-// overlap and kernel stores lose 2-12 %, so that path keeps its copies.
+// overlap the next chunk's upload (tools/hostsweep.py, RS(10,4) 256 KiB: encode 41.7 -> 47.6
+// GiB/s).  Reconstruct also uploads by kernel loads from such memory (below).  With 2-D
+// DMA rows (S % 8 == 0) the engines already overlap, so that path keeps its copies.
 uint8_t* host_alias(void* p, size_t len) {
     auto alias = [](void* q) -> uint8_t* {
         hipPointerAttribute_t a{};
@@ -626,18 +626,27 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
     const int ns = nblocks > chunk ? 3 : 1;
     // odd S: parity straight into page-locked host memory when it is one contiguous
     // [block][row][S] run (host_alias); 2-D DMA rows stay faster than kernel stores
-    uint8_t* zc = c->opt_zero_copy && !d2 && parity_block_stride == m * S ? host_alias(parity, nblocks * m * S)
-                                                                          : nullptr;
+    uint8_t* zc = c->opt_zero_copy && !d2 ? host_alias(parity, (nblocks - 1) * parity_block_stride + m * S) : nullptr;
+    // zero_copy 2 (A/B only): the upload by kernel loads too (RS(10,4) 256 KiB: 47.6 -> 34.6
+    // GiB/s; the copy engine uploads a whole data block faster than kernel loads do)
+    const uint8_t* zin = c->opt_zero_copy == 2 && !d2
+                             ? host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S)
+                             : nullptr;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
         if ((rc = reserve(st.d_in, st.in_cap, nb * in_bs))) return rc;
         if ((rc = reserve(st.d_out, st.out_cap, nb * out_bs))) return rc;
-        if (!d2 && (rc = reserve(st.d_lin, st.lin_cap, nb * k * S))) return rc;
+        if (!d2 && !zin && (rc = reserve(st.d_lin, st.lin_cap, nb * k * S))) return rc;
         const uint8_t* src = data + b0 * data_block_stride;
         uint8_t* dst = parity + b0 * parity_block_stride;
         // host -> device
-        if (d2 && data_block_stride == k * S) {
+        if (zin) {
+            for (size_t r = 0; r < k; r++)
+                if ((rc = repitch(st.d_in + r * Sp, in_bs, zin + b0 * data_block_stride + r * S, data_block_stride, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2 && data_block_stride == k * S) {
             HIP_TRY(hipMemcpy2DAsync(st.d_in, Sp, src, S, S, nb * k, hipMemcpyHostToDevice, st.stream));
         } else if (d2) {
             for (size_t b = 0; b < nb; b++)
@@ -654,8 +663,13 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
         // device -> host
-        if (zc) {
+        if (zc && parity_block_stride == m * S) {
             if ((rc = repitch(zc + b0 * m * S, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
+        } else if (zc) {
+            for (size_t r = 0; r < m; r++)
+                if ((rc = repitch(zc + b0 * parity_block_stride + r * S, parity_block_stride, st.d_out + r * Sp, out_bs,
+                                  S, nb, st.stream)))
+                    return rc;
         } else if (d2 && parity_block_stride == m * S) {
             HIP_TRY(hipMemcpy2DAsync(dst, S, st.d_out, Sp, S, nb * m, hipMemcpyDeviceToHost, st.stream));
         } else if (d2) {
@@ -707,6 +721,11 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
     // odd S: rebuilt rows straight into page-locked host memory (see host_alias)
     uint8_t* zc = c->opt_zero_copy && !d2 ? host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)
                                           : nullptr;
+    // the upload by kernel loads too: only the k rows the plan reads cross PCIe, where the
+    // linear copy would ship whole blocks (RS(10,4) 256 KiB batches: 35.5 -> 42.9 GiB/s).
+    // One launch per row, so small calls keep the single linear copy (tools/latency.cpp:
+    // a 4 KiB block took 59 us this way against 26 us with the copy).
+    const uint8_t* zin = nblocks * size_t(c->n) * S >= (size_t(4) << 20) ? zc : nullptr;
     if (!d2 && !zc) {  // pinned landing area for the rebuilt rows, scattered on the host at the end
         const size_t need = nblocks * nr * S;
         if (c->h_stage_cap < need) {
@@ -722,7 +741,12 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
         const size_t nb = std::min(chunk, nblocks - b0);
         if ((rc = reserve(st.d_in, st.in_cap, nb * bs))) return rc;
         uint8_t* h = shards + b0 * block_stride;
-        if (d2) {
+        if (zin) {  // only the k rows the plan reads cross PCIe
+            for (int r : in_rows)
+                if ((rc = repitch(st.d_in + size_t(r) * Sp, bs, zin + b0 * block_stride + size_t(r) * S, block_stride, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2) {
             for (int r : in_rows)
                 HIP_TRY(hipMemcpy2DAsync(st.d_in + size_t(r) * Sp, bs, h + size_t(r) * S, block_stride, S, nb,
                                          hipMemcpyHostToDevice, st.stream));

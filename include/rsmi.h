@@ -146,9 +146,10 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
  * policy: -1 auto per output width (default), 0 default loads and stores, 1 nontemporal loads
  * and stores, 2 nontemporal loads only), "waves_per_cu" (grid cap, 0 = occupancy),
  * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: for shard
- * sizes that are not a multiple of 8, the host batch calls write results into page-locked
- * destinations (rsmi_host_alloc) with kernel stores over PCIe instead of a device->host
- * copy; 0 = always copy).  Returns
+ * sizes that are not a multiple of 8 and page-locked host buffers (rsmi_host_alloc), the
+ * host batch calls write results with kernel stores over PCIe instead of a device->host
+ * copy, and reconstruct reads its k input rows with kernel loads; 2 = encode also uploads
+ * by kernel loads (A/B); 0 = always copy).  Returns
  * RSMI_ERR_INVALID_ARG for unknown keys or values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */

@@ -154,4 +154,5 @@ def test_null_arguments():
             assert L.rsmi_set_option(c._h, b"nontemporal", v) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"prefetch", 505) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"zero_copy", 0) == rsmi.OK
-        assert L.rsmi_set_option(c._h, b"zero_copy", 2) == rsmi.ErrInvalidArg
+        assert L.rsmi_set_option(c._h, b"zero_copy", 2) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"zero_copy", 3) == rsmi.ErrInvalidArg

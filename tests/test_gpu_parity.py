@@ -316,14 +316,15 @@ class _HostBufs:
 
 @pytest.mark.parametrize("S", [26215, 26216, 4096, 1, 104858])
 @pytest.mark.parametrize("padded", [False, True])
-@pytest.mark.parametrize("memory", ["pageable", "pinned", "pinned-no-zero-copy"])
+@pytest.mark.parametrize("memory", ["pageable", "pinned", "pinned-no-zero-copy", "pinned-zero-copy-2"])
 def test_batch_host_layouts(S, padded, memory):
     """Host batch entry points over odd/even S and contiguous vs padded host block strides
     (linear-copy + device repitch path for odd S, 2-D DMA path otherwise), from pageable
     and page-locked host memory (results written back by kernel stores over PCIe)."""
     bufs = _HostBufs(memory != "pageable")
     try:
-        _batch_host_layouts(S, padded, bufs, memory != "pinned-no-zero-copy")
+        zc = {"pinned-no-zero-copy": 0, "pinned-zero-copy-2": 2}.get(memory, 1)
+        _batch_host_layouts(S, padded, bufs, zc)
     finally:
         bufs.free()
 
@@ -341,7 +342,7 @@ def _batch_host_layouts(S, padded, bufs, zero_copy):
     par = bufs.full(nb * pbs, 0x77)
     want = orc.encode_fast(k, m, blocks)
     with rsmi.Codec(k, m) as c:
-        c.set_option("zero_copy", 1 if zero_copy else 0)
+        c.set_option("zero_copy", zero_copy)
         c.encode_batch_host_ptr(data.ctypes.data, dbs, par.ctypes.data, pbs, S, nb)
         for b in range(nb):
             assert np.array_equal(par[b * pbs:b * pbs + m * S].reshape(m, S), want[b]), b

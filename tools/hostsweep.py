@@ -30,7 +30,7 @@ def main():
         present = [i not in lost for i in range(n)]
         c = rsmi.Codec(k, m)
         res = {}
-        for zc in (0, 1, 0, 1):
+        for zc in (0, 1, 2, 0, 1, 2):
             c.set_option("zero_copy", zc)
             c.encode_batch_host_ptr(din, k * S, dpar, m * S, S, nb)
             t0 = time.perf_counter()

@@ -1,0 +1,58 @@
+// latency.cpp -- per-block call latency of the C-ABI (the Dag Node's per-key Put / Get seam,
+// erasure.go:51-93): rsmi_encode_block and a 1-lost-shard rsmi_reconstruct, from pageable
+// (std::vector, like Go slices over cgo) and page-locked (rsmi_host_alloc) buffers.
+// Diagnostic; prints microseconds per call (median of 200).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../include/rsmi.h"
+
+using clk = std::chrono::steady_clock;
+
+template <class F>
+static double median_us(F f, int iters = 200) {
+    std::vector<double> t;
+    for (int i = 0; i < iters; i++) {
+        auto a = clk::now();
+        if (f() != RSMI_OK) {
+            std::fprintf(stderr, "call failed\n");
+            std::exit(1);
+        }
+        t.push_back(std::chrono::duration<double, std::micro>(clk::now() - a).count());
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main() {
+    const int k = 10, m = 4, n = k + m;
+    rsmi_ctx* c = nullptr;
+    if (rsmi_open(k, m, 0, &c) != RSMI_OK) return 2;
+    for (size_t B : {size_t(4096), size_t(65536), size_t(262144), size_t(1048576), size_t(4194304)}) {
+        const size_t S = rsmi_shard_size(B, k);
+        std::mt19937 r(1);
+        std::vector<uint8_t> blk(B), out(n * S);
+        for (auto& x : blk) x = uint8_t(r());
+        uint8_t* pblk = static_cast<uint8_t*>(rsmi_host_alloc(B));
+        uint8_t* pout = static_cast<uint8_t*>(rsmi_host_alloc(n * S));
+        std::memcpy(pblk, blk.data(), B);
+        std::vector<uint8_t> present(n, 1);
+        present[0] = 0;
+        const double e_pg = median_us([&] { return rsmi_encode_block(c, blk.data(), B, out.data()); });
+        const double r_pg = median_us([&] { return rsmi_reconstruct(c, out.data(), S, present.data(), 1); });
+        const double e_pin = median_us([&] { return rsmi_encode_block(c, pblk, B, pout); });
+        const double r_pin = median_us([&] { return rsmi_reconstruct(c, pout, S, present.data(), 1); });
+        std::printf("B=%8zu  encode_block %8.1f us pageable %8.1f us pinned | reconstruct(1 lost) %8.1f us pageable "
+                    "%8.1f us pinned  (%.2f / %.2f GiB/s pageable)\n",
+                    B, e_pg, e_pin, r_pg, r_pin, B / e_pg / 1073.741824, B / r_pg / 1073.741824);
+        rsmi_host_free(pblk);
+        rsmi_host_free(pout);
+    }
+    rsmi_close(c);
+    return 0;
+}
