@@ -89,9 +89,17 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     const uint32_t step_b = nw / tpb, step_t = nw - step_b * tpb;
 
     for (; t < ntiles; t += nw) {
+#ifndef RSMI_DIAG_CACHED
         const uint8_t* ib = in + uint64_t(blk) * in_bs;
         uint8_t* ob = out + uint64_t(blk) * out_bs;
         const uint32_t ch0 = tib * (kWave * D) + lane;
+#else  // diagnostic build (tools/Makefile diag-cached): tiles wrap onto the first 16
+       // blocks (~7 MB, cache-resident), so the kernel's own issue rate (VALU, LDS, waits)
+       // is what the launch time shows
+        const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
+        uint8_t* ob = out + uint64_t(blk & 15) * out_bs;
+        const uint32_t ch0 = tib * (kWave * D) + lane;
+#endif
         uint32_t chl[D];  // load chunk, clamped: every lane's loads stay unconditional
 #pragma unroll
         for (int d = 0; d < D; d++) {

@@ -251,6 +251,76 @@ extern "C" int membw_pol_launch(int K, int M, int ntl, int nts, const void* in, 
     return hipGetLastError();
 }
 
+// Feature bisection between membw_rows (the XOR ceiling) and rs_fast_kernel: FEAT bit 0 =
+// the kernel's row ring (6 rows in flight, one sched_barrier region per row), bit 1 = five
+// broadcast ds_read_b128 table reads per row from LDS (folded into the XOR so they stay
+// live), bit 2 = the partial-last-chunk store branch.
+template <int K, int M, int FEAT>
+__global__ __launch_bounds__(256) void membw_rows3(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                   uint32_t tpb, uint32_t ntiles, uint32_t S) {
+    __shared__ u32x4 s_tbl[K * 5];
+    for (int i = threadIdx.x; i < K * 5; i += 256) s_tbl[i] = u32x4{uint32_t(i), 0u, 0u, 0u} * 0u;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    constexpr int P = (FEAT & 1) ? 6 : K;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t blk = t / tpb, tib = t - blk * tpb;
+        const uint32_t ch = tib * 64 + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        u32x4 v[P];
+#pragma unroll
+        for (int c = 0; c < P; c++) v[c] = ld<true>(reinterpret_cast<const u32x4*>(ib + c * rs) + chl);
+        uint32_t tb = 0;
+        asm volatile("" : "+v"(tb));
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            acc ^= v[c % P];
+            if constexpr ((FEAT & 2) != 0) {
+#pragma unroll
+                for (int f = 0; f < 5; f++) acc ^= s_tbl[tb + c * 5 + f];
+            }
+            if (c + P < K) v[c % P] = ld<true>(reinterpret_cast<const u32x4*>(ib + (c + P) * rs) + chl);
+            if constexpr ((FEAT & 1) != 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("" : "+v"(acc));
+        if (ch < cpb) {
+            const uint32_t boff = ch * 16u;
+            if ((FEAT & 4) == 0 || boff + 16u <= S) {
+#pragma unroll
+                for (int j = 0; j < M; j++) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+            } else {
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    uint8_t* q = ob + j * rs + boff;
+                    for (uint32_t b = 0; b < 16 && boff + b < S; b++) q[b] = uint8_t(acc[b / 4] >> (8 * (b % 4)));
+                }
+            }
+        }
+    }
+}
+
+extern "C" int membw_rows3_launch(int K, int M, int FEAT, const void* in, void* out, uint64_t in_bs, uint64_t rs,
+                                  uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+#define F(k, m, f) \
+    if (K == k && M == m && FEAT == f) membw_rows3<k, m, f><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles, S); else
+#define F8(k, m) F(k, m, 0) F(k, m, 1) F(k, m, 2) F(k, m, 3) F(k, m, 4) F(k, m, 5) F(k, m, 6) F(k, m, 7)
+    F8(10, 4) F8(10, 1) return -1;
+#undef F8
+#undef F
+    return hipGetLastError();
+}
+
 extern "C" {
 int membw_rows2_launch(int K, int M, int W, int ORDER, const void* in, void* out, uint64_t in_bs, uint64_t rs,
                        uint64_t out_bs, uint32_t S, uint64_t nblocks, int grid, void* stream) {
