@@ -111,22 +111,26 @@ def cpu_baseline(k, m, B, lost, data_only, seconds):
     data = np.ascontiguousarray(shards[:, :k])
     par = np.zeros((nb, m, S), dtype=np.uint8)
 
-    def one():
-        L.rs_cpu_encode_batch(k, m, data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, threads)
+    def one(th):
+        L.rs_cpu_encode_batch(k, m, data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, th)
         if lost:
             L.rs_cpu_reconstruct_batch(k, m, shards.ctypes.data, n * S, S, nb, present.ctypes.data,
-                                       1 if data_only else 0, threads)
+                                       1 if data_only else 0, th)
 
-    one()  # warm
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
-        one()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    def rate(th, budget):
+        one(th)  # warm
+        reps = 0
+        t0 = time.perf_counter()
+        while True:
+            one(th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return reps, el
+
+    reps, el = rate(threads, seconds)
     gibs = reps * nb * B / el / 2**30
+    reps1, el1 = rate(1, max(1.0, seconds / 4))  # the 1-core figure SURVEY.md 8(d) asks for
     what = "encode" + (f"+{'ReconstructData' if data_only else 'Reconstruct'}(lost {lost})" if lost else "")
     return {
         "value": round(gibs, 3),
@@ -135,6 +139,7 @@ def cpu_baseline(k, m, B, lost, data_only, seconds):
         "kind": "port",
         "sample": f"{reps} passes x {nb} blocks of {B // 1024} KiB RS({k},{m}) {what}, "
                   f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s",
+        "single_core_value": round(reps1 * nb * B / el1 / 2**30, 3),
     }
 
 
@@ -268,8 +273,9 @@ def main():
     el = time.perf_counter() - t0
     el_max = max_over_ranks(el, world)
 
-    enc_ms = sum(ev_b[i].elapsed_time(ev_a[i]) for i in range(a.steps)) / a.steps
-    rec_ms = sum(ev_a[i].elapsed_time(ev_b[i + 1]) for i in range(a.steps)) / a.steps
+    enc_t = sorted(ev_b[i].elapsed_time(ev_a[i]) for i in range(a.steps))
+    rec_t = sorted(ev_a[i].elapsed_time(ev_b[i + 1]) for i in range(a.steps))
+    enc_ms, rec_ms = sum(enc_t) / a.steps, sum(rec_t) / a.steps
     r = len([i for i in lost if i < k or not data_only])
     enc_bytes = nb * (k + m) * S
     rec_bytes = nb * (k + r) * S
@@ -312,6 +318,7 @@ def main():
             "kernel": enc_kernel,
             "algorithmic_bytes_per_launch": enc_bytes,
             "avg_launch_ms": round(enc_ms, 4),
+            "median_launch_ms": round(enc_t[a.steps // 2], 4),
         },
         "cpu_baseline": None,
     }
