@@ -1,0 +1,65 @@
+// crc16.cpp -- host half of the split CRC-16 (see crc16.hpp).
+#include "crc16.hpp"
+
+#include <cstdlib>
+
+namespace rsmi {
+
+namespace {
+uint16_t zero_byte(const uint16_t* T, uint16_t s) { return uint16_t(T[s & 0xFF] ^ (s >> 8)); }
+}  // namespace
+
+Crc16Tables::Crc16Tables() {
+    for (int i = 0; i < 256; i++) {
+        uint16_t c = uint16_t(i);
+        for (int j = 0; j < 8; j++) c = (c & 1) ? uint16_t((c >> 1) ^ 0xA001) : uint16_t(c >> 1);
+        T[i] = c;
+    }
+    for (int b = 0; b < 256; b++) {
+        U[0][b] = T[b];
+        for (int p = 1; p < 16; p++) U[p][b] = zero_byte(T, U[p - 1][b]);
+    }
+    // A^(2^0) = A; A^(2^(i+1)) = A^(2^i) applied twice (tables are linear in the byte index)
+    for (int x = 0; x < 256; x++) {
+        P[0][0][x] = zero_byte(T, uint16_t(x));
+        P[0][1][x] = zero_byte(T, uint16_t(x << 8));
+    }
+    for (int i = 1; i < kCrcPowers; i++)
+        for (int h = 0; h < 2; h++)
+            for (int x = 0; x < 256; x++) {
+                const uint16_t v = P[i - 1][h][x];
+                P[i][h][x] = uint16_t(P[i - 1][0][v & 0xFF] ^ P[i - 1][1][v >> 8]);
+            }
+    // the group order the negative shifts rely on: A^32767 = I on a basis
+    for (int bit = 0; bit < 16; bit++)
+        if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();
+}
+
+uint16_t Crc16Tables::shift(uint16_t s, uint64_t n) const {
+    uint32_t e = uint32_t(n % kCrcOrder);
+    for (int i = 0; e; i++, e >>= 1)
+        if (e & 1) s = pow2(i, s);
+    return s;
+}
+
+uint16_t Crc16Tables::fold(uint16_t s, const uint8_t* p, size_t n) const {
+    for (size_t i = 0; i < n; i++) s = uint16_t(T[(s ^ p[i]) & 0xFF] ^ (s >> 8));
+    return s;
+}
+
+const Crc16Tables& crc16_tables() {
+    static const Crc16Tables t;
+    return t;
+}
+
+uint16_t crc16_checksum(const uint8_t* p, size_t n) {
+    return uint16_t(~crc16_tables().fold(0xFFFF, p, n));
+}
+
+uint16_t crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
+    const Crc16Tables& t = crc16_tables();
+    const uint16_t s = t.fold(0xFFFF, head, head_len);
+    return uint16_t(~(t.shift(s, data_len) ^ uint16_t(raw)));
+}
+
+}  // namespace rsmi

@@ -1,0 +1,47 @@
+// crc16.hpp -- CRC-16 "IBM" (howeyc/crc16 Checksum(data, IBMTable), the datanode entry
+// checksum of dag/node/datanode/server.go:70) split into pieces the GPU can compute in
+// parallel.
+//
+// Notation (reflected register s, 16 bits; T = makeTable(0xA001)):
+//   byte update    s' = T[(s ^ b) & 0xFF] ^ (s >> 8)        (howeyc update(), per byte)
+//   zero byte      A(s) = T[s & 0xFF] ^ (s >> 8)            (linear over GF(2))
+//   raw CRC        R(D) = fold of the byte update over D from s = 0
+//   Checksum(D)    = ~fold from s = 0xFFFF = ~(A^|D|(0xFFFF) ^ R(D))
+// The byte update is A(s) ^ T[b], so a fold from s0 over D is A^|D|(s0) ^ R(D) and
+//   R(D1 || D2) = A^|D2|(R(D1)) ^ R(D2).
+// A is invertible with A^32767 = I (x^16+x^15+x^2+1 = (x+1)(x^15+x+1), x^15+x+1 primitive),
+// so shifts by negative byte counts are shifts by (n mod 32767).
+//
+// Device split (rs_kernels.hip rs_crc16_rows_kernel): each lane folds 16-byte chunks with
+// the positional tables U[p][b] = A^p(T[b]) (R(chunk) = XOR_p U[15-p][b_p]), lanes and tiles
+// combine with the power tables A^(2^i), and one atomic XOR per (row, segment) lands the
+// row's R(D) in a u32.  The host turns R(D) into the datanode checksum with entry_crc().
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace rsmi {
+
+constexpr int kCrcPowers = 15;  // A^(2^i), i < 15: any exponent mod 32767
+constexpr uint32_t kCrcOrder = 32767;
+
+struct Crc16Tables {
+    uint16_t T[256];                  // howeyc makeTable(IBM)
+    uint16_t U[16][256];              // U[p][b] = A^p(T[b])
+    uint16_t P[kCrcPowers][2][256];   // P[i][0][x] = A^(2^i)(x), P[i][1][x] = A^(2^i)(x << 8)
+    Crc16Tables();
+    uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
+    // A^n(s) for any n >= 0 (reduced mod 32767)
+    uint16_t shift(uint16_t s, uint64_t n) const;
+    // fold from register s over p[0..n)
+    uint16_t fold(uint16_t s, const uint8_t* p, size_t n) const;
+};
+
+const Crc16Tables& crc16_tables();
+
+// howeyc Checksum(p, IBMTable)
+uint16_t crc16_checksum(const uint8_t* p, size_t n);
+// Checksum(head || D) given only R(D) and |D| (head may be empty)
+uint16_t crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len);
+
+}  // namespace rsmi

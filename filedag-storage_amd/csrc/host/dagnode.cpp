@@ -162,6 +162,17 @@ Bytes DagNode::encode_meta(int32_t size) {
     return b;
 }
 
+uint16_t DagNode::entry_checksum(const Bytes& meta, size_t S, uint32_t raw) {
+    // |meta size (4 LE)|data size (4 LE)|meta| precede the shard in the checksummed bytes
+    Bytes head(8 + meta.size());
+    for (int i = 0; i < 4; i++) {
+        head[i] = uint8_t(uint32_t(meta.size()) >> (8 * i));
+        head[4 + i] = uint8_t(uint32_t(S) >> (8 * i));
+    }
+    std::copy(meta.begin(), meta.end(), head.begin() + 8);
+    return rsmi_crc16_entry(head.data(), head.size(), raw, S);
+}
+
 Status DagNode::get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online) {
     const size_t n = nodes_.size();
     std::vector<Meta> metas(n);
@@ -214,11 +225,15 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
     if (!s.ok()) return s;
     std::vector<Bytes> shards;
-    s = enc.EncodeData(block, &shards);
+    std::vector<uint32_t> raw;
+    s = gpu_checksums_ ? enc.EncodeDataWithCrc(block, &shards, &raw) : enc.EncodeData(block, &shards);
     if (!s.ok()) return s;
     const int wq = EntryQuorum().second;
     QuorumWait w(wq, int(nodes_.size()) - wq + 1);
-    for (size_t i = 0; i < nodes_.size(); i++) w.add(nodes_[i].client->Put(key, meta, shards[i]));  // no cancel
+    for (size_t i = 0; i < nodes_.size(); i++)  // no cancel
+        w.add(raw.empty() ? nodes_[i].client->Put(key, meta, shards[i])
+                          : nodes_[i].client->PutWithChecksum(key, meta, shards[i],
+                                                              entry_checksum(meta, shards[i].size(), raw[i])));
     return w.result("Write failed. Insufficient number of nodes online");
 }
 
@@ -245,6 +260,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         const size_t chunk = staging_blocks(size_t(n) * S);
         const Bytes meta = encode_meta(int32_t(B));
         const int wq = EntryQuorum().second;
+        std::vector<uint32_t> raw;
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
             const size_t* idx = g.second.data() + c0;
@@ -258,7 +274,13 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 std::memcpy(flat + j * n * S, blocks[idx[j]].data(), B);
                 std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
             }
-            rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
+            if (gpu_checksums_) {
+                raw.resize(nb * size_t(n));
+                rc = rsmi_encode_batch_host_crc(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb,
+                                                raw.data());
+            } else {
+                rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
+            }
             if (rc) {
                 for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
                 continue;
@@ -266,8 +288,13 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             for (size_t j = 0; j < nb; j++) {
                 QuorumWait w(wq, n - wq + 1);
                 const uint8_t* base = flat + j * n * S;
-                for (int i = 0; i < n; i++)
-                    w.add(nodes_[i].client->Put(keys[idx[j]], meta, Bytes(base + size_t(i) * S, base + size_t(i + 1) * S)));
+                for (int i = 0; i < n; i++) {
+                    Bytes shard(base + size_t(i) * S, base + size_t(i + 1) * S);
+                    w.add(gpu_checksums_
+                              ? nodes_[i].client->PutWithChecksum(keys[idx[j]], meta, shard,
+                                                                  entry_checksum(meta, S, raw[j * n + i]))
+                              : nodes_[i].client->Put(keys[idx[j]], meta, shard));
+                }
                 results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
             }
         }

@@ -101,6 +101,11 @@ public:
     const DagNodeConfig& GetConfig() const { return config_; }
     bool GetDataNodeState(int set_index) const;
     void SetDataNodeState(int set_index, bool v) { nodes_.at(set_index).state = v; }
+    // Put / PutMany compute each shard's datanode entry checksum on the GPU, from the rows
+    // the encode already holds, and send it with the shard (DataNodeClient::PutWithChecksum)
+    // instead of leaving the byte-serial CRC to the datanode.  On by
+    // default; the stored entries are byte-identical either way.
+    void SetGpuChecksums(bool v) { gpu_checksums_ = v; }
     std::pair<int, int> EntryQuorum() const;  // (read, write)
     size_t RepairQueueLen();
 
@@ -117,12 +122,15 @@ private:
                         const std::vector<int>& indexes);
     Status fetch_for_repair(const std::string& key, int repair_index, std::vector<Bytes>* shards);
     static Bytes encode_meta(int32_t size);
+    // server.go:70's checksum of the entry (meta, S-byte shard) from the shard's R(shard)
+    static uint16_t entry_checksum(const Bytes& meta, size_t S, uint32_t raw);
 
     DagNodeConfig config_;
     std::vector<StorageNode> nodes_;
     std::vector<uint8_t> slots_;
     int num_slots_ = 0;
     int device_ = 0;
+    bool gpu_checksums_ = true;
 
     std::mutex q_mu_;
     std::condition_variable q_cv_;

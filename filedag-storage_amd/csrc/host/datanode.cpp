@@ -62,17 +62,25 @@ uint16_t crc16_ibm(const uint8_t* p, size_t n, uint16_t crc) {
     return uint16_t(~crc);
 }
 
-Status DataNodeServer::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
+Status DataNodeServer::store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc) {
     if (key.empty()) return Status::Error("Key cannot be empty");  // badger, server_test.go:14-22
     Bytes e(size_t(kHeaderSize) + meta.size() + data.size());
     put_le32(e.data() + 4, uint32_t(meta.size()));
     put_le32(e.data() + 8, uint32_t(data.size()));
     if (!meta.empty()) std::memcpy(e.data() + kHeaderSize, meta.data(), meta.size());
     if (!data.empty()) std::memcpy(e.data() + kHeaderSize + meta.size(), data.data(), data.size());
-    put_le32(e.data(), crc16_ibm(e.data() + 4, e.size() - 4));  // server.go:70-75
+    put_le32(e.data(), crc ? *crc : crc16_ibm(e.data() + 4, e.size() - 4));  // server.go:70-75
     std::lock_guard<std::mutex> g(mu_);
     kv_[key] = std::move(e);
     return Status::Ok();
+}
+
+Status DataNodeServer::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
+    return store(key, meta, data, nullptr);
+}
+
+Status DataNodeServer::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+    return store(key, meta, data, &crc);
 }
 
 Status DataNodeServer::Get(const std::string& key, Bytes* meta, Bytes* data) {
@@ -133,6 +141,9 @@ Status InProcDataNode::down() const { return Status::Error("rpc error: code = Un
 
 Status InProcDataNode::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
     return offline_ ? down() : server_.Put(key, meta, data);
+}
+Status InProcDataNode::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+    return offline_ ? down() : server_.PutWithChecksum(key, meta, data, crc);
 }
 Status InProcDataNode::Get(const std::string& key, Bytes* meta, Bytes* data) {
     return offline_ ? down() : server_.Get(key, meta, data);

@@ -40,6 +40,13 @@ class DataNodeClient {
 public:
     virtual ~DataNodeClient() = default;
     virtual Status Put(const std::string& key, const Bytes& meta, const Bytes& data) = 0;
+    // Put with the entry checksum computed by the sender (the DagNode gets R(shard) from the
+    // GPU encode).  Over gRPC this is an optional AddRequest field; a
+    // datanode without it recomputes, which is what this default does.
+    virtual Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+        (void)crc;
+        return Put(key, meta, data);
+    }
     virtual Status Get(const std::string& key, Bytes* meta, Bytes* data) = 0;
     virtual Status GetMeta(const std::string& key, Bytes* meta) = 0;
     virtual Status Delete(const std::string& key) = 0;
@@ -53,6 +60,9 @@ public:
 class DataNodeServer {
 public:
     Status Put(const std::string& key, const Bytes& meta, const Bytes& data);
+    // the same entry, with the sender's checksum in place of the server.go:70 CRC pass; Get
+    // and GetMeta still verify it, so a wrong sender checksum fails the read like corruption
+    Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc);
     Status Get(const std::string& key, Bytes* meta, Bytes* data);
     Status GetMeta(const std::string& key, Bytes* meta);
     Status Delete(const std::string& key);
@@ -64,6 +74,7 @@ public:
     void Wipe();
 
 private:
+    Status store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc);
     std::mutex mu_;
     std::map<std::string, Bytes> kv_;
 };
@@ -73,6 +84,7 @@ class InProcDataNode : public DataNodeClient {
 public:
     explicit InProcDataNode(std::string addr) : addr_(std::move(addr)) {}
     Status Put(const std::string& key, const Bytes& meta, const Bytes& data) override;
+    Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) override;
     Status Get(const std::string& key, Bytes* meta, Bytes* data) override;
     Status GetMeta(const std::string& key, Bytes* meta) override;
     Status Delete(const std::string& key) override;

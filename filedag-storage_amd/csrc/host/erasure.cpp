@@ -102,6 +102,23 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     return Status::Ok();
 }
 
+Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw) const {
+    const int n = data_blocks_ + parity_blocks_;
+    shards->assign(size_t(n), Bytes());
+    raw->clear();
+    if (data.empty()) return Status::Ok();  // erasure.go:52-54
+    int rc;
+    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    if (!c) return rsmi_status(rc);
+    const size_t S = rsmi_shard_size(data.size(), data_blocks_);
+    Bytes flat(size_t(n) * S);
+    raw->assign(size_t(n), 0);
+    rc = rsmi_encode_block_crc(c, data.data(), data.size(), flat.data(), raw->data());
+    if (rc) return rsmi_status(rc);
+    for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    return Status::Ok();
+}
+
 Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
     const int n = data_blocks_ + parity_blocks_;
     if (int(shards.size()) != n) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);

@@ -57,6 +57,9 @@ class Erasure {
 public:
     static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);
     Status EncodeData(const Bytes& data, std::vector<Bytes>* shards) const;
+    // EncodeData plus R(shard) of every shard from the GPU (include/rsmi.h, datanode CRC-16);
+    // raw is left empty for an empty block
+    Status EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw) const;
     Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
     Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;
     int64_t ShardSize() const { return ceil_frac(block_size_, data_blocks_); }

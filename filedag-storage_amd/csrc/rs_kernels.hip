@@ -24,6 +24,7 @@
 
 #include <cstdint>
 
+#include "crc16.hpp"
 #include "rs_plan.hpp"
 
 namespace rsmi {
@@ -315,6 +316,101 @@ __global__ __launch_bounds__(kWG) void rs_repitch_kernel(const uint8_t* __restri
 }
 
 void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
+
+// ------------------------------------------------------------------ CRC-16 of shard rows
+// R(row) of the datanode entry checksum (crc16.hpp has the algebra).  A wave owns one
+// segment of kCrcSegTiles consecutive 1 KiB tiles of one row: each lane loads its 16-byte
+// chunk of every tile (all loads in flight first), folds each chunk with 16 positional
+// LDS lookups and carries a running register across the tiles (A^1024 between tiles).  A
+// Hillis-Steele scan over the 64 lanes (A^(16*2^j) per level) leaves the segment's value,
+// relative to the segment's end, in lane 63; shifting it by (S - segment end) mod 32767
+// bytes places it relative to the row's end, and one atomic XOR adds it into the row's
+// word.  Bytes at or past S read as zero (zero bytes contribute nothing to R, they only
+// move the reference point, which the final shift accounts for).
+__device__ __forceinline__ uint32_t crc_pow(const uint16_t* sP, int i, uint32_t s) {
+    return uint32_t(sP[i * 512 + (s & 0xFF)]) ^ uint32_t(sP[i * 512 + 256 + (s >> 8)]);
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ u32x4 crc_chunk_load(const uint8_t* row, uint64_t off, uint64_t S) {
+    u32x4 v = {0, 0, 0, 0};
+    if (off >= S) return v;
+    if constexpr (ALIGNED) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+        if (off + 16 > S) {
+            const int valid = int(S - off);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int nb = valid - 4 * w;
+                const uint32_t mask = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+                v[w] &= mask;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (off + q < S) v[q >> 2] |= uint32_t(row[off + q]) << (8 * (q & 3));
+    }
+    return v;
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
+                                                            const uint8_t* __restrict__ base, uint64_t bstride,
+                                                            uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
+                                                            uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
+                                                            uint64_t out_bs) {
+    __shared__ uint32_t s_tbl[kCrcTableWords];
+    for (int i = threadIdx.x; i < kCrcTableWords; i += kWG) s_tbl[i] = tbl[i];
+    __syncthreads();
+    const uint16_t* sU = reinterpret_cast<const uint16_t*>(s_tbl);
+    const uint16_t* sP = sU + 16 * 256;
+
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
+        const uint32_t seg = uint32_t(it % nseg);
+        const uint64_t rid = it / nseg;
+        const uint64_t b = rid / nrows;
+        const uint32_t r = uint32_t(rid - b * nrows);
+        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+        const uint32_t t0 = seg * kCrcSegTiles;
+        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
+        u32x4 v[kCrcSegTiles];
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++)
+            if (uint32_t(i) < nt) v[i] = crc_chunk_load<ALIGNED>(row, (uint64_t(t0 + i) * kWave + lane) * 16, S);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++) {
+            if (uint32_t(i) < nt) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int p = 0; p < 16; p++) c ^= sU[(15 - p) * 256 + ((v[i][p >> 2] >> (8 * (p & 3))) & 0xFF)];
+                acc = crc_pow(sP, 10, acc) ^ c;  // previous tiles move 1 KiB further from the end
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t w = crc_pow(sP, 4 + j, acc);  // 16 * 2^j bytes
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (lane >= (1u << j)) acc ^= t;
+        }
+        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
+        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
+        if (e < 0) e += kCrcOrder;
+#pragma unroll
+        for (int i = 0; i < kCrcPowers; i++)
+            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
+        if (lane == kWave - 1) atomicXor(out + b * out_bs + r, acc);
+    }
+}
+
+void* crc16_rows_kernel(bool aligned) {
+    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true>)
+                   : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false>);
+}
 
 // ------------------------------------------------------------------ dispatch table
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd>

@@ -38,4 +38,10 @@ const ExpKernelTable& exp_kernels();
 void* generic_kernel();
 void* repitch_kernel();
 
+// CRC-16 of shard rows (crc16.hpp): device tables are U[16][256] then P[15][2][256] (u16),
+// kCrcTableWords dwords; a wave folds kCrcSegTiles 1 KiB tiles of one row.
+constexpr int kCrcSegTiles = 8;
+constexpr int kCrcTableWords = (16 * 256 + 15 * 2 * 256) / 2;
+void* crc16_rows_kernel(bool aligned);
+
 }  // namespace rsmi

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/rsmi.h"
+#include "crc16.hpp"
 #include "gf256.hpp"
 #include "rs_plan.hpp"
 
@@ -63,6 +64,9 @@ struct rsmi_ctx {
     std::vector<Staging> staging;  // [0] single-block calls, [0..2] batch pipeline
     uint8_t* h_stage = nullptr;    // pinned landing area for rebuilt rows (odd S)
     size_t h_stage_cap = 0;
+    uint32_t* d_crc_tbl = nullptr;  // CRC-16 device tables (crc16.hpp), uploaded on first use
+    uint8_t* d_crc = nullptr;       // raw row CRCs (u32) of host batch calls
+    size_t crc_cap = 0;
     // options
     int opt_d = 1;
     int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
@@ -383,6 +387,8 @@ void rsmi_close(rsmi_ctx* c) {
                 if (s.stream) (void)hipStreamDestroy(s.stream);
             }
             if (c->h_stage) (void)hipHostFree(c->h_stage);
+            if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
+            if (c->d_crc) (void)hipFree(c->d_crc);
         }
     }
     delete c;
@@ -601,12 +607,51 @@ uint8_t* host_alias(void* p, size_t len) {
     return last == first + (len - 1) ? first : nullptr;  // one allocation end to end
 }
 
+// CRC-16 device tables, uploaded once per context (caller holds ctx->mu)
+int ensure_crc_tables(rsmi_ctx* c) {
+    if (c->d_crc_tbl) return RSMI_OK;
+    const Crc16Tables& t = crc16_tables();
+    static_assert(sizeof(t.U) + sizeof(t.P) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
+    std::memcpy(h.data(), t.U, sizeof(t.U));
+    std::memcpy(h.data() + 16 * 256, t.P, sizeof(t.P));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
+    HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    return RSMI_OK;
+}
+
+// R(row) of nrows rows per block into out[b*out_bs + r] (zeroed first), stream-ordered.
+int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
+               uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream) {
+    if (!nblocks || !nrows) return RSMI_OK;
+    int rc = ensure_crc_tables(c);
+    if (rc) return rc;
+    HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
+    if (S == 0) return RSMI_OK;  // R(empty) = 0
+    const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
+    void* fn = crc16_rows_kernel(aligned);
+    const uint64_t tile = uint64_t(kWave) * 16;
+    uint32_t tpb = uint32_t((S + tile - 1) / tile);
+    uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
+    uint64_t nitems = nblocks * nrows * nseg;
+    int& occ = c->occupancy[fn];
+    if (occ <= 0) {
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
+        if (occ <= 0) occ = 1;
+    }
+    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
+    const uint32_t* tb = c->d_crc_tbl;
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
+    HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
+    return RSMI_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                           size_t parity_block_stride, size_t S, size_t nblocks) {
+static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (data_block_stride < size_t(c->k) * S || parity_block_stride < size_t(c->m) * S) return RSMI_ERR_INVALID_ARG;
@@ -632,6 +677,8 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
     const uint8_t* zin = c->opt_zero_copy == 2 && !d2
                              ? host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S)
                              : nullptr;
+    const size_t n = k + m;
+    if (raw_out && (rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
@@ -662,6 +709,11 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
             if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * k, st.stream))) return rc;
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
+        if (raw_out) {  // R(shard) of the k data rows and the m parity rows, [block][row]
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n;
+            if ((rc = launch_crc(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream))) return rc;
+            if ((rc = launch_crc(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream))) return rc;
+        }
         // device -> host
         if (zc && parity_block_stride == m * S) {
             if ((rc = repitch(zc + b0 * m * S, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
@@ -688,7 +740,51 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
         }
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
+    if (raw_out) HIP_TRY(hipMemcpy(raw_out, c->d_crc, nblocks * n * 4, hipMemcpyDeviceToHost));
     return RSMI_OK;
+}
+
+int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                           size_t parity_block_stride, size_t S, size_t nblocks) {
+    return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, nullptr);
+}
+
+int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                               size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
+    if (!raw_out) return RSMI_ERR_INVALID_ARG;
+    return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+}
+
+int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out || !raw_out) return RSMI_ERR_INVALID_ARG;
+    const size_t S = rsmi_shard_size(B, c->k);
+    std::memcpy(shards_out, block, B);
+    std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
+    return encode_host_impl(c, shards_out, size_t(c->k) * S, shards_out + size_t(c->k) * S, size_t(c->m) * S, S, 1,
+                            raw_out);
+}
+
+int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) {
+    if (!c || !d_rows || !d_raw_out || nrows < 0 || out_block_stride < size_t(nrows)) return RSMI_ERR_INVALID_ARG;
+    if (nrows > 1 && shard_stride < S) return RSMI_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    rc = launch_crc(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
+                    static_cast<hipStream_t>(stream));
+    if (rc) return rc;
+    c->last_kernel = "rs_crc16_rows_kernel";
+    return hip_status(hipGetLastError());
+}
+
+uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
+
+uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
+    return crc16_entry(head, head_len, raw, data_len);
 }
 
 static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,

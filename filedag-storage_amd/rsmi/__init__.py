@@ -79,6 +79,13 @@ def lib() -> ctypes.CDLL:
         "rsmi_host_free": (None, [ctypes.c_void_p]),
         "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
         "rsmi_reconstruct_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, ctypes.c_int, ctypes.c_void_p]),
+        "rsmi_crc16_ibm": (ctypes.c_uint16, [u8p, c_size]),
+        "rsmi_crc16_entry": (ctypes.c_uint16, [u8p, c_size, ctypes.c_uint32, c_size]),
+        "rsmi_crc16_rows_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, ctypes.c_int, c_size, c_size,
+                                               ctypes.c_void_p, c_size, ctypes.c_void_p]),
+        "rsmi_encode_batch_host_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
+                                                      ctypes.c_void_p]),
+        "rsmi_encode_block_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
@@ -197,6 +204,26 @@ class Codec:
         _check(lib().rsmi_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                       ctypes.addressof(_buf(q))))
 
+    def encode_block_crc(self, block: bytes):
+        """encode_block plus R(shard) of every shard (GPU CRC-16, include/rsmi.h)."""
+        S = lib().rsmi_shard_size(len(block), self.k)
+        out = bytearray(self.n * S)
+        src = bytearray(block)
+        raw = (ctypes.c_uint32 * self.n)()
+        _check(lib().rsmi_encode_block_crc(self._h, ctypes.addressof(_buf(src)) if src else None, len(block),
+                                           ctypes.addressof(_buf(out)) if out else None, raw))
+        return bytes(out), list(raw)
+
+    def encode_batch_host_crc_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
+                                  nblocks: int, raw_ptr: int) -> None:
+        _check(lib().rsmi_encode_batch_host_crc(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
+                                                raw_ptr))
+
+    def crc16_rows_dev(self, d_rows: int, rs: int, bs: int, nrows: int, S: int, nblocks: int, d_out: int,
+                       out_bs: int, stream: int = 0) -> None:
+        _check(lib().rsmi_crc16_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
+                                         stream or None))
+
     # -- device memory (raw pointers, e.g. torch tensor.data_ptr()); stream = hipStream_t
     def encode_batch_dev(self, d_data: int, data_rs: int, data_bs: int, d_parity: int, parity_rs: int,
                          parity_bs: int, S: int, nblocks: int, stream: int = 0) -> None:
@@ -298,6 +325,18 @@ class Erasure:
 
 def NewErasure(data_blocks: int, parity_blocks: int, block_size: int, device: int = 0) -> Erasure:
     return Erasure(data_blocks, parity_blocks, block_size, device)
+
+
+def crc16_ibm(data: bytes) -> int:
+    """howeyc/crc16 Checksum(data, IBMTable) (dag/node/datanode/server.go:70), host side."""
+    b = bytearray(data)
+    return lib().rsmi_crc16_ibm(ctypes.addressof(_buf(b)) if b else None, len(b))
+
+
+def crc16_entry(head: bytes, raw: int, data_len: int) -> int:
+    """Checksum(head || D) from R(D) = raw and |D| (include/rsmi.h rsmi_crc16_entry)."""
+    h = bytearray(head)
+    return lib().rsmi_crc16_entry(ctypes.addressof(_buf(h)) if h else None, len(h), raw, data_len)
 
 
 def recommended_pitch(S: int) -> int:

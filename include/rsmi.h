@@ -140,6 +140,39 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
                                     size_t S, size_t nblocks, const uint8_t* present, const uint8_t* required,
                                     void* stream);
 
+/* ------------------------------------------------------------------ datanode CRC-16 */
+
+/* The datanode stores every shard as |crc (4 LE)|meta size|data size|meta|data| with
+ * crc = howeyc/crc16 Checksum(entry[4:], IBMTable) (dag/node/datanode/server.go:58-75),
+ * and re-checks it on Get / GetMeta (server.go:93-97, :115-119).  These entry points move
+ * the byte-serial CRC over the shard bytes onto the GPU; the host
+ * only folds in the 12-byte header.  "Raw" CRC R(D) = the CRC-16 register after D from a
+ * zero register, no complement (reflected polynomial 0xA001), held in a uint32. */
+
+/* howeyc Checksum(p, IBMTable) on the host. */
+uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n);
+
+/* Checksum(head || D) from R(D) and |D|: with head = |meta size (4 LE)|data size (4 LE)|meta|
+ * this is the entry checksum server.go:70 computes for a shard D.  head may be empty. */
+uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len);
+
+/* R(row) for nrows rows of S bytes per block on the device: row r of block b at
+ * d_rows + b*block_stride + r*shard_stride; d_raw_out[b*out_block_stride + r] is zeroed and
+ * then receives R(row).  Any alignment (16-byte aligned rows take the fast path).
+ * Stream-ordered. */
+int rsmi_crc16_rows_dev(rsmi_ctx* ctx, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream);
+
+/* rsmi_encode_batch_host plus R(shard) of every shard it touched, computed on the GPU from
+ * the rows already resident there: raw_out[b*(k+m) + r] for data rows r < k and parity rows
+ * k <= r < k+m.  DagNode.Put / PutMany hand these to the datanodes, which then store the
+ * entry without a host CRC pass. */
+int rsmi_encode_batch_host_crc(rsmi_ctx* ctx, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                               size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out);
+
+/* rsmi_encode_block plus raw_out[r] = R(shard r), r < k+m. */
+int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out);
+
 /* ------------------------------------------------------------------ tuning / introspection */
 
 /* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache

@@ -34,6 +34,11 @@ int rs_oracle_reconstruct(int k, int m, uint8_t* shards, size_t S, const uint8_t
 int rs_oracle_check_shards(int n, const size_t* lens, int nil_ok, size_t* S_out);
 int rs_oracle_selftest(void);
 
+/* datanode entry checksum (crc16_oracle.c): howeyc/crc16 Checksum(p, IBMTable), and the
+ * checksum server.go:70 stores for an entry holding meta and data */
+uint16_t rs_oracle_crc16_ibm(const uint8_t* p, size_t n);
+uint32_t rs_oracle_datanode_entry_crc(const uint8_t* meta, size_t meta_len, const uint8_t* data, size_t data_len);
+
 /* fast multi-threaded CPU path (rs_cpu_fast.c): same results, used only as bench.py's
  * cpu_baseline and cross-checked against the scalar path in tests */
 int rs_cpu_encode_batch(int k, int m, const uint8_t* data, size_t data_block_stride,

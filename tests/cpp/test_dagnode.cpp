@@ -122,6 +122,24 @@ static void test_datanode_server() {
     CHECK(crc16_ibm(reinterpret_cast<const uint8_t*>(cv), 9) == 0xB4C8);
 }
 
+static void test_datanode_sender_checksum() {
+    DataNodeServer s;
+    const Bytes meta{4, 0, 0, 0}, data = str("shard-bytes");
+    CHECK_OK(s.Put("a", meta, data));
+    Bytes ea;
+    CHECK(s.RawEntry("a", &ea));
+    const uint16_t good = uint16_t(ea[0] | ea[1] << 8);
+    CHECK_OK(s.PutWithChecksum("b", meta, data, good));
+    Bytes eb;
+    CHECK(s.RawEntry("b", &eb));
+    CHECK(ea == eb);
+    CHECK_OK(s.PutWithChecksum("c", meta, data, uint16_t(good ^ 1)));
+    Bytes m2, d2;
+    Status st = s.Get("c", &m2, &d2);
+    CHECK(!st.ok() && st.err == "checking crc failed");
+    CHECK(rs_oracle_datanode_entry_crc(meta.data(), meta.size(), data.data(), data.size()) == good);
+}
+
 static void test_quorum_helpers() {
     // reduceQuorumErrs
     std::vector<Status> errs = {Status(), Status(), Status::Error("x"), Status::Error(kErrNodeNotFound)};
@@ -426,6 +444,53 @@ static void test_migrate() {
     }
 }
 
+// GPU entry checksums: entries stored through Put / PutMany with the
+// checksum computed on the GPU are byte-identical to the datanode's own server.go:70 pass,
+// and their checksum equals the oracle's for every shard, block size and batch shape.
+static void test_gpu_entry_checksums() {
+    for (auto km : {std::make_pair(2, 1), std::make_pair(10, 4), std::make_pair(16, 4)}) {
+        const int k = km.first, m = km.second, n = k + m;
+        Cluster gpu(k, m), host(k, m);
+        host.node->SetGpuChecksums(false);
+        std::mt19937_64 r(77 + k);
+        std::vector<std::string> keys;
+        std::vector<Bytes> blocks;
+        const size_t sizes[] = {1, 6, 17, 4099, 262144, 262145, 1048590};
+        for (size_t sz : sizes) {
+            keys.push_back("single-" + std::to_string(sz));
+            blocks.push_back(rand_bytes(r, sz));
+            CHECK_OK(gpu.node->Put(keys.back(), blocks.back()));
+            CHECK_OK(host.node->Put(keys.back(), blocks.back()));
+        }
+        std::vector<std::string> bk;
+        std::vector<Bytes> bb;
+        for (int i = 0; i < 37; i++) {
+            bk.push_back("batch-" + std::to_string(i));
+            bb.push_back(rand_bytes(r, 262144));
+        }
+        CHECK_OK(gpu.node->PutMany(bk, bb));
+        CHECK_OK(host.node->PutMany(bk, bb));
+        keys.insert(keys.end(), bk.begin(), bk.end());
+        blocks.insert(blocks.end(), bb.begin(), bb.end());
+        for (size_t j = 0; j < keys.size(); j++) {
+            auto want = oracle_shards(k, m, blocks[j]);
+            Bytes meta(4);
+            for (int b = 0; b < 4; b++) meta[b] = uint8_t(uint32_t(blocks[j].size()) >> (8 * b));
+            for (int i = 0; i < n; i++) {
+                Bytes eg, eh;
+                CHECK(gpu.dn[i]->server().RawEntry(keys[j], &eg));
+                CHECK(host.dn[i]->server().RawEntry(keys[j], &eh));
+                CHECK(eg == eh);
+                const uint32_t crc = uint32_t(eg[0]) | uint32_t(eg[1]) << 8 | uint32_t(eg[2]) << 16 | uint32_t(eg[3]) << 24;
+                CHECK(crc == rs_oracle_datanode_entry_crc(meta.data(), 4, want[i].data(), want[i].size()));
+            }
+            Bytes got;
+            CHECK_OK(gpu.node->Get(keys[j], &got));
+            CHECK(got == blocks[j]);
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (rs_oracle_selftest() != 0) {
@@ -433,6 +498,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     test_datanode_server();
+    test_datanode_sender_checksum();
     test_quorum_helpers();
     test_config_and_slots();
     if (mode == "gpu") {
@@ -445,6 +511,7 @@ int main(int argc, char** argv) {
         test_getmany();
         test_batches_span_staging_chunks();
         test_migrate();
+        test_gpu_entry_checksums();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
     return g_fail ? 1 : 0;

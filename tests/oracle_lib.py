@@ -36,6 +36,10 @@ def lib():
         L.rs_cpu_encode_batch.argtypes = [i, i, vp, sz, vp, sz, sz, sz, i]
         L.rs_cpu_reconstruct_batch.argtypes = [i, i, vp, sz, sz, sz, vp, i, i]
         L.rs_cpu_isa.restype = ctypes.c_char_p
+        L.rs_oracle_crc16_ibm.restype = ctypes.c_uint16
+        L.rs_oracle_crc16_ibm.argtypes = [vp, sz]
+        L.rs_oracle_datanode_entry_crc.restype = ctypes.c_uint32
+        L.rs_oracle_datanode_entry_crc.argtypes = [vp, sz, vp, sz]
         _L = L
     return _L
 
@@ -98,3 +102,22 @@ def splitmix64_bytes(seed: int, nbytes: int) -> np.ndarray:
         x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         x = x ^ (x >> np.uint64(31))
     return x.view(np.uint8)[:nbytes].copy()
+
+
+def crc16_ibm(data) -> int:
+    """howeyc Checksum(data, IBMTable) via the byte-serial oracle (crc16_oracle.c)."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return int(lib().rs_oracle_crc16_ibm(ptr(a) if a.size else None, a.size))
+
+
+def datanode_entry_crc(meta, data) -> int:
+    """The checksum dag/node/datanode/server.go:70 stores for an entry (meta, data)."""
+    m = np.frombuffer(bytes(meta), dtype=np.uint8).copy()
+    d = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return int(lib().rs_oracle_datanode_entry_crc(ptr(m) if m.size else None, m.size,
+                                                  ptr(d) if d.size else None, d.size))
+
+
+def entry_head(meta, data_len: int) -> bytes:
+    """|meta size (4 LE)|data size (4 LE)|meta| -- the checksummed bytes before the data."""
+    return len(meta).to_bytes(4, "little") + data_len.to_bytes(4, "little") + bytes(meta)

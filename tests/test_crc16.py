@@ -1,0 +1,177 @@
+"""Datanode entry checksum (dag/node/datanode/server.go:58-75, howeyc/crc16 IBMTable) and
+its GPU split (include/rsmi.h "datanode CRC-16").
+
+CPU tests pin the byte-serial oracle (crc16_oracle.c) to the CRC-16/USB check value and
+prove the host half of the split -- rsmi_crc16_entry folding a 12-byte entry header onto
+R(data) -- against the oracle's whole-entry checksum, with R(data) computed here in pure
+Python.  GPU tests check the device R(row) kernel and the encode+CRC host batches against
+the oracle byte for byte.  The CRC variant itself is parity-unpinned (no reference test
+holds a value)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+import rsmi
+from rsmi import multi
+
+_T = []
+
+
+def _table():
+    if not _T:
+        for i in range(256):
+            c = i
+            for _ in range(8):
+                c = (c >> 1) ^ 0xA001 if c & 1 else c >> 1
+            _T.append(c)
+    return _T
+
+
+def raw_crc(data: bytes, s: int = 0) -> int:
+    """R(D): the register after D from s (no complement) -- pure-Python byte loop."""
+    T = _table()
+    for b in data:
+        s = T[(s ^ b) & 0xFF] ^ (s >> 8)
+    return s
+
+
+def test_oracle_check_value():
+    assert orc.crc16_ibm(b"123456789") == 0xB4C8  # CRC-16/USB catalogue check
+    assert orc.crc16_ibm(b"") == 0x0000  # ~(~0) with no bytes
+    assert orc.crc16_ibm(b"123456789") == multi.crc16_ibm(b"123456789")
+
+
+def test_library_checksum_matches_oracle():
+    r = random.Random(11)
+    for n in [0, 1, 2, 15, 16, 17, 255, 1024, 4099, 26215]:
+        b = bytes(r.randrange(256) for _ in range(n))
+        assert rsmi.crc16_ibm(b) == orc.crc16_ibm(b), n
+
+
+def test_oracle_entry_crc_is_checksum_of_framed_entry():
+    meta = (262144).to_bytes(4, "little")
+    data = bytes(range(200))
+    framed = orc.entry_head(meta, len(data)) + data
+    assert orc.datanode_entry_crc(meta, data) == orc.crc16_ibm(framed)
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 16, 1023, 1024, 1025, 26215, 40000])
+def test_entry_from_raw_matches_oracle(n):
+    """rsmi_crc16_entry(head, R(D), |D|) == Checksum(head || D): the host half of the split,
+    including shifts past the 32767-byte order of the zero-byte map."""
+    r = random.Random(n)
+    data = bytes(r.randrange(256) for _ in range(n))
+    meta = (n * 10 + 3).to_bytes(4, "little")
+    head = orc.entry_head(meta, n)
+    assert rsmi.crc16_entry(head, raw_crc(data), n) == orc.datanode_entry_crc(meta, data)
+    assert rsmi.crc16_entry(b"", raw_crc(data), n) == orc.crc16_ibm(data)
+
+
+def test_raw_crc_is_linear():
+    """R(D1 || D2) = A^|D2|(R(D1)) ^ R(D2): the identity the GPU combine rests on."""
+    r = random.Random(3)
+    d1 = bytes(r.randrange(256) for _ in range(37))
+    d2 = bytes(r.randrange(256) for _ in range(91))
+    shifted = raw_crc(b"\0" * len(d2), raw_crc(d1))
+    assert raw_crc(d1 + d2) == shifted ^ raw_crc(d2)
+
+
+def _device_rows(nb, nrows, S, pitch, offset, seed):
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    bs = nrows * pitch
+    host = torch.randint(0, 256, (offset + nb * bs + 64,), dtype=torch.uint8, generator=g)
+    return host, host.to("cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1024, 1025, 8191, 8192, 8193, 26215, 104858, 262144])
+@pytest.mark.parametrize("layout", ["aligned", "unaligned"])
+def test_rows_dev_matches_oracle(S, layout):
+    import torch
+
+    nrows, nb = 3, 5
+    if layout == "aligned":
+        pitch, off = (S + 15) // 16 * 16 + 16, 0
+    else:
+        pitch, off = S + 3, 5
+    host, dev = _device_rows(nb, nrows, S, pitch, off, S)
+    out = torch.full((nb, nrows + 1), 0xDEAD, dtype=torch.int32, device="cuda")
+    with rsmi.Codec(4, 2) as c:
+        c.crc16_rows_dev(dev.data_ptr() + off, pitch, nrows * pitch, nrows, S, nb, out.data_ptr(), nrows + 1)
+        torch.cuda.synchronize()
+    got = out.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    h = host.numpy()
+    for b in range(nb):
+        assert got[b, nrows] == 0xDEAD  # slots past nrows untouched
+        for r in range(nrows):
+            row = h[off + b * nrows * pitch + r * pitch:][:S].tobytes()
+            assert got[b, r] < 0x10000
+            assert rsmi.crc16_entry(b"", int(got[b, r]), S) == orc.crc16_ibm(row), (b, r)
+
+
+@pytest.mark.gpu
+def test_rows_dev_full_size_batch():
+    """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows: a checksum of checksums against the
+    oracle on a sample of rows, plus every row nonzero-tested against its own recompute."""
+    import torch
+
+    k, m, nb = 10, 4, 4096
+    n, S = k + m, 26215
+    pitch = rsmi.recommended_pitch(S)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    dev = torch.randint(0, 256, (nb, n, pitch), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
+    with rsmi.Codec(k, m) as c:
+        c.crc16_rows_dev(dev.data_ptr(), pitch, n * pitch, n, S, nb, out.data_ptr(), n)
+        torch.cuda.synchronize()
+        assert c.last_kernel() == "rs_crc16_rows_kernel"
+    got = out.cpu().numpy()
+    rng = random.Random(1)
+    for _ in range(64):
+        b, r = rng.randrange(nb), rng.randrange(n)
+        row = dev[b, r, :S].cpu().numpy().tobytes()
+        assert rsmi.crc16_entry(b"", int(got[b, r]) & 0xFFFF, S) == orc.crc16_ibm(row)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B", [(2, 1, 6), (4, 2, 262144), (10, 4, 262144), (10, 4, 1048576), (16, 4, 65536 + 7)])
+def test_encode_batch_host_crc_entries_match_oracle(k, m, B):
+    """Every shard's datanode entry checksum from the GPU split equals server.go:70 on the
+    oracle's shards."""
+    n = k + m
+    S = (B + k - 1) // k
+    nb = 6
+    r = np.random.default_rng(B + k)
+    data = np.zeros((nb, k * S), dtype=np.uint8)
+    data[:, :B] = r.integers(0, 256, size=(nb, B), dtype=np.uint8)
+    par = np.zeros((nb, m * S), dtype=np.uint8)
+    raw = np.zeros((nb, n), dtype=np.uint32)
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_host_crc_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, raw.ctypes.data)
+    meta = B.to_bytes(4, "little")
+    head = orc.entry_head(meta, S)
+    for b in range(nb):
+        want_par = orc.encode(k, m, data[b].reshape(k, S))
+        assert np.array_equal(par[b].reshape(m, S), want_par)
+        rows = list(data[b].reshape(k, S)) + list(want_par)
+        for i in range(n):
+            assert rsmi.crc16_entry(head, int(raw[b, i]), S) == orc.datanode_entry_crc(meta, rows[i].tobytes()), (b, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 6, 4099, 262144])
+def test_encode_block_crc(B):
+    k, m = 10, 4
+    block = bytes(np.random.default_rng(B).integers(0, 256, size=B, dtype=np.uint8))
+    with rsmi.Codec(k, m) as c:
+        shards, raw = c.encode_block_crc(block)
+    S = len(shards) // (k + m)
+    for i in range(k + m):
+        row = shards[i * S:(i + 1) * S]
+        assert rsmi.crc16_entry(b"", raw[i], S) == orc.crc16_ibm(row)
+    assert shards[:B] == block

@@ -1,5 +1,6 @@
 // bench_dagnode.cpp -- end-to-end rates of the Dag Node mirror over in-process datanodes
-// (host memory in, framed+CRC'd shard entries out): per-block vs GPU-batched Put, Get with
+// (host memory in, framed+CRC'd shard entries out): per-block vs GPU-batched Put (entry
+// checksums from the GPU, and from the datanode's own CRC pass), Get with
 // a lost data shard, and RepairDataNode.  Diagnostic; numbers recorded in DESIGN.md.
 #include <chrono>
 #include <cstdio>
@@ -40,7 +41,17 @@ int main(int argc, char** argv) {
     }
     const double gib = double(N) * B / (1 << 30);
     d->Put("warm", blocks[0]);
+    // host CRC (datanode computes server.go:70) first, then GPU entry checksums (default)
+    d->SetGpuChecksums(false);
     auto t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Put(keys[i], blocks[i]);
+    const double put1h = secs(t0);
+    t0 = clk::now();
+    d->PutMany(keys, blocks);
+    const double putbh = secs(t0);
+    d->SetGpuChecksums(true);
+    d->Put("warm", blocks[0]);
+    t0 = clk::now();
     for (int i = 0; i < N; i++) d->Put(keys[i], blocks[i]);
     const double put1 = secs(t0);
     t0 = clk::now();
@@ -73,7 +84,8 @@ int main(int argc, char** argv) {
     d->RepairDataNodeBatched(0, 3, 256, &rep);
     const double repb = secs(t0);
     std::printf("RS(%d,%d) %d blocks x %zu B (%.2f GiB payload), in-process datanodes\n", k, m, N, B, gib);
-    std::printf("Put per block      %8.2f GiB/s\nPutMany (batched)  %8.2f GiB/s\n", gib / put1, gib / putb);
+    std::printf("Put per block      %8.2f GiB/s (datanode CRC: %.2f)\n", gib / put1, gib / put1h);
+    std::printf("PutMany (batched)  %8.2f GiB/s (datanode CRC: %.2f)\n", gib / putb, gib / putbh);
     std::printf("Get, 1 lost shard  %8.2f GiB/s\nGetMany (batched)  %8.2f GiB/s\n", gib / get1, gib / getb);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Diagnostic: rs_crc16_rows_kernel bandwidth (R(row) of every shard row, the datanode entry
+checksum's device half) over the bench layout: 4096 RS(10,4) 256 KiB blocks, 14 rows of
+S = 26215 at 32 KiB pitch; and 1 MiB / 4 MiB shapes.  Bytes counted: rows x S read."""
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
+import rsmi  # noqa: E402
+
+
+def main():
+    st = torch.cuda.current_stream()
+    for k, m, B, nb in ((10, 4, 262144, 4096), (10, 4, 1 << 20, 1024), (16, 4, 4 << 20, 256)):
+        n = k + m
+        S = (B + k - 1) // k
+        p = rsmi.recommended_pitch(S)
+        buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
+        out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
+        c = rsmi.Codec(k, m)
+        f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
+        t_end = time.perf_counter() + 0.2
+        while time.perf_counter() < t_end:
+            f()
+            torch.cuda.synchronize()
+        ts = []
+        for _ in range(20):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            f()
+            e1.record(st)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S}: {med * 1e3:8.1f} us  "
+              f"{nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
+        c.close()
+
+
+if __name__ == "__main__":
+    main()
