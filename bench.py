@@ -183,6 +183,35 @@ def copy_inclusive(codec, k, m, S, nb, lost, data_only):
     if lost:
         res["reconstruct_GiBs"] = round(reps * nb * B / (t2 - t1) / 2**30, 2)
         res["enc_plus_rec_GiBs"] = round(reps * nb * B / (t2 - t0) / 2**30, 2)
+        # mixed (BASELINE configs[4]): an encode stream and a reconstruct stream at once, each on
+        # its own context (own HIP streams and staging), so one call's uploads overlap the
+        # other's, and the D2H of either rides beside the H2D of both (PCIe is full duplex)
+        import threading
+
+        other = rsmi.Codec(k, m, codec.device)
+        other.reconstruct_batch_host_ptr(dsh, n * S, S, nb, present, data_only)
+        errs = []
+
+        def run(f):
+            try:
+                for _ in range(reps):
+                    f()
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(lambda: codec.encode_batch_host_ptr(din, k * S, dpar, m * S, S, nb),)),
+              threading.Thread(target=run, args=(lambda: other.reconstruct_batch_host_ptr(
+                  dsh, n * S, S, nb, present, data_only),))]
+        t3 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        t4 = time.perf_counter()
+        other.close()
+        if errs:
+            raise errs[0]
+        res["mixed_concurrent_GiBs"] = round(2 * reps * nb * B / (t4 - t3) / 2**30, 2)
     for p in (din, dpar, dsh):
         L.rsmi_host_free(p)
     return res

@@ -101,6 +101,35 @@ __global__ __launch_bounds__(256) void membw_rows2(const uint8_t* __restrict__ i
     }
 }
 
+// Banded tile order: tiles [s*G, (s+1)*G) of every block form band s, and bands run one
+// after another (block-major inside a band).  G = tpb is ORDER 0; smaller G spreads the
+// waves in flight over more blocks, each on a shorter run of its rows.
+template <int K, int M>
+__global__ __launch_bounds__(256) void membw_rows_band(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t cpb,
+                                                   uint32_t tpb, uint32_t ntiles, uint32_t nblocks, uint32_t G) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t nw = gridDim.x * 4;
+    const uint32_t band = nblocks * G;
+    for (uint32_t t = blockIdx.x * 4 + wid; t < ntiles; t += nw) {
+        const uint32_t s = t / band, r = t - s * band;
+        const uint32_t gs = tpb - s * G < G ? tpb - s * G : G;
+        const uint32_t blk = r / gs, tib = s * G + (r - blk * gs);
+        const uint8_t* ib = in + uint64_t(blk) * in_bs;
+        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        const uint32_t ch = tib * 64 + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K; c++) acc ^= ld<true>(reinterpret_cast<const u32x4*>(ib + c * rs) + chl);
+        if (ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < M; j++) st<true>(reinterpret_cast<u32x4*>(ob + j * rs) + ch, acc + j);
+        }
+    }
+}
+
 // Read-only / write-only halves of the rows pattern (the DRAM's own read and write
 // ceilings for this access shape).  RO stores only when a lane's XOR hits a magic value
 // (never, for random data), so the loads stay live.
@@ -336,6 +365,21 @@ int membw_rows2_launch(int K, int M, int W, int ORDER, const void* in, void* out
     R2O(10, 4, 1) R2O(10, 4, 2) R2O(10, 4, 4) R2O(10, 1, 1) R2O(10, 1, 2) R2O(10, 1, 4) return -1;
 #undef R2O
 #undef R2
+    return hipGetLastError();
+}
+
+int membw_rows_band_launch(int K, int M, const void* in, void* out, uint64_t in_bs, uint64_t rs, uint64_t out_bs,
+                       uint32_t S, uint64_t nblocks, uint32_t G, int grid, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    if (G == 0 || G > tpb) G = tpb;
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+    const uint32_t nb = uint32_t(nblocks);
+    if (K == 10 && M == 4) membw_rows_band<10, 4><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles, nb, G);
+    else if (K == 10 && M == 1) membw_rows_band<10, 1><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, cpb, tpb, ntiles, nb, G);
+    else return -1;
     return hipGetLastError();
 }
 
