@@ -19,6 +19,11 @@ Crc16Tables::Crc16Tables() {
         U[0][b] = T[b];
         for (int p = 1; p < 16; p++) U[p][b] = zero_byte(T, U[p - 1][b]);
     }
+    for (int p = 0; p < 16; p++)
+        for (int v = 0; v < 16; v++) {
+            N[2 * p][v] = U[15 - p][v];
+            N[2 * p + 1][v] = U[15 - p][v << 4];
+        }
     // A^(2^0) = A; A^(2^(i+1)) = A^(2^i) applied twice (tables are linear in the byte index)
     for (int x = 0; x < 256; x++) {
         P[0][0][x] = zero_byte(T, uint16_t(x));

@@ -13,7 +13,8 @@
 // so shifts by negative byte counts are shifts by (n mod 32767).
 //
 // Device split (rs_kernels.hip rs_crc16_rows_kernel): each lane folds 16-byte chunks with
-// the positional tables U[p][b] = A^p(T[b]) (R(chunk) = XOR_p U[15-p][b_p]), lanes and tiles
+// positional tables -- R(chunk) = XOR_p U[15-p][b_p], U[p][b] = A^p(T[b]), or by linearity
+// the same with one lookup per nibble in 16-entry tables N -- lanes and tiles
 // combine with the power tables A^(2^i), and one atomic XOR per (row, segment) lands the
 // row's R(D) in a u32.  The host turns R(D) into the datanode checksum with entry_crc().
 #pragma once
@@ -28,6 +29,7 @@ constexpr uint32_t kCrcOrder = 32767;
 struct Crc16Tables {
     uint16_t T[256];                  // howeyc makeTable(IBM)
     uint16_t U[16][256];              // U[p][b] = A^p(T[b])
+    uint16_t N[32][16];               // nibble tables: N[2p][v] = U[15-p][v], N[2p+1][v] = U[15-p][v << 4]
     uint16_t P[kCrcPowers][2][256];   // P[i][0][x] = A^(2^i)(x), P[i][1][x] = A^(2^i)(x << 8)
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }

@@ -320,8 +320,11 @@ void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 // ------------------------------------------------------------------ CRC-16 of shard rows
 // R(row) of the datanode entry checksum (crc16.hpp has the algebra).  A wave owns one
 // segment of kCrcSegTiles consecutive 1 KiB tiles of one row: each lane loads its 16-byte
-// chunk of every tile (all loads in flight first), folds each chunk with 16 positional
-// LDS lookups and carries a running register across the tiles (A^1024 between tiles).  A
+// chunk of every tile (all loads in flight first), folds each chunk with positional LDS
+// lookups -- 32 nibble lookups in 16-entry tables (FOLD 1: every wave-wide lookup reads 8
+// distinct dwords in 8 distinct banks, so it never conflicts) or 16 byte lookups in
+// 256-entry tables (FOLD 0: random banks) -- and carries a running register across the
+// tiles (A^1024 between tiles).  A
 // Hillis-Steele scan over the 64 lanes (A^(16*2^j) per level) leaves the segment's value,
 // relative to the segment's end, in lane 63; shifting it by (S - segment end) mod 32767
 // bytes places it relative to the row's end, and one atomic XOR adds it into the row's
@@ -354,17 +357,20 @@ __device__ __forceinline__ u32x4 crc_chunk_load(const uint8_t* row, uint64_t off
     return v;
 }
 
-template <bool ALIGNED>
+template <bool ALIGNED, int FOLD>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
                                                             uint64_t out_bs) {
-    __shared__ uint32_t s_tbl[kCrcTableWords];
-    for (int i = threadIdx.x; i < kCrcTableWords; i += kWG) s_tbl[i] = tbl[i];
+    constexpr int kFoldWords = FOLD == 0 ? kCrcUWords : kCrcNWords;
+    constexpr int kFoldOff = FOLD == 0 ? kCrcPWords : kCrcPWords + kCrcUWords;
+    __shared__ uint32_t s_tbl[kCrcPWords + kFoldWords];
+    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
+    for (int i = threadIdx.x; i < kFoldWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kFoldOff + i];
     __syncthreads();
-    const uint16_t* sU = reinterpret_cast<const uint16_t*>(s_tbl);
-    const uint16_t* sP = sU + 16 * 256;
+    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
+    const uint16_t* sF = sP + kCrcPWords * 2;  // U[16][256] or N[32][16]
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -380,14 +386,42 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
         u32x4 v[kCrcSegTiles];
 #pragma unroll
         for (int i = 0; i < kCrcSegTiles; i++)
-            if (uint32_t(i) < nt) v[i] = crc_chunk_load<ALIGNED>(row, (uint64_t(t0 + i) * kWave + lane) * 16, S);
+            if (uint32_t(i) < nt) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
+                // wave-uniform: only a row's last tile needs the per-lane bounds and masks
+                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+                else
+                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
+            }
         uint32_t acc = 0;
 #pragma unroll
         for (int i = 0; i < kCrcSegTiles; i++) {
             if (uint32_t(i) < nt) {
                 uint32_t c = 0;
+                if constexpr (FOLD == 0) {
 #pragma unroll
-                for (int p = 0; p < 16; p++) c ^= sU[(15 - p) * 256 + ((v[i][p >> 2] >> (8 * (p & 3))) & 0xFF)];
+                    for (int p = 0; p < 16; p++) c ^= sF[(15 - p) * 256 + ((v[i][p >> 2] >> (8 * (p & 3))) & 0xFF)];
+                } else {
+                    // nibble byte offsets into the u16 tables (2 x nibble), one dword at a time
+                    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sF);
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        uint32_t lo = (v[i][w] << 1) & 0x1E1E1E1Eu, hi = (v[i][w] >> 3) & 0x1E1E1E1Eu;
+                        // opaque: keeps the two masks (else the compiler re-derives a shift
+                        // and an AND per nibble), so each offset is one byte extract
+                        asm volatile("" : "+v"(lo), "+v"(hi));
+                        uint32_t l[8];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int p = 4 * w + q;
+                            l[2 * q] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + ((lo >> (8 * q)) & 0xFF));
+                            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
+                        }
+                        // 8 lookups into the register with four 3-input XORs
+                        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+                    }
+                }
                 acc = crc_pow(sP, 10, acc) ^ c;  // previous tiles move 1 KiB further from the end
             }
         }
@@ -407,9 +441,12 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
     }
 }
 
-void* crc16_rows_kernel(bool aligned) {
-    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true>)
-                   : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false>);
+void* crc16_rows_kernel(bool aligned, int fold) {
+    if (fold == 0)
+        return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 0>)
+                       : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false, 0>);
+    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 1>)
+                   : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false, 1>);
 }
 
 // ------------------------------------------------------------------ dispatch table

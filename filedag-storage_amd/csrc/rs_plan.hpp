@@ -38,10 +38,15 @@ const ExpKernelTable& exp_kernels();
 void* generic_kernel();
 void* repitch_kernel();
 
-// CRC-16 of shard rows (crc16.hpp): device tables are U[16][256] then P[15][2][256] (u16),
-// kCrcTableWords dwords; a wave folds kCrcSegTiles 1 KiB tiles of one row.
+// CRC-16 of shard rows (crc16.hpp): the device table buffer holds P[15][2][256], then
+// U[16][256], then N[32][16] (u16); a wave folds kCrcSegTiles 1 KiB tiles of one row.
+// Chunk fold: 0 = one U lookup per byte (256-entry tables, bank conflicts), 1 = one N
+// lookup per nibble (16-entry tables: each lookup touches 8 distinct banks, conflict-free).
 constexpr int kCrcSegTiles = 8;
-constexpr int kCrcTableWords = (16 * 256 + 15 * 2 * 256) / 2;
-void* crc16_rows_kernel(bool aligned);
+constexpr int kCrcPWords = 15 * 2 * 256 / 2;
+constexpr int kCrcUWords = 16 * 256 / 2;
+constexpr int kCrcNWords = 32 * 16 / 2;
+constexpr int kCrcTableWords = kCrcPWords + kCrcUWords + kCrcNWords;
+void* crc16_rows_kernel(bool aligned, int fold);
 
 }  // namespace rsmi

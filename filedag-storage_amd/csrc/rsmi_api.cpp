@@ -73,6 +73,7 @@ struct rsmi_ctx {
     long opt_waves_per_cu = 0;
     int opt_prefetch = 0;
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
+    int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
     std::string last_kernel;
 };
 
@@ -463,6 +464,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "zero_copy")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
+    } else if (!std::strcmp(key, "crc_fold")) {
+        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_crc_fold = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;
@@ -611,10 +615,11 @@ uint8_t* host_alias(void* p, size_t len) {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.U) + sizeof(t.P) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.U) + sizeof(t.N) == size_t(kCrcTableWords) * 4, "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
-    std::memcpy(h.data(), t.U, sizeof(t.U));
-    std::memcpy(h.data() + 16 * 256, t.P, sizeof(t.P));
+    std::memcpy(h.data(), t.P, sizeof(t.P));
+    std::memcpy(h.data() + kCrcPWords * 2, t.U, sizeof(t.U));
+    std::memcpy(h.data() + (kCrcPWords + kCrcUWords) * 2, t.N, sizeof(t.N));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -629,7 +634,7 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
     if (S == 0) return RSMI_OK;  // R(empty) = 0
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = crc16_rows_kernel(aligned);
+    void* fn = crc16_rows_kernel(aligned, c->opt_crc_fold);
     const uint64_t tile = uint64_t(kWave) * 16;
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;

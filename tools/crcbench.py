@@ -22,24 +22,26 @@ def main():
         p = rsmi.recommended_pitch(S)
         buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
         out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
-        c = rsmi.Codec(k, m)
-        f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
-        t_end = time.perf_counter() + 0.2
-        while time.perf_counter() < t_end:
-            f()
-            torch.cuda.synchronize()
-        ts = []
-        for _ in range(20):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            f()
-            e1.record(st)
-            e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        med = statistics.median(ts)
-        print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S}: {med * 1e3:8.1f} us  "
-              f"{nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
-        c.close()
+        for fold in (1, 0):
+            c = rsmi.Codec(k, m)
+            c.set_option("crc_fold", fold)
+            f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
+            t_end = time.perf_counter() + 0.2
+            while time.perf_counter() < t_end:
+                f()
+                torch.cuda.synchronize()
+            ts = []
+            for _ in range(20):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                f()
+                e1.record(st)
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} fold={'nibble' if fold else 'byte'}: "
+                  f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
+            c.close()
 
 
 if __name__ == "__main__":
