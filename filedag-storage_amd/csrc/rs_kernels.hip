@@ -56,7 +56,10 @@ constexpr int default_prefetch() {
 // loads and stores, 1 = nontemporal loads and stores, 2 = nontemporal loads, default stores),
 // PF rows in flight per lane (0 = default_prefetch), WPS waves per SIMD the register
 // allocation must allow.
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd>
+// TS: table source.  0 = all five field words per output from LDS (broadcast
+// ds_read_b128); 1 = fields 0 and 2 from LDS, fields 1, 3 and 4 by scalar loads into SGPRs
+// (each v_perm takes one SGPR operand), cutting the LDS return traffic by 3/5.
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -130,8 +133,23 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         asm volatile("" : "+v"(tb));
         const u32x4* tbl = s_tbl + tb;
         u32x4 Tn[5];
+        auto load_tables = [&](int c, u32x4 (&dst)[5]) {
+            if constexpr (TS == 0) {
 #pragma unroll
-        for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
+                for (int f = 0; f < 5; f++) dst[f] = tbl[c * 5 + f];
+            } else {
+                dst[0] = tbl[c * 5 + 0];
+                dst[2] = tbl[c * 5 + 2];
+                const u32x4* g = reinterpret_cast<const u32x4*>(plan->tbl) + c * 5;
+#pragma unroll
+                for (int f : {1, 3, 4}) {
+                    const u32x4 w = g[f];  // uniform address: s_load_dwordx4
+#pragma unroll
+                    for (int j = 0; j < 4; j++) dst[f][j] = __builtin_amdgcn_readfirstlane(w[j]);
+                }
+            }
+        };
+        load_tables(0, Tn);
 
 #pragma unroll
         for (int c = 0; c < K; c++) {
@@ -180,10 +198,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                     }
                 }
             if (c + P < K) load_col(c + P, v[slot]);
-            if (c + 1 < K) {
-#pragma unroll
-                for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
-            }
+            if (c + 1 < K) load_tables(c + 1, Tn);
             __builtin_amdgcn_sched_barrier(0);
         }
         // Anchor the results outside the store predicate; otherwise the compiler sinks the
@@ -450,9 +465,9 @@ void* crc16_rows_kernel(bool aligned, int fold) {
 }
 
 // ------------------------------------------------------------------ dispatch table
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd>
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS>);
 }
 
 template <int K, int D, int NT>
@@ -487,6 +502,8 @@ const ExpKernelTable& exp_kernels() {
         x.fn[1][0] = fast_ptr<10, 1, 1, 1, 4>();
         x.fn[1][1] = fast_ptr<10, 1, 1, 1, 8>();
         x.fn[1][2] = fast_ptr<10, 1, 1, 1, 10>();
+        x.fn[0][3] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 1>();
+        x.fn[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 1>();
         return x;
     }();
     return t;

@@ -27,10 +27,11 @@ struct FastKernelTable {
     void* fn[17][kMaxMT + 1][3][3];
 };
 
-// Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1, NT=1);
-// v 0/1/2 = 4/8/10 rows in flight.
+// Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1);
+// v 0/1/2 = 4/8/10 rows in flight (NT=1); v 3 = split table source (TS=1; NT 1 for MT4,
+// 2 for MT1, the auto policy's choices).
 struct ExpKernelTable {
-    void* fn[2][3];
+    void* fn[2][4];
 };
 
 const FastKernelTable& fast_kernels();

@@ -74,6 +74,7 @@ struct rsmi_ctx {
     int opt_prefetch = 0;
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
+    int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
     std::string last_kernel;
 };
 
@@ -250,11 +251,15 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
         const int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
         void* fn = nullptr;
         if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
-        int pf_label = 0;
+        int pf_label = 0, ts_label = 0;
         if (fn && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
             const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][pi];
             pf_label = c->opt_prefetch;
+        } else if (fn && c->opt_tables == 1 && t.K == 10 && D == 1 &&
+                   ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
+            fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][3];
+            ts_label = 1;
         }
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
@@ -281,6 +286,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             }
             c->last_kernel = kernel_label(t.K, t.MT, D, NT, true);
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
+            if (ts_label) c->last_kernel += ",TS=1";
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -464,6 +470,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "zero_copy")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
+    } else if (!std::strcmp(key, "tables")) {
+        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_tables = int(value);
     } else if (!std::strcmp(key, "crc_fold")) {
         if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
         c->opt_crc_fold = int(value);

@@ -183,7 +183,8 @@ int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t
  * host batch calls write results with kernel stores over PCIe instead of a device->host
  * copy, and reconstruct reads its k input rows with kernel loads; 2 = encode also uploads
  * by kernel loads (A/B); 0 = always copy), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
-(default), 0 = byte tables (A/B)).  Returns
+(default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
+table fields into SGPRs by scalar loads instead of LDS (A/B)).  Returns
  * RSMI_ERR_INVALID_ARG for unknown keys or values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */
