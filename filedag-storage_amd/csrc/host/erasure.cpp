@@ -96,7 +96,7 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     Bytes flat(size_t(n) * S);
-    rc = rsmi_encode_block(c, data.data(), data.size(), flat.data());
+    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat.data(), nullptr);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
     return Status::Ok();
@@ -113,7 +113,7 @@ Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards,
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     Bytes flat(size_t(n) * S);
     raw->assign(size_t(n), 0);
-    rc = rsmi_encode_block_crc(c, data.data(), data.size(), flat.data(), raw->data());
+    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat.data(), raw->data());
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
     return Status::Ok();

@@ -56,6 +56,8 @@ inline size_t staging_blocks(size_t block_bytes) {
 class Erasure {
 public:
     static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);
+    // through rsmi_encode_block_coalesced: concurrent Puts on one process-wide context are
+    // batched on the GPU (group commit); a lone caller runs alone, unchanged
     Status EncodeData(const Bytes& data, std::vector<Bytes>* shards) const;
     // EncodeData plus R(shard) of every shard from the GPU (include/rsmi.h, datanode CRC-16);
     // raw is left empty for an empty block

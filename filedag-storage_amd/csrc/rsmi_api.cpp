@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,7 +77,25 @@ struct rsmi_ctx {
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
     int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
+    long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
+    long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;
+    // group commit for rsmi_encode_block_coalesced (see there)
+    struct CoalReq {
+        const uint8_t* block;
+        size_t B;
+        uint8_t* out;
+        uint32_t* raw;
+        int rc;
+        bool done;
+    };
+    std::mutex q_mu;
+    std::condition_variable q_cv;
+    std::vector<CoalReq*> q_pending;
+    bool q_executing = false;
+    uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
+    size_t h_coal_cap = 0;
+    std::atomic<uint64_t> stat_coal_calls{0}, stat_coal_batches{0};
 };
 
 namespace {
@@ -394,6 +414,7 @@ void rsmi_close(rsmi_ctx* c) {
                 if (s.stream) (void)hipStreamDestroy(s.stream);
             }
             if (c->h_stage) (void)hipHostFree(c->h_stage);
+            if (c->h_coal) (void)hipHostFree(c->h_coal);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
         }
@@ -473,6 +494,12 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "tables")) {
         if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
+    } else if (!std::strcmp(key, "coalesce_us")) {
+        if (value < 0 || value > 100000) return RSMI_ERR_INVALID_ARG;
+        c->opt_coalesce_us = value;
+    } else if (!std::strcmp(key, "coalesce_max")) {
+        if (value < 1 || value > 65536) return RSMI_ERR_INVALID_ARG;
+        c->opt_coalesce_max = value;
     } else if (!std::strcmp(key, "crc_fold")) {
         if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
         c->opt_crc_fold = int(value);
@@ -778,6 +805,103 @@ int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* 
     std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
     return encode_host_impl(c, shards_out, size_t(c->k) * S, shards_out + size_t(c->k) * S, size_t(c->m) * S, S, 1,
                             raw_out);
+}
+
+// ---------------------------------------------------------------- coalesced single blocks
+// DagNode.Put hands the engine one block per call (node.go:358-408), from many goroutines at
+// once.  Group commit turns those calls into GPU batches without a thread of our own: a
+// caller that finds no batch executing becomes the executor, takes every block queued so
+// far (optionally waiting coalesce_us for more), runs them as rsmi_encode_batch_host(_crc)
+// calls grouped by shard size, and wakes their callers.  Blocks that arrive while a batch
+// runs queue up and form the next batch.  A lone caller never waits: its batch is itself.
+static int run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    std::map<size_t, std::vector<rsmi_ctx::CoalReq*>> by_s;
+    for (auto* r : batch) by_s[rsmi_shard_size(r->B, c->k)].push_back(r);
+    for (auto& g : by_s) {
+        const size_t S = g.first;
+        const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
+        for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk) {
+            const size_t nb = std::min(chunk, g.second.size() - j0);
+            rsmi_ctx::CoalReq* const* rq = g.second.data() + j0;
+            const size_t need = nb * n * S;
+            if (c->h_coal_cap < need) {
+                if (c->h_coal) (void)hipHostFree(c->h_coal);
+                c->h_coal = nullptr;
+                c->h_coal_cap = 0;
+                if (hipHostMalloc(reinterpret_cast<void**>(&c->h_coal), need, hipHostMallocDefault) != hipSuccess) {
+                    (void)hipGetLastError();
+                    for (size_t j = 0; j < nb; j++) rq[j]->rc = RSMI_ERR_DEVICE;
+                    continue;
+                }
+                c->h_coal_cap = need;
+            }
+            bool want_raw = false;
+            for (size_t j = 0; j < nb; j++) {
+                uint8_t* dst = c->h_coal + j * n * S;
+                std::memcpy(dst, rq[j]->block, rq[j]->B);
+                std::memset(dst + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
+                want_raw |= rq[j]->raw != nullptr;
+            }
+            std::vector<uint32_t> raw(want_raw ? nb * n : 0);
+            const int rc = encode_host_impl(c, c->h_coal, n * S, c->h_coal + k * S, n * S, S, nb,
+                                            want_raw ? raw.data() : nullptr);
+            for (size_t j = 0; j < nb; j++) {
+                rq[j]->rc = rc;
+                if (rc) continue;
+                std::memcpy(rq[j]->out, c->h_coal + j * n * S, n * S);
+                if (rq[j]->raw) std::memcpy(rq[j]->raw, raw.data() + j * n, n * 4);
+            }
+        }
+    }
+    return RSMI_OK;
+}
+
+int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                uint32_t* raw_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        int rc = ensure_device(c);
+        if (rc) return rc;
+    }
+    rsmi_ctx::CoalReq req{block, B, shards_out, raw_out, RSMI_OK, false};
+    c->stat_coal_calls++;
+    std::unique_lock<std::mutex> lk(c->q_mu);
+    c->q_pending.push_back(&req);
+    c->q_cv.notify_all();  // an executor waiting out coalesce_us may now have enough
+    while (!req.done) {
+        if (c->q_executing) {
+            c->q_cv.wait(lk);
+            continue;
+        }
+        c->q_executing = true;
+        const size_t cap = size_t(c->opt_coalesce_max);
+        if (c->opt_coalesce_us > 0 && c->q_pending.size() < cap)
+            c->q_cv.wait_for(lk, std::chrono::microseconds(c->opt_coalesce_us),
+                             [&] { return c->q_pending.size() >= cap; });
+        std::vector<rsmi_ctx::CoalReq*> batch;
+        const size_t take = std::min(cap, c->q_pending.size());
+        batch.assign(c->q_pending.begin(), c->q_pending.begin() + take);
+        c->q_pending.erase(c->q_pending.begin(), c->q_pending.begin() + take);
+        lk.unlock();
+        run_coalesced(c, batch);
+        c->stat_coal_batches++;
+        lk.lock();
+        for (auto* r : batch) r->done = true;
+        c->q_executing = false;
+        c->q_cv.notify_all();
+    }
+    return req.rc;
+}
+
+long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
+    if (!c || !key) return -1;
+    if (!std::strcmp(key, "coalesced_calls")) return long(c->stat_coal_calls.load());
+    if (!std::strcmp(key, "coalesced_batches")) return long(c->stat_coal_batches.load());
+    return -1;
 }
 
 int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,

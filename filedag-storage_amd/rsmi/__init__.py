@@ -79,6 +79,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_host_free": (None, [ctypes.c_void_p]),
         "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
         "rsmi_reconstruct_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, ctypes.c_int, ctypes.c_void_p]),
+        "rsmi_encode_block_coalesced": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
+        "rsmi_get_stat": (ctypes.c_long, [ctypes.c_void_p, ctypes.c_char_p]),
         "rsmi_crc16_ibm": (ctypes.c_uint16, [u8p, c_size]),
         "rsmi_crc16_entry": (ctypes.c_uint16, [u8p, c_size, ctypes.c_uint32, c_size]),
         "rsmi_crc16_rows_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, ctypes.c_int, c_size, c_size,
@@ -213,6 +215,19 @@ class Codec:
         _check(lib().rsmi_encode_block_crc(self._h, ctypes.addressof(_buf(src)) if src else None, len(block),
                                            ctypes.addressof(_buf(out)) if out else None, raw))
         return bytes(out), list(raw)
+
+    def encode_block_coalesced(self, block: bytes, want_raw: bool = False):
+        """encode_block, batched with concurrent callers on this context (group commit)."""
+        S = lib().rsmi_shard_size(len(block), self.k)
+        out = bytearray(self.n * S)
+        src = bytearray(block)
+        raw = (ctypes.c_uint32 * self.n)() if want_raw else None
+        _check(lib().rsmi_encode_block_coalesced(self._h, ctypes.addressof(_buf(src)) if src else None, len(block),
+                                                 ctypes.addressof(_buf(out)) if out else None, raw))
+        return (bytes(out), list(raw)) if want_raw else bytes(out)
+
+    def stat(self, key: str) -> int:
+        return lib().rsmi_get_stat(self._h, key.encode())
 
     def encode_batch_host_crc_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
                                   nblocks: int, raw_ptr: int) -> None:

@@ -140,6 +140,19 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
                                     size_t S, size_t nblocks, const uint8_t* present, const uint8_t* required,
                                     void* stream);
 
+/* Erasure.EncodeData for one block (same output as rsmi_encode_block, plus R(shard) in
+ * raw_out[0..k+m) when raw_out is not NULL), coalesced with concurrent callers on the same
+ * context: DagNode.Put runs once per block from many goroutines (node.go:358-408), and
+ * group commit turns those calls into GPU batches.  The caller that finds no batch running
+ * executes every block queued so far (waiting up to option "coalesce_us" for more, default
+ * 0; at most "coalesce_max" blocks, default 256) and wakes the others; blocks arriving
+ * meanwhile form the next batch.  A lone caller never waits on anyone. */
+int rsmi_encode_block_coalesced(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                uint32_t* raw_out);
+
+/* Counters: "coalesced_calls", "coalesced_batches".  -1 for an unknown key. */
+long rsmi_get_stat(const rsmi_ctx* ctx, const char* key);
+
 /* ------------------------------------------------------------------ datanode CRC-16 */
 
 /* The datanode stores every shard as |crc (4 LE)|meta size|data size|meta|data| with
@@ -184,7 +197,8 @@ int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t
  * copy, and reconstruct reads its k input rows with kernel loads; 2 = encode also uploads
  * by kernel loads (A/B); 0 = always copy), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
 (default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
-table fields into SGPRs by scalar loads instead of LDS (A/B)).  Returns
+table fields into SGPRs by scalar loads instead of LDS (A/B)), "coalesce_us" / "coalesce_max"
+(rsmi_encode_block_coalesced).  Returns
  * RSMI_ERR_INVALID_ARG for unknown keys or values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */

@@ -12,6 +12,7 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../filedag-storage_amd/csrc/host/dagnode.hpp"
@@ -491,6 +492,51 @@ static void test_gpu_entry_checksums() {
     }
 }
 
+// Concurrent DagNode.Put from many threads (the reference's goroutine-per-request Dag Pool):
+// the per-block encodes coalesce into GPU batches (rsmi_encode_block_coalesced), and every
+// stored shard and entry checksum still equals the oracle's.
+static void test_concurrent_puts() {
+    const int k = 10, m = 4, n = k + m;
+    Cluster c(k, m);
+    const int T = 12, per = 10;
+    std::vector<std::string> keys(size_t(T * per));
+    std::vector<Bytes> blocks(size_t(T * per));
+    std::mt19937_64 r(99);
+    for (int i = 0; i < T * per; i++) {
+        keys[i] = "conc-" + std::to_string(i);
+        blocks[i] = rand_bytes(r, i % 7 == 0 ? 4099 : 262144);
+    }
+    int rc;
+    rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
+    CHECK(ctx != nullptr);
+    const long calls0 = rsmi_get_stat(ctx, "coalesced_calls"), batches0 = rsmi_get_stat(ctx, "coalesced_batches");
+    std::vector<std::thread> th;
+    std::vector<Status> st(size_t(T * per));
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (int j = 0; j < per; j++) st[size_t(t * per + j)] = c.node->Put(keys[t * per + j], blocks[t * per + j]);
+        });
+    for (auto& x : th) x.join();
+    const long calls = rsmi_get_stat(ctx, "coalesced_calls") - calls0;
+    const long batches = rsmi_get_stat(ctx, "coalesced_batches") - batches0;
+    CHECK(calls == T * per);
+    CHECK(batches >= 1 && batches <= calls);
+    std::printf("concurrent puts: %ld encodes in %ld GPU batches\n", calls, batches);
+    for (int i = 0; i < T * per; i++) {
+        CHECK_OK(st[i]);
+        auto want = oracle_shards(k, m, blocks[i]);
+        Bytes meta(4);
+        for (int b = 0; b < 4; b++) meta[b] = uint8_t(uint32_t(blocks[i].size()) >> (8 * b));
+        for (int s = 0; s < n; s++) {
+            CHECK(stored_shard(*c.dn[s], keys[i]) == want[s]);
+            Bytes e;
+            CHECK(c.dn[s]->server().RawEntry(keys[i], &e));
+            const uint32_t crc = uint32_t(e[0]) | uint32_t(e[1]) << 8 | uint32_t(e[2]) << 16 | uint32_t(e[3]) << 24;
+            CHECK(crc == rs_oracle_datanode_entry_crc(meta.data(), 4, want[s].data(), want[s].size()));
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (rs_oracle_selftest() != 0) {
@@ -512,6 +558,7 @@ int main(int argc, char** argv) {
         test_batches_span_staging_chunks();
         test_migrate();
         test_gpu_entry_checksums();
+        test_concurrent_puts();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
     return g_fail ? 1 : 0;

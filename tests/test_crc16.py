@@ -175,3 +175,59 @@ def test_encode_block_crc(B):
         row = shards[i * S:(i + 1) * S]
         assert rsmi.crc16_entry(b"", raw[i], S) == orc.crc16_ibm(row)
     assert shards[:B] == block
+
+
+@pytest.mark.gpu
+def test_coalesced_encode_concurrent_callers():
+    """rsmi_encode_block_coalesced from 16 threads at once (DagNode.Put's shape): every block's
+    shards and raw CRCs equal the oracle's, mixed block sizes batch by shard size, and the
+    calls were coalesced into fewer GPU batches than calls."""
+    import threading
+
+    k, m = 10, 4
+    n = k + m
+    rng = np.random.default_rng(21)
+    sizes = [262144] * 40 + [262143] * 8 + [6, 1, 4099, 1048576]
+    blocks = [bytes(rng.integers(0, 256, size=B, dtype=np.uint8)) for B in sizes]
+    out = [None] * len(blocks)
+    with rsmi.Codec(k, m) as c:
+        c.set_option("coalesce_us", 200)
+        nxt = [0]
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= len(blocks):
+                    return
+                out[i] = c.encode_block_coalesced(blocks[i], want_raw=(i % 2 == 0))
+
+        th = [threading.Thread(target=worker) for _ in range(16)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        calls, batches = c.stat("coalesced_calls"), c.stat("coalesced_batches")
+    assert calls == len(blocks)
+    assert 1 <= batches < calls
+    for i, B in enumerate(sizes):
+        S = (B + k - 1) // k
+        got = out[i][0] if i % 2 == 0 else out[i]
+        want = orc.split(k, m, blocks[i])
+        want[k:] = orc.encode(k, m, want[:k])
+        assert got == want.tobytes(), i
+        if i % 2 == 0:
+            for r in range(n):
+                assert rsmi.crc16_entry(b"", out[i][1][r], S) == orc.crc16_ibm(want[r].tobytes())
+
+
+@pytest.mark.gpu
+def test_coalesced_encode_lone_caller_and_errors():
+    with rsmi.Codec(4, 2) as c:
+        assert c.encode_block_coalesced(b"123456") == c.encode_block(b"123456")
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.encode_block_coalesced(b"")
+        assert e.value.code == rsmi.ErrShortData
+        assert c.stat("coalesced_batches") == 1

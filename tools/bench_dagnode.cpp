@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdio>
 #include <random>
+#include <thread>
 
 #include "../filedag-storage_amd/csrc/host/dagnode.hpp"
 
@@ -57,6 +58,27 @@ int main(int argc, char** argv) {
     t0 = clk::now();
     d->PutMany(keys, blocks);
     const double putb = secs(t0);
+    // Put from 16 threads at once: the per-block encodes coalesce into GPU batches
+    const int T = 16;
+    long c0 = 0, b0 = 0;
+    int rc;
+    rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
+    if (ctx) {
+        c0 = rsmi_get_stat(ctx, "coalesced_calls");
+        b0 = rsmi_get_stat(ctx, "coalesced_batches");
+    }
+    t0 = clk::now();
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                for (int i = t; i < N; i += T) d->Put(keys[i], blocks[i]);
+            });
+        for (auto& x : th) x.join();
+    }
+    const double putT = secs(t0);
+    const long calls = ctx ? rsmi_get_stat(ctx, "coalesced_calls") - c0 : 0;
+    const long batches = ctx ? rsmi_get_stat(ctx, "coalesced_batches") - b0 : 0;
     // CRC + framing alone (the datanode's byte-serial CPU loop), for context
     t0 = clk::now();
     volatile uint16_t sink = 0;
@@ -86,6 +108,8 @@ int main(int argc, char** argv) {
     std::printf("RS(%d,%d) %d blocks x %zu B (%.2f GiB payload), in-process datanodes\n", k, m, N, B, gib);
     std::printf("Put per block      %8.2f GiB/s (datanode CRC: %.2f)\n", gib / put1, gib / put1h);
     std::printf("PutMany (batched)  %8.2f GiB/s (datanode CRC: %.2f)\n", gib / putb, gib / putbh);
+    std::printf("Put, %d threads    %8.2f GiB/s (%ld encodes in %ld coalesced GPU batches)\n", T, gib / putT, calls,
+                batches);
     std::printf("Get, 1 lost shard  %8.2f GiB/s\nGetMany (batched)  %8.2f GiB/s\n", gib / get1, gib / getb);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);
