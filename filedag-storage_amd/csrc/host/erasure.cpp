@@ -143,7 +143,8 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
     Bytes flat(size_t(n) * S);  // [][]byte -> one contiguous buffer for the C-ABI
     for (int i = 0; i < n; i++)
         if (present[i]) std::memcpy(flat.data() + size_t(i) * S, shards[i].data(), S);
-    rc = rsmi_reconstruct(c, flat.data(), S, present.data(), data_only ? 1 : 0);
+    // coalesced: concurrent degraded Gets usually miss the same node's shard, so they batch
+    rc = rsmi_reconstruct_coalesced(c, flat.data(), S, present.data(), data_only ? 1 : 0);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++)
         if (!present[i] && (i < data_blocks_ || !data_only))

@@ -82,10 +82,13 @@ struct rsmi_ctx {
     std::string last_kernel;
     // group commit for rsmi_encode_block_coalesced (see there)
     struct CoalReq {
+        // encode: block/B in, out = (k+m)*S shards, raw optional; reconstruct: out = n*S
+        // shards in place, present / want flags (group key covers S, pattern, want)
         const uint8_t* block;
         size_t B;
         uint8_t* out;
         uint32_t* raw;
+        std::string key;
         int rc;
         bool done;
     };
@@ -814,60 +817,89 @@ int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* 
 // far (optionally waiting coalesce_us for more), runs them as rsmi_encode_batch_host(_crc)
 // calls grouped by shard size, and wakes their callers.  Blocks that arrive while a batch
 // runs queue up and form the next batch.  A lone caller never waits: its batch is itself.
-static int run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
-    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
-    std::map<size_t, std::vector<rsmi_ctx::CoalReq*>> by_s;
-    for (auto* r : batch) by_s[rsmi_shard_size(r->B, c->k)].push_back(r);
-    for (auto& g : by_s) {
-        const size_t S = g.first;
-        const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
-        for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk) {
-            const size_t nb = std::min(chunk, g.second.size() - j0);
-            rsmi_ctx::CoalReq* const* rq = g.second.data() + j0;
-            const size_t need = nb * n * S;
-            if (c->h_coal_cap < need) {
-                if (c->h_coal) (void)hipHostFree(c->h_coal);
-                c->h_coal = nullptr;
-                c->h_coal_cap = 0;
-                if (hipHostMalloc(reinterpret_cast<void**>(&c->h_coal), need, hipHostMallocDefault) != hipSuccess) {
-                    (void)hipGetLastError();
-                    for (size_t j = 0; j < nb; j++) rq[j]->rc = RSMI_ERR_DEVICE;
-                    continue;
-                }
-                c->h_coal_cap = need;
-            }
-            bool want_raw = false;
-            for (size_t j = 0; j < nb; j++) {
-                uint8_t* dst = c->h_coal + j * n * S;
-                std::memcpy(dst, rq[j]->block, rq[j]->B);
-                std::memset(dst + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
-                want_raw |= rq[j]->raw != nullptr;
-            }
-            std::vector<uint32_t> raw(want_raw ? nb * n : 0);
-            const int rc = encode_host_impl(c, c->h_coal, n * S, c->h_coal + k * S, n * S, S, nb,
-                                            want_raw ? raw.data() : nullptr);
-            for (size_t j = 0; j < nb; j++) {
-                rq[j]->rc = rc;
-                if (rc) continue;
-                std::memcpy(rq[j]->out, c->h_coal + j * n * S, n * S);
-                if (rq[j]->raw) std::memcpy(rq[j]->raw, raw.data() + j * n, n * 4);
-            }
-        }
+static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                 const uint8_t* present, const uint8_t* want);
+
+// page-locked staging of the executing batch (only the executor touches it)
+static uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
+    if (c->h_coal_cap >= need) return c->h_coal;
+    if (c->h_coal) (void)hipHostFree(c->h_coal);
+    c->h_coal = nullptr;
+    c->h_coal_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_coal), need, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
     }
-    return RSMI_OK;
+    c->h_coal_cap = need;
+    return c->h_coal;
 }
 
-int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
-                                uint32_t* raw_out) {
-    if (!c) return RSMI_ERR_INVALID_ARG;
-    if (B == 0) return RSMI_ERR_SHORT_DATA;
-    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+// One group of a coalesced batch: same request key, i.e. same kind and shard size (and,
+// for reconstruct, the same survivor pattern and requested rows).
+static void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    const std::string& key = rq[0]->key;
+    const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
+    uint8_t* h = coal_stage(c, nb * n * S);
+    if (!h) {
+        for (size_t j = 0; j < nb; j++) rq[j]->rc = RSMI_ERR_DEVICE;
+        return;
+    }
+    if (key[0] == 'E') {
+        bool want_raw = false;
+        for (size_t j = 0; j < nb; j++) {
+            uint8_t* dst = h + j * n * S;
+            std::memcpy(dst, rq[j]->block, rq[j]->B);
+            std::memset(dst + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
+            want_raw |= rq[j]->raw != nullptr;
+        }
+        std::vector<uint32_t> raw(want_raw ? nb * n : 0);
+        const int rc = encode_host_impl(c, h, n * S, h + k * S, n * S, S, nb, want_raw ? raw.data() : nullptr);
+        for (size_t j = 0; j < nb; j++) {
+            rq[j]->rc = rc;
+            if (rc) continue;
+            std::memcpy(rq[j]->out, h + j * n * S, n * S);
+            if (rq[j]->raw) std::memcpy(rq[j]->raw, raw.data() + j * n, n * 4);
+        }
+        return;
+    }
+    // 'R': key = "R<S>:<n flags present><n flags want>"
+    const char* f = key.c_str() + key.find(':') + 1;
+    std::vector<uint8_t> present(n), want(n);
+    for (size_t i = 0; i < n; i++) {
+        present[i] = uint8_t(f[i] == '1');
+        want[i] = uint8_t(f[n + i] == '1');
+    }
+    for (size_t j = 0; j < nb; j++) std::memcpy(h + j * n * S, rq[j]->out, n * S);
+    const int rc = reconstruct_host_impl(c, h, n * S, S, nb, present.data(), want.data());
+    for (size_t j = 0; j < nb; j++) {
+        rq[j]->rc = rc;
+        if (rc) continue;
+        for (size_t i = 0; i < n; i++)
+            if (!present[i] && want[i]) std::memcpy(rq[j]->out + i * S, h + (j * n + i) * S, S);
+    }
+}
+
+static void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
+    const size_t n = size_t(c->n);
+    std::map<std::string, std::vector<rsmi_ctx::CoalReq*>> groups;
+    for (auto* r : batch) groups[r->key].push_back(r);
+    for (auto& g : groups) {
+        const std::string& key = g.first;
+        const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
+        const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
+        for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk)
+            run_coalesced_group(c, g.second.data() + j0, std::min(chunk, g.second.size() - j0));
+    }
+}
+
+// Queue a request and either wait for the executor or become it (group commit).
+static int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
     {
         std::lock_guard<std::mutex> g(c->mu);
         int rc = ensure_device(c);
         if (rc) return rc;
     }
-    rsmi_ctx::CoalReq req{block, B, shards_out, raw_out, RSMI_OK, false};
     c->stat_coal_calls++;
     std::unique_lock<std::mutex> lk(c->q_mu);
     c->q_pending.push_back(&req);
@@ -882,9 +914,8 @@ int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uin
         if (c->opt_coalesce_us > 0 && c->q_pending.size() < cap)
             c->q_cv.wait_for(lk, std::chrono::microseconds(c->opt_coalesce_us),
                              [&] { return c->q_pending.size() >= cap; });
-        std::vector<rsmi_ctx::CoalReq*> batch;
         const size_t take = std::min(cap, c->q_pending.size());
-        batch.assign(c->q_pending.begin(), c->q_pending.begin() + take);
+        std::vector<rsmi_ctx::CoalReq*> batch(c->q_pending.begin(), c->q_pending.begin() + take);
         c->q_pending.erase(c->q_pending.begin(), c->q_pending.begin() + take);
         lk.unlock();
         run_coalesced(c, batch);
@@ -895,6 +926,30 @@ int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uin
         c->q_cv.notify_all();
     }
     return req.rc;
+}
+
+int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                uint32_t* raw_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+    rsmi_ctx::CoalReq req{block, B, shards_out, raw_out, "E" + std::to_string(rsmi_shard_size(B, c->k)) + ":",
+                          RSMI_OK, false};
+    return coalesce(c, req);
+}
+
+int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+    if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    const std::vector<uint8_t> want = want_mask(c, present, data_only);
+    int pre = reconstruct_precheck(c, present, want.data());
+    if (pre < 0) return -pre;
+    if (pre == 1) return RSMI_OK;
+    std::string key = "R" + std::to_string(S) + ":";
+    for (int i = 0; i < c->n; i++) key.push_back(present[i] ? '1' : '0');
+    for (int i = 0; i < c->n; i++) key.push_back(want[i] ? '1' : '0');
+    rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, std::move(key), RSMI_OK, false};
+    return coalesce(c, req);
 }
 
 long rsmi_get_stat(const rsmi_ctx* c, const char* key) {

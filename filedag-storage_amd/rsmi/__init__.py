@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
         "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
         "rsmi_reconstruct_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, ctypes.c_int, ctypes.c_void_p]),
         "rsmi_encode_block_coalesced": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
+        "rsmi_reconstruct_coalesced": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_int]),
         "rsmi_get_stat": (ctypes.c_long, [ctypes.c_void_p, ctypes.c_char_p]),
         "rsmi_crc16_ibm": (ctypes.c_uint16, [u8p, c_size]),
         "rsmi_crc16_entry": (ctypes.c_uint16, [u8p, c_size, ctypes.c_uint32, c_size]),
@@ -225,6 +226,12 @@ class Codec:
         _check(lib().rsmi_encode_block_coalesced(self._h, ctypes.addressof(_buf(src)) if src else None, len(block),
                                                  ctypes.addressof(_buf(out)) if out else None, raw))
         return (bytes(out), list(raw)) if want_raw else bytes(out)
+
+    def reconstruct_coalesced(self, shards: bytearray, S: int, present: Sequence[bool], data_only: bool) -> None:
+        """reconstruct, batched with concurrent callers on this context (group commit)."""
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_reconstruct_coalesced(self._h, ctypes.addressof(_buf(shards)), S,
+                                                ctypes.addressof(_buf(p)), 1 if data_only else 0))
 
     def stat(self, key: str) -> int:
         return lib().rsmi_get_stat(self._h, key.encode())

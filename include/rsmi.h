@@ -150,7 +150,14 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
 int rsmi_encode_block_coalesced(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out,
                                 uint32_t* raw_out);
 
-/* Counters: "coalesced_calls", "coalesced_batches".  -1 for an unknown key. */
+/* rsmi_reconstruct (same arguments, results and errors), coalesced the same way.  When a
+ * datanode is down every concurrent DagNode.Get misses the same shard (node.go:277-282), so
+ * concurrent degraded reads share one erasure pattern and batch into one launch; requests
+ * with different shard sizes or patterns run as separate groups of the same batch. */
+int rsmi_reconstruct_coalesced(rsmi_ctx* ctx, uint8_t* shards, size_t S, const uint8_t* present, int data_only);
+
+/* Counters: "coalesced_calls", "coalesced_batches" (both coalesced entry points).  -1 for an
+ * unknown key. */
 long rsmi_get_stat(const rsmi_ctx* ctx, const char* key);
 
 /* ------------------------------------------------------------------ datanode CRC-16 */

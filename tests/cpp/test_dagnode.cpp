@@ -522,6 +522,26 @@ static void test_concurrent_puts() {
     CHECK(calls == T * per);
     CHECK(batches >= 1 && batches <= calls);
     std::printf("concurrent puts: %ld encodes in %ld GPU batches\n", calls, batches);
+    // degraded Gets from the same threads with data shard 2's node down: one erasure
+    // pattern, so the per-key reconstructs coalesce; every block must come back intact
+    c.dn[2]->SetOffline(true);
+    const long rc0 = rsmi_get_stat(ctx, "coalesced_calls"), rb0 = rsmi_get_stat(ctx, "coalesced_batches");
+    std::vector<Bytes> got(size_t(T * per));
+    std::vector<Status> gst(size_t(T * per));
+    th.clear();
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (int j = 0; j < per; j++) gst[size_t(t * per + j)] = c.node->Get(keys[t * per + j], &got[size_t(t * per + j)]);
+        });
+    for (auto& x : th) x.join();
+    c.dn[2]->SetOffline(false);
+    const long rcalls = rsmi_get_stat(ctx, "coalesced_calls") - rc0, rbatches = rsmi_get_stat(ctx, "coalesced_batches") - rb0;
+    CHECK(rcalls == T * per);
+    std::printf("concurrent degraded gets: %ld reconstructs in %ld GPU batches\n", rcalls, rbatches);
+    for (int i = 0; i < T * per; i++) {
+        CHECK_OK(gst[i]);
+        CHECK(got[i] == blocks[i]);
+    }
     for (int i = 0; i < T * per; i++) {
         CHECK_OK(st[i]);
         auto want = oracle_shards(k, m, blocks[i]);

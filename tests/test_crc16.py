@@ -231,3 +231,57 @@ def test_coalesced_encode_lone_caller_and_errors():
             c.encode_block_coalesced(b"")
         assert e.value.code == rsmi.ErrShortData
         assert c.stat("coalesced_batches") == 1
+
+
+@pytest.mark.gpu
+def test_coalesced_reconstruct_concurrent_callers():
+    """rsmi_reconstruct_coalesced from 16 threads (concurrent degraded DagNode.Gets): two
+    erasure patterns, both data_only modes and two shard sizes in flight together; every
+    rebuilt row equals the original, present rows are untouched."""
+    import threading
+
+    k, m = 10, 4
+    n = k + m
+    rng = np.random.default_rng(5)
+    jobs = []
+    for i in range(48):
+        B = 262144 if i % 3 else 4099
+        block = bytes(rng.integers(0, 256, size=B, dtype=np.uint8))
+        sh = orc.split(k, m, block)
+        sh[k:] = orc.encode(k, m, sh[:k])
+        lost = [0] if i % 2 else [3, 11]
+        data_only = i % 4 != 1
+        work = sh.copy()
+        for r in lost:
+            work[r] = 0
+        jobs.append((sh, bytearray(work.tobytes()), [r not in lost for r in range(n)], data_only, lost))
+    with rsmi.Codec(k, m) as c:
+        c.set_option("coalesce_us", 200)
+        nxt = [0]
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    nxt[0] += 1
+                if i >= len(jobs):
+                    return
+                sh, work, present, data_only, _ = jobs[i]
+                c.reconstruct_coalesced(work, sh.shape[1], present, data_only)
+
+        th = [threading.Thread(target=worker) for _ in range(16)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert c.stat("coalesced_batches") < c.stat("coalesced_calls") == len(jobs)
+    for sh, work, present, data_only, lost in jobs:
+        got = np.frombuffer(bytes(work), dtype=np.uint8).reshape(n, -1)
+        for r in range(n):
+            if present[r]:
+                assert np.array_equal(got[r], sh[r])
+            elif r < k or not data_only:
+                assert np.array_equal(got[r], sh[r]), (lost, data_only, r)
+            else:
+                assert not got[r].any()  # ReconstructData leaves missing parity alone

@@ -94,6 +94,21 @@ int main(int argc, char** argv) {
     t0 = clk::now();
     d->GetMany(keys, &gm, &st, 256);
     const double getb = secs(t0);
+    // degraded Get from 16 threads: the reconstructs coalesce (one erasure pattern)
+    const long gc0 = ctx ? rsmi_get_stat(ctx, "coalesced_calls") : 0, gb0 = ctx ? rsmi_get_stat(ctx, "coalesced_batches") : 0;
+    t0 = clk::now();
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                Bytes b;
+                for (int i = t; i < N; i += T) d->Get(keys[i], &b);
+            });
+        for (auto& x : th) x.join();
+    }
+    const double getT = secs(t0);
+    const long gcalls = ctx ? rsmi_get_stat(ctx, "coalesced_calls") - gc0 : 0;
+    const long gbatches = ctx ? rsmi_get_stat(ctx, "coalesced_batches") - gb0 : 0;
     dn[0]->SetOffline(false);
     d->RunRepairTasks();
     dn[3]->server().Wipe();
@@ -111,6 +126,8 @@ int main(int argc, char** argv) {
     std::printf("Put, %d threads    %8.2f GiB/s (%ld encodes in %ld coalesced GPU batches)\n", T, gib / putT, calls,
                 batches);
     std::printf("Get, 1 lost shard  %8.2f GiB/s\nGetMany (batched)  %8.2f GiB/s\n", gib / get1, gib / getb);
+    std::printf("Get, %d threads    %8.2f GiB/s (%ld reconstructs in %ld coalesced GPU batches)\n", T, gib / getT,
+                gcalls, gbatches);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);
     std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes)\n", gib / crc);
