@@ -156,3 +156,36 @@ def test_null_arguments():
         assert L.rsmi_set_option(c._h, b"zero_copy", 0) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"zero_copy", 2) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"zero_copy", 3) == rsmi.ErrInvalidArg
+
+
+def test_new_options_and_stats_validate():
+    L = rsmi.lib()
+    with rsmi.Codec(10, 4) as c:
+        for key, good, bad in [(b"tables", 1, 2), (b"crc_fold", 0, 2), (b"coalesce_us", 50, -1),
+                               (b"coalesce_max", 16, 0)]:
+            assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
+            assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key
+        assert c.stat("coalesced_calls") == 0 and c.stat("coalesced_batches") == 0
+        assert c.stat("no_such_counter") == -1
+
+
+def test_coalesced_calls_fail_loudly_without_gpu():
+    """No CPU fallback on the coalesced entry points either; argument errors come first."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with rsmi.Codec(10, 4) as c:
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.encode_block_coalesced(b"x" * 100)
+        assert e.value.code == rsmi.ErrNoDevice
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.encode_block_coalesced(b"")
+        assert e.value.code == rsmi.ErrShortData
+        sh = bytearray(14 * 10)
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.reconstruct_coalesced(sh, 10, [i != 0 for i in range(14)], True)
+        assert e.value.code == rsmi.ErrNoDevice
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.reconstruct_coalesced(sh, 10, [i > 4 for i in range(14)], True)
+        assert e.value.code == rsmi.ErrTooFewShards

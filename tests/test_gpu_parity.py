@@ -133,7 +133,7 @@ def _dev_layout(k, m, S, nblocks, pad):
 @pytest.mark.parametrize("opts", [{}, {"chunks_per_lane": 2}, {"nontemporal": 0},
                                   {"chunks_per_lane": 2, "nontemporal": 0}, {"prefetch": 4}, {"prefetch": 8},
                                   {"prefetch": 10}, {"nontemporal": 1}, {"nontemporal": 2},
-                                  {"nontemporal": 2, "chunks_per_lane": 2}])
+                                  {"nontemporal": 2, "chunks_per_lane": 2}, {"tables": 1}])
 def test_encode_batch_dev_vs_oracle(k, m, S, nblocks, opts):
     rs, dbs, pbs = _dev_layout(k, m, S, nblocks, 256)
     host = np.zeros((nblocks, k, rs), dtype=np.uint8)
@@ -173,7 +173,8 @@ def test_encode_batch_dev_unaligned_generic(k, m, S, nblocks):
                          [(10, 4, 26215, 64, [0], True), (16, 4, 262144 // 16, 8, [0, 9], False),
                           (4, 2, 65536, 16, [1, 4], False), (10, 4, 26215, 16, [3, 11, 12, 13], False),
                           (2, 1, 131072, 4, [1], False)])
-@pytest.mark.parametrize("opts", [{}, {"prefetch": 10}, {"nontemporal": 0}, {"nontemporal": 1}, {"nontemporal": 2}])
+@pytest.mark.parametrize("opts", [{}, {"prefetch": 10}, {"nontemporal": 0}, {"nontemporal": 1}, {"nontemporal": 2},
+                                  {"tables": 1}])
 def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only, opts):
     n = k + m
     rs = (S + 255) // 256 * 256
