@@ -61,3 +61,27 @@ def test_two_rank_gloo_partition_and_timing(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     ok = np.load(os.path.join(tmp_path, "ok.npy"))
     assert ok.all(), ok
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_torchrun_on_one_gpu():
+    """The N>1 bench path on real hardware: `torch.distributed.run` with 2 ranks sharing
+    cuda:0 (--share-device; the 8-GPU run belongs to the driver).  Each rank codes its own
+    blocks, rank 0 prints one JSON line whose value counts both ranks' payload."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "1", "--blocks", "256", "--settle-ms", "0",
+           "--share-device"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["steps"] == 5 and j["scaling"] == "weak"
+    payload = 2 * 256 * 262144 * 5
+    assert abs(j["value"] - payload / (j["ms_per_step"] * 5e-3) / 2**30) / j["value"] < 0.01
+    assert j["cpu_baseline"] is None  # only rank 0 at N=1 times the CPU
