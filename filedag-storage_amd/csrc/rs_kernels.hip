@@ -34,6 +34,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));  // any byte alignment
 
 __device__ __forceinline__ uint32_t u4get(const u32x4& v, int i) { return v[i]; }
 
@@ -41,6 +42,18 @@ template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
+}
+// Byte-aligned 16-byte access: the ROCm runtime runs gfx9+ in unaligned access mode, so this
+// is still one global_load/store_dwordx4 (the memory pipeline splits it as needed).
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
+    else return *reinterpret_cast<const u32x4u*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16u(uint8_t* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4u*>(p));
+    else *reinterpret_cast<u32x4u*>(p) = v;
 }
 
 // Default rows in flight per lane for the software pipeline.
@@ -59,7 +72,14 @@ constexpr int default_prefetch() {
 // TS: table source.  0 = all five field words per output from LDS (broadcast
 // ds_read_b128); 1 = fields 0 and 2 from LDS, fields 1, 3 and 4 by scalar loads into SGPRs
 // (each v_perm takes one SGPR operand), cutting the LDS return traffic by 3/5.
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0>
+// UA: rows at any byte alignment and pitch (S >= 16; D = 1).  A lane's 16-byte window starts
+// at min(16*ch, S - 16): the row's last window overlaps the one before it instead of running
+// past S, so loads never leave [0, S) and every store is a whole 16-byte window (the
+// overlapped bytes get the same value from both lanes).  This serves the Split layout itself
+// (rows back to back at pitch S, odd for RS(10,4)) and page-locked host memory read and
+// written in place over PCIe.
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
+          bool UA = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -110,10 +130,17 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             const uint32_t ch = ch0 + kWave * d;
             chl[d] = ch < cpb ? ch : cpb - 1;
         }
+        uint32_t win[D];  // UA: byte offset of the lane's 16-byte window
+#pragma unroll
+        for (int d = 0; d < D; d++) win[d] = UA ? (chl[d] * 16u < S - 16u ? chl[d] * 16u : S - 16u) : 0u;
         auto load_col = [&](int c, u32x4 (&dst)[D]) {
 #pragma unroll
-            for (int d = 0; d < D; d++)
-                dst[d] = ld16<NT != 0>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
+            for (int d = 0; d < D; d++) {
+                if constexpr (UA)
+                    dst[d] = ld16u<NT != 0>(ib + in_off[c] + win[d]);
+                else
+                    dst[d] = ld16<NT != 0>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
+            }
         };
 
         // Software pipeline over the K input rows: a ring of P rows in flight, one
@@ -211,7 +238,12 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
         for (int d = 0; d < D; d++) {
             const uint32_t ch = ch0 + kWave * d;
-            if (ch < cpb) {
+            if (UA && ch < cpb) {
+#pragma unroll
+                for (int j = 0; j < MT; j++)
+                    st16u<NT == 1>(ob + out_off[j] + win[d], u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1],
+                                                                   acc[j][d * 4 + 2], acc[j][d * 4 + 3]});
+            } else if (!UA && ch < cpb) {
                 const uint32_t boff = ch * 16u;
                 if (boff + 16u <= S) {
 #pragma unroll
@@ -364,6 +396,8 @@ __device__ __forceinline__ u32x4 crc_chunk_load(const uint8_t* row, uint64_t off
                 v[w] &= mask;
             }
         }
+    } else if (off + 16 <= S) {
+        v = ld16u<true>(row + off);  // byte-aligned 16-byte load (also over PCIe from host memory)
     } else {
 #pragma unroll
         for (int q = 0; q < 16; q++)
@@ -465,9 +499,10 @@ void* crc16_rows_kernel(bool aligned, int fold) {
 }
 
 // ------------------------------------------------------------------ dispatch table
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0>
+template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
+          bool UA = false>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA>);
 }
 
 template <int K, int D, int NT>
@@ -476,6 +511,19 @@ static void fill_k(FastKernelTable& t) {
     t.fn[K][2][D][NT] = fast_ptr<K, 2, D, NT>();
     t.fn[K][3][D][NT] = fast_ptr<K, 3, D, NT>();
     t.fn[K][4][D][NT] = fast_ptr<K, 4, D, NT>();
+}
+
+// unaligned-layout kernels: D = 1, cache policy 1 (write-heavy tiles) or 2 (read-heavy)
+template <int K>
+static void fill_ua(FastKernelTable& t) {
+    t.ua[K][1][1] = fast_ptr<K, 1, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][2][1] = fast_ptr<K, 2, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][3][1] = fast_ptr<K, 3, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][4][1] = fast_ptr<K, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][1][2] = fast_ptr<K, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][2][2] = fast_ptr<K, 2, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][3][2] = fast_ptr<K, 3, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua[K][4][2] = fast_ptr<K, 4, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
 }
 
 template <int D, int NT>
@@ -518,6 +566,16 @@ const FastKernelTable& fast_kernels() {
         fill_d<2, 1>(x);
         fill_d<1, 2>(x);
         fill_d<2, 2>(x);
+        fill_ua<1>(x);
+        fill_ua<2>(x);
+        fill_ua<3>(x);
+        fill_ua<4>(x);
+        fill_ua<5>(x);
+        fill_ua<6>(x);
+        fill_ua<8>(x);
+        fill_ua<10>(x);
+        fill_ua<12>(x);
+        fill_ua<16>(x);
         return x;
     }();
     return t;

@@ -25,6 +25,7 @@ struct RsPlanDev {
 // the cache policy (0 default, 1 nontemporal loads + stores, 2 nontemporal loads only).
 struct FastKernelTable {
     void* fn[17][kMaxMT + 1][3][3];
+    void* ua[17][kMaxMT + 1][3];  // unaligned-layout variants [K][MT][NT], D = 1
 };
 
 // Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1);

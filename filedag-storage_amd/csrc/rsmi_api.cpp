@@ -77,6 +77,9 @@ struct rsmi_ctx {
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
     int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
+    long opt_small_bytes = 2L << 20;  // host calls up to this many shard bytes run zero-copy
+    uint8_t* h_small = nullptr;       // page-locked staging of small calls (pageable callers)
+    size_t h_small_cap = 0;
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;
@@ -269,17 +272,21 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
     const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
                          in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (uint64_t(1) << 31);
-    const int D = c->opt_d;
+    // any other layout with rows of at least 16 bytes: the unaligned-window variant (D = 1)
+    const bool ua = !aligned && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
     for (const DevTile& t : plan.tiles) {
-        const int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
+        const int D = ua ? 1 : c->opt_d;
+        int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
+        if (ua && NT == 0) NT = auto_cache_policy(t.K, t.MT);  // UA variants exist for policies 1 and 2
         void* fn = nullptr;
         if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
+        if (ua && t.K <= 16) fn = fast_kernels().ua[t.K][t.MT][NT];
         int pf_label = 0, ts_label = 0;
-        if (fn && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
+        if (fn && !ua && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
             const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][pi];
             pf_label = c->opt_prefetch;
-        } else if (fn && c->opt_tables == 1 && t.K == 10 && D == 1 &&
+        } else if (fn && !ua && c->opt_tables == 1 && t.K == 10 && D == 1 &&
                    ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][3];
             ts_label = 1;
@@ -308,6 +315,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
             }
             c->last_kernel = kernel_label(t.K, t.MT, D, NT, true);
+            if (ua) c->last_kernel += ",UA";
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
             if (ts_label) c->last_kernel += ",TS=1";
         } else {
@@ -418,6 +426,7 @@ void rsmi_close(rsmi_ctx* c) {
             }
             if (c->h_stage) (void)hipHostFree(c->h_stage);
             if (c->h_coal) (void)hipHostFree(c->h_coal);
+            if (c->h_small) (void)hipHostFree(c->h_small);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
         }
@@ -497,6 +506,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "tables")) {
         if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
+    } else if (!std::strcmp(key, "small_call_bytes")) {
+        if (value < 0) return RSMI_ERR_INVALID_ARG;
+        c->opt_small_bytes = value;
     } else if (!std::strcmp(key, "coalesce_us")) {
         if (value < 0 || value > 100000) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_us = value;
@@ -666,11 +678,11 @@ int ensure_crc_tables(rsmi_ctx* c) {
 
 // R(row) of nrows rows per block into out[b*out_bs + r] (zeroed first), stream-ordered.
 int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
-               uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream) {
+               uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream, bool zero = true) {
     if (!nblocks || !nrows) return RSMI_OK;
     int rc = ensure_crc_tables(c);
     if (rc) return rc;
-    HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
+    if (zero) HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
     if (S == 0) return RSMI_OK;  // R(empty) = 0
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
     void* fn = crc16_rows_kernel(aligned, c->opt_crc_fold);
@@ -694,6 +706,75 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 
 extern "C" {
 
+// ---------------------------------------------------------------- small host calls
+// A per-block call (DagNode.Put / Get, one 256 KiB block) is latency-bound: the copy-engine
+// path pays a DMA setup on each side of the kernel.  Small calls instead run ONE kernel that
+// reads its input rows from page-locked host memory and writes its output rows back over
+// PCIe (the unaligned-window kernels take the Split layout's odd row pitch as is).  Pageable
+// callers (Go slices over cgo) are staged through a page-locked buffer by CPU copies.
+// Caller holds ctx->mu.
+static uint8_t* small_stage(rsmi_ctx* c, size_t need) {
+    if (c->h_small_cap >= need) return c->h_small;
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    c->h_small = nullptr;
+    c->h_small_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_small), std::max<size_t>(need, 1 << 20), hipHostMallocDefault) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    c->h_small_cap = std::max<size_t>(need, 1 << 20);
+    return c->h_small;
+}
+
+static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
+                        size_t S, size_t nblocks, uint32_t* raw_out) {
+    const size_t k = size_t(c->k), m = size_t(c->m);
+    hipStream_t st = c->staging[0].stream;
+    const uint8_t* in = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * dbs + k * S);
+    uint8_t* out = host_alias(parity, (nblocks - 1) * pbs + m * S);
+    size_t in_bs = dbs, out_bs = pbs;
+    uint8_t* hs = nullptr;
+    if (!in || !out || raw_out) {  // staging also lands the raw CRCs, after the shard bytes
+        hs = small_stage(c, nblocks * (k + m) * S + nblocks * (k + m) * 4);
+        if (!hs) return RSMI_ERR_DEVICE;
+    }
+    if (!in) {
+        for (size_t b = 0; b < nblocks; b++) std::memcpy(hs + b * k * S, data + b * dbs, k * S);
+        in = host_alias(hs, nblocks * k * S);
+        in_bs = k * S;
+    }
+    uint8_t* hout = hs ? hs + nblocks * k * S : nullptr;
+    const bool stage_out = out == nullptr;
+    if (stage_out) {
+        out = host_alias(hout, nblocks * m * S);
+        out_bs = m * S;
+    }
+    if (!in || !out) return RSMI_ERR_DEVICE;
+    int rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st);
+    if (rc) return rc;
+    uint32_t* hraw = nullptr;
+    if (raw_out) {
+        // R(shard) of the rows where they lie (host memory, read back over PCIe), summed in
+        // device memory, then stored into the page-locked staging by a copy kernel
+        const size_t n = k + m;
+        if ((rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
+        uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc);
+        HIP_TRY(hipMemsetAsync(cr, 0, nblocks * n * 4, st));
+        if ((rc = launch_crc(c, in, S, in_bs, uint32_t(k), S, nblocks, cr, n, st, false))) return rc;
+        if ((rc = launch_crc(c, out, S, out_bs, uint32_t(m), S, nblocks, cr + k, n, st, false))) return rc;
+        hraw = reinterpret_cast<uint32_t*>(hs + nblocks * n * S);
+        if ((rc = repitch(host_alias(hraw, nblocks * n * 4), nblocks * n * 4, reinterpret_cast<uint8_t*>(cr),
+                          nblocks * n * 4, nblocks * n * 4, 1, st)))
+            return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (stage_out)
+        for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
+    if (raw_out) std::memcpy(raw_out, hraw, nblocks * (k + m) * 4);
+    return RSMI_OK;
+}
+
 static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                             size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
@@ -708,6 +789,8 @@ static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_
     rc = encode_plan(c, plan);
     if (rc) return rc;
     const size_t k = size_t(c->k), m = size_t(c->m);
+    if (nblocks * (k + m) * S <= size_t(c->opt_small_bytes))
+        return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
     const size_t Sp = rsmi_recommended_pitch(S);
     const size_t in_bs = k * Sp, out_bs = m * Sp;
     const bool d2 = dma_2d_ok(S);
@@ -755,8 +838,10 @@ static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
         if (raw_out) {  // R(shard) of the k data rows and the m parity rows, [block][row]
             uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n;
-            if ((rc = launch_crc(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream))) return rc;
-            if ((rc = launch_crc(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream))) return rc;
+            HIP_TRY(hipMemsetAsync(cr, 0, nb * n * 4, st.stream));
+            if ((rc = launch_crc(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream, false))) return rc;
+            if ((rc = launch_crc(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream, false)))
+                return rc;
         }
         // device -> host
         if (zc && parity_block_stride == m * S) {
@@ -980,6 +1065,36 @@ uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, si
     return crc16_entry(head, head_len, raw, data_len);
 }
 
+// Small reconstruct calls in place over PCIe (see encode_small): page-locked shards are
+// read and rebuilt where they lie; pageable ones are staged (survivor rows in, rebuilt rows
+// back).  Caller holds ctx->mu.
+static int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                             const uint8_t* present, const uint8_t* want) {
+    const size_t n = size_t(c->n);
+    hipStream_t st = c->staging[0].stream;
+    uint8_t* dev = host_alias(shards, (nblocks - 1) * bs + n * S);
+    size_t dbs = bs;
+    uint8_t* hs = nullptr;
+    if (!dev) {
+        hs = small_stage(c, nblocks * n * S);
+        if (!hs) return RSMI_ERR_DEVICE;
+        for (size_t b = 0; b < nblocks; b++)
+            for (size_t i = 0; i < n; i++)
+                if (present[i]) std::memcpy(hs + (b * n + i) * S, shards + b * bs + i * S, S);
+        dev = host_alias(hs, nblocks * n * S);
+        dbs = n * S;
+        if (!dev) return RSMI_ERR_DEVICE;
+    }
+    int rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hs)
+        for (size_t b = 0; b < nblocks; b++)
+            for (size_t i = 0; i < n; i++)
+                if (!present[i] && want[i]) std::memcpy(shards + b * bs + i * S, hs + (b * n + i) * S, S);
+    return RSMI_OK;
+}
+
 static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                  const uint8_t* present, const uint8_t* want) {
     if (!c || !shards || !present || !want) return RSMI_ERR_INVALID_ARG;
@@ -995,6 +1110,8 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
     std::shared_ptr<Plan> plan;
     rc = reconstruct_plan(c, present, want, plan);
     if (rc) return rc;
+    if (nblocks * size_t(c->n) * S <= size_t(c->opt_small_bytes))
+        return reconstruct_small(c, *plan, shards, block_stride, S, nblocks, present, want);
     // rows to ship: the k survivors in; the missing rows the plan writes, out
     std::vector<int> in_rows, out_rows;
     for (int i = 0; i < c->n && int(in_rows.size()) < c->k; i++)

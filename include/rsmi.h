@@ -205,7 +205,10 @@ int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t
  * by kernel loads (A/B); 0 = always copy), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
 (default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
 table fields into SGPRs by scalar loads instead of LDS (A/B)), "coalesce_us" / "coalesce_max"
-(rsmi_encode_block_coalesced).  Returns
+(rsmi_encode_block_coalesced), "small_call_bytes" (host calls moving at most this many shard
+bytes, default 2 MiB, run as one kernel that reads and writes page-locked host memory in
+place over PCIe -- pageable buffers are staged through a page-locked one by CPU copies --
+instead of the copy-engine pipeline; 0 = never).  Returns
  * RSMI_ERR_INVALID_ARG for unknown keys or values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */

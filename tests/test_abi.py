@@ -189,3 +189,11 @@ def test_coalesced_calls_fail_loudly_without_gpu():
         with pytest.raises(rsmi.RsmiError) as e:
             c.reconstruct_coalesced(sh, 10, [i > 4 for i in range(14)], True)
         assert e.value.code == rsmi.ErrTooFewShards
+
+
+def test_small_call_option_validates():
+    L = rsmi.lib()
+    with rsmi.Codec(10, 4) as c:
+        assert L.rsmi_set_option(c._h, b"small_call_bytes", 0) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"small_call_bytes", 1 << 30) == rsmi.OK
+        assert L.rsmi_set_option(c._h, b"small_call_bytes", -1) == rsmi.ErrInvalidArg

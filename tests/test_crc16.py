@@ -142,7 +142,8 @@ def test_rows_dev_full_size_batch():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,B", [(2, 1, 6), (4, 2, 262144), (10, 4, 262144), (10, 4, 1048576), (16, 4, 65536 + 7)])
-def test_encode_batch_host_crc_entries_match_oracle(k, m, B):
+@pytest.mark.parametrize("small", [0, 1 << 30])
+def test_encode_batch_host_crc_entries_match_oracle(k, m, B, small):
     """Every shard's datanode entry checksum from the GPU split equals server.go:70 on the
     oracle's shards."""
     n = k + m
@@ -154,6 +155,7 @@ def test_encode_batch_host_crc_entries_match_oracle(k, m, B):
     par = np.zeros((nb, m * S), dtype=np.uint8)
     raw = np.zeros((nb, n), dtype=np.uint32)
     with rsmi.Codec(k, m) as c:
+        c.set_option("small_call_bytes", small)  # copy-engine pipeline / zero-copy single kernel
         c.encode_batch_host_crc_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, raw.ctypes.data)
     meta = B.to_bytes(4, "little")
     head = orc.entry_head(meta, S)

@@ -155,18 +155,66 @@ def test_encode_batch_dev_vs_oracle(k, m, S, nblocks, opts):
     assert (got[:, :, S:] == 0x5A).all()
 
 
-@pytest.mark.parametrize("k,m,S,nblocks", [(10, 4, 26215, 5), (4, 2, 1001, 7), (20, 4, 333, 3)])
-def test_encode_batch_dev_unaligned_generic(k, m, S, nblocks):
-    """Contiguous k*S layout with odd S (the Split layout itself): byte-granular kernel."""
+@pytest.mark.parametrize("k,m,S,nblocks", [(10, 4, 26215, 5), (4, 2, 1001, 7), (20, 4, 333, 3), (3, 2, 15, 9),
+                                           (10, 4, 16, 4), (10, 4, 17, 4), (16, 4, 104858, 3)])
+def test_encode_batch_dev_unaligned(k, m, S, nblocks):
+    """Contiguous k*S layout with odd S (the Split layout itself): the unaligned-window fast
+    kernel for K <= 16 and S >= 16, the byte-granular kernel otherwise."""
     host = _rng_bytes(77, nblocks * k * S).reshape(nblocks, k, S)
     d_in = torch.from_numpy(host.reshape(-1).copy()).cuda()
     d_out = torch.zeros(nblocks * m * S, dtype=torch.uint8, device="cuda")
     with rsmi.Codec(k, m) as c:
         c.encode_batch_dev(d_in.data_ptr(), S, k * S, d_out.data_ptr(), S, m * S, S, nblocks, 0)
         torch.cuda.synchronize()
-        assert "generic" in c.last_kernel()
+        if S % 16 == 0:  # contiguous rows of a multiple of 16 bytes are an aligned layout
+            assert "rs_fast_kernel" in c.last_kernel() and ",UA" not in c.last_kernel()
+        else:
+            assert (",UA" if k <= 16 and S >= 16 else "generic") in c.last_kernel()
     got = d_out.cpu().numpy().reshape(nblocks, m, S)
     assert np.array_equal(got, orc.encode_fast(k, m, host))
+
+
+@pytest.mark.parametrize("S", [16, 17, 31, 33, 1023, 26215])
+@pytest.mark.parametrize("offset", [1, 3, 8])
+@pytest.mark.parametrize("lost,data_only", [([0], True), ([2, 11], False), ([10, 12], False)])
+def test_unaligned_window_kernel_guards_and_reconstruct(S, offset, lost, data_only):
+    """UA kernels on rows at an odd base and pitch S + 5: guard bytes between rows stay
+    untouched by encode and by the in-place reconstruct, and every row matches the oracle."""
+    k, m, nb = 10, 4, 6
+    n = k + m
+    rs = S + 5
+    bs = n * rs + 3
+    host = np.full(offset + nb * bs + 32, 0x5A, dtype=np.uint8)
+    data = _rng_bytes(S + offset, nb * k * S).reshape(nb, k, S)
+    for b in range(nb):
+        for c in range(k):
+            host[offset + b * bs + c * rs:][:S] = data[b, c]
+    d = torch.from_numpy(host.copy()).cuda()
+    base = d.data_ptr() + offset
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_dev(base, rs, bs, base + k * rs, rs, bs, S, nb, 0)
+        torch.cuda.synchronize()
+        assert ",UA" in c.last_kernel()
+        got = d.cpu().numpy()
+        full = np.zeros((nb, n, S), dtype=np.uint8)
+        full[:, :k] = data
+        full[:, k:] = orc.encode_fast(k, m, data)
+        expect = host.copy()
+        for b in range(nb):
+            for i in range(n):
+                expect[offset + b * bs + i * rs:][:S] = full[b, i]
+        assert np.array_equal(got, expect)  # rows right, every guard byte still 0x5A
+        for b in range(nb):
+            for i in lost:
+                d[offset + b * bs + i * rs: offset + b * bs + i * rs + S] = 0
+        c.reconstruct_batch_dev(base, rs, bs, S, nb, [i not in lost for i in range(n)], data_only, 0)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+    for b in range(nb):
+        for i in lost:
+            if i >= k and data_only:
+                expect[offset + b * bs + i * rs:][:S] = 0
+    assert np.array_equal(got, expect)
 
 
 @pytest.mark.parametrize("k,m,S,nblocks,lost,data_only",
@@ -359,3 +407,52 @@ def _batch_host_layouts(S, padded, bufs, zero_copy):
                 sh[b * sbs + r * S:b * sbs + (r + 1) * S] = 0
         c.reconstruct_batch_host_ptr(sh.ctypes.data, sbs, S, nb, [i not in lost for i in range(n)], False)
         assert np.array_equal(sh, full)
+
+
+@pytest.mark.parametrize("small", [0, 1 << 30])
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("k,m,B,nb", [(10, 4, 262144, 3), (10, 4, 4099, 5), (4, 2, 6, 2), (2, 1, 131072, 2),
+                                      (16, 4, 1048576 + 14, 1)])
+def test_host_small_call_path_matches_pipeline(small, pinned, k, m, B, nb):
+    """Host batch calls through the zero-copy single-kernel path (small_call_bytes large) and
+    through the copy-engine pipeline (small_call_bytes 0) give the oracle's bytes, from
+    pageable and page-locked buffers, for encode and for both reconstruct modes."""
+    import ctypes
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    nbytes = nb * n * S
+    if pinned:
+        ptr = L.rsmi_host_alloc(nbytes)
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
+    else:
+        arr = np.zeros(nbytes, dtype=np.uint8)
+        ptr = arr.ctypes.data
+    try:
+        sh = arr.reshape(nb, n, S)
+        sh[:] = 0
+        rng = np.random.default_rng(B + nb)
+        data = rng.integers(0, 256, size=(nb, k * S), dtype=np.uint8)
+        data[:, B:] = 0
+        sh[:, :k] = data.reshape(nb, k, S)
+        want = orc.encode_fast(k, m, np.ascontiguousarray(sh[:, :k]))
+        with rsmi.Codec(k, m) as c:
+            c.set_option("small_call_bytes", small)
+            c.encode_batch_host_ptr(ptr, n * S, ptr + k * S, n * S, S, nb)
+            assert np.array_equal(sh[:, k:], want)
+            full = sh.copy()
+            pats = [([0], True), ([k], True)] + ([([1, n - 1], False)] if m >= 2 else [([n - 1], False)])
+            for lost, data_only in pats:
+                sh[:, lost] = 0xEE
+                present = [i not in lost for i in range(n)]
+                c.reconstruct_batch_host_ptr(ptr, n * S, S, nb, present, data_only)
+                for i in lost:
+                    if i < k or not data_only:
+                        assert np.array_equal(sh[:, i], full[:, i]), (lost, data_only, i)
+                    else:
+                        assert (sh[:, i] == 0xEE).all()
+                sh[:] = full
+    finally:
+        if pinned:
+            L.rsmi_host_free(ptr)

@@ -47,9 +47,11 @@ int main() {
         const double r_pg = median_us([&] { return rsmi_reconstruct(c, out.data(), S, present.data(), 1); });
         const double e_pin = median_us([&] { return rsmi_encode_block(c, pblk, B, pout); });
         const double r_pin = median_us([&] { return rsmi_reconstruct(c, pout, S, present.data(), 1); });
+        std::vector<uint32_t> raw(n);
+        const double ec_pg = median_us([&] { return rsmi_encode_block_crc(c, blk.data(), B, out.data(), raw.data()); });
         std::printf("B=%8zu  encode_block %8.1f us pageable %8.1f us pinned | reconstruct(1 lost) %8.1f us pageable "
-                    "%8.1f us pinned  (%.2f / %.2f GiB/s pageable)\n",
-                    B, e_pg, e_pin, r_pg, r_pin, B / e_pg / 1073.741824, B / r_pg / 1073.741824);
+                    "%8.1f us pinned  (%.2f / %.2f GiB/s pageable) | encode_block_crc %8.1f us pageable\n",
+                    B, e_pg, e_pin, r_pg, r_pin, B / e_pg / 1073.741824, B / r_pg / 1073.741824, ec_pg);
         rsmi_host_free(pblk);
         rsmi_host_free(pout);
     }
