@@ -78,18 +78,29 @@ constexpr int default_prefetch() {
 // overlapped bytes get the same value from both lanes).  This serves the Split layout itself
 // (rows back to back at pitch S, odd for RS(10,4)) and page-locked host memory read and
 // written in place over PCIe.
+// CRC (with UA only): also fold every row the tile reads or writes into per-chunk CRC-16
+// values (crc16.hpp: R of the chunk's bytes relative to the chunk's end, nibble tables) and
+// store them as u16 at crc_out[(block * crc_slots + shard) * tpb * 64 + chunk]; input row c is
+// shard in_row[c], output row j is shard crc_out_slot0 + out_row[j].  rs_crc16_combine_kernel
+// turns them into R(row).  The small host path uses this so the shard bytes cross PCIe once.
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false>
+          bool UA = false, bool CRC = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
-                                                       uint32_t ntiles) {
+                                                       uint32_t ntiles, const uint32_t* __restrict__ crc_tbl,
+                                                       uint16_t* __restrict__ crc_out, uint32_t crc_slots,
+                                                       uint32_t crc_out_slot0) {
+    static_assert(!CRC || (UA && D == 1), "fused chunk CRCs: unaligned-window kernels only");
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
+    __shared__ uint32_t s_crc[CRC ? kCrcNWords : 1];
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
         for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+        if constexpr (CRC)
+            for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_crc[i] = crc_tbl[kCrcPWords + kCrcUWords + i];
     }
     __syncthreads();
 
@@ -133,6 +144,51 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         uint32_t win[D];  // UA: byte offset of the lane's 16-byte window
 #pragma unroll
         for (int d = 0; d < D; d++) win[d] = UA ? (chl[d] * 16u < S - 16u ? chl[d] * 16u : S - 16u) : 0u;
+        // CRC: the lane's chunk of one row -> u16 chunk value (bytes of the window before the
+        // chunk's start -- only in the row's overlapping last window -- count as zero)
+        // leading bytes of the lane's window that belong to the previous chunk (the last
+        // window only), as per-dword keep masks; branch-free so the folds stay in straight code
+        u32x4 keep = {~0u, ~0u, ~0u, ~0u};
+        if constexpr (CRC) {
+            const int lead = int(chl[0] * 16u - win[0]);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int nb = lead - 4 * w;
+                keep[w] = nb >= 4 ? 0u : nb <= 0 ? ~0u : ~((1u << (8 * nb)) - 1u);
+            }
+        }
+        uint16_t* crc_tile = nullptr;  // this lane's chunk slot in shard 0 of the tile's block
+        if constexpr (CRC) {
+            crc_tile = crc_out + uint64_t(blk) * crc_slots * (uint64_t(tpb) * kWave) + ch0;
+            asm volatile("" : "+v"(crc_tile));
+        }
+        auto crc_store = [&](u32x4 x, uint32_t shard) {
+            if constexpr (CRC) {
+                const uint32_t ch = ch0;
+                {
+                    x &= keep;
+                    const uint8_t* nbt = reinterpret_cast<const uint8_t*>(s_crc);
+                    uint32_t cr = 0;
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        uint32_t lo = (x[w] << 1) & 0x1E1E1E1Eu, hi = (x[w] >> 3) & 0x1E1E1E1Eu;
+                        asm volatile("" : "+v"(lo), "+v"(hi));
+                        uint32_t l[8];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int p = 4 * w + q;
+                            l[2 * q] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + ((lo >> (8 * q)) & 0xFF));
+                            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
+                        }
+                        cr = xor3(cr, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+                    }
+                    // unconditional: lanes past the row's end own padding slots (chunk pitch
+                    // tpb * 64), so no branch splits the column loop (a branch there lets the
+                    // compiler sink every column's GF math past it)
+                    crc_tile[uint64_t(shard) * (uint64_t(tpb) * kWave)] = uint16_t(cr);
+                }
+            }
+        };
         auto load_col = [&](int c, u32x4 (&dst)[D]) {
 #pragma unroll
             for (int d = 0; d < D; d++) {
@@ -224,6 +280,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                         }
                     }
                 }
+            if constexpr (CRC) crc_store(v[slot][0], plan->in_row[c]);
             if (c + P < K) load_col(c + P, v[slot]);
             if (c + 1 < K) load_tables(c + 1, Tn);
             __builtin_amdgcn_sched_barrier(0);
@@ -240,9 +297,14 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             const uint32_t ch = ch0 + kWave * d;
             if (UA && ch < cpb) {
 #pragma unroll
-                for (int j = 0; j < MT; j++)
-                    st16u<NT == 1>(ob + out_off[j] + win[d], u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1],
-                                                                   acc[j][d * 4 + 2], acc[j][d * 4 + 3]});
+                for (int j = 0; j < MT; j++) {
+                    const u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
+                    st16u<NT == 1>(ob + out_off[j] + win[d], o);
+                    if constexpr (CRC) {
+                        crc_store(o, crc_out_slot0 + plan->out_row[j]);
+                        __builtin_amdgcn_sched_barrier(0);  // one row's 32 table reads in flight at a time
+                    }
+                }
             } else if (!UA && ch < cpb) {
                 const uint32_t boff = ch * 16u;
                 if (boff + 16u <= S) {
@@ -490,6 +552,54 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
     }
 }
 
+// R(row) from the fused kernels' per-chunk values (rs_fast_kernel CRC): one wave per row.
+// Lane l folds chunks l, l + 64, ... (A^1024 between them), a lane scan combines the lanes
+// (A^(16*2^j)), and lane 63 shifts the total from the 1 KiB grid end to the row end.  The
+// row's last chunk is relative to S (its window ends at S), so it first moves onto the
+// 16-byte grid by A^(16*cpb - S).  out[row] is written once (host memory allowed).
+__global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* __restrict__ tbl,
+                                                               const uint16_t* __restrict__ chunks, uint32_t cpb,
+                                                               uint32_t pitch, uint64_t S, uint64_t nrows,
+                                                               uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_tbl[kCrcPWords];
+    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
+    __syncthreads();
+    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    const uint32_t T = (cpb + kWave - 1) / kWave;
+    const uint32_t lead = uint32_t((uint64_t(cpb) * 16 - S) % kCrcOrder);  // 16*cpb - S < 16
+    for (uint64_t r = uint64_t(blockIdx.x) * (kWG / kWave) + wid; r < nrows; r += nw) {
+        const uint16_t* rc = chunks + r * pitch;
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < T; t++) {
+            const uint32_t ch = t * kWave + lane;
+            uint32_t c = ch < cpb ? rc[ch] : 0u;
+            if (ch == cpb - 1) {  // onto the grid: as if followed by 16*cpb - S zero bytes
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if ((lead >> i) & 1) c = crc_pow(sP, i, c);
+            }
+            acc = crc_pow(sP, 10, acc) ^ c;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t w = crc_pow(sP, 4 + j, acc);
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (lane >= (1u << j)) acc ^= t;
+        }
+        int64_t e = (int64_t(S) - int64_t(T) * (kWave * 16)) % int64_t(kCrcOrder);
+        if (e < 0) e += kCrcOrder;
+#pragma unroll
+        for (int i = 0; i < kCrcPowers; i++)
+            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
+        if (lane == kWave - 1) out[r] = acc;
+    }
+}
+
+void* crc16_combine_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_kernel); }
+
 void* crc16_rows_kernel(bool aligned, int fold) {
     if (fold == 0)
         return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 0>)
@@ -500,9 +610,18 @@ void* crc16_rows_kernel(bool aligned, int fold) {
 
 // ------------------------------------------------------------------ dispatch table
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false>
+          bool UA = false, bool CRC = false>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC>);
+}
+
+// fused chunk-CRC variants: UA, D = 1, the auto cache policy of the shape
+constexpr int auto_nt(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
+template <int K, int MT>
+static void* crc_ptr() {
+    // 2 waves/SIMD: the chunk folds need registers beyond the 128 the streaming kernels keep
+    // to, and these serve latency-bound small calls, not HBM streams
+    return fast_ptr<K, MT, 1, auto_nt(K, MT), 0, true, 2, 0, true, true>();
 }
 
 template <int K, int D, int NT>
@@ -524,6 +643,10 @@ static void fill_ua(FastKernelTable& t) {
     t.ua[K][2][2] = fast_ptr<K, 2, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
     t.ua[K][3][2] = fast_ptr<K, 3, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
     t.ua[K][4][2] = fast_ptr<K, 4, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
+    t.ua_crc[K][1] = crc_ptr<K, 1>();
+    t.ua_crc[K][2] = crc_ptr<K, 2>();
+    t.ua_crc[K][3] = crc_ptr<K, 3>();
+    t.ua_crc[K][4] = crc_ptr<K, 4>();
 }
 
 template <int D, int NT>

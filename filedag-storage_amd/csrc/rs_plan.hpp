@@ -26,6 +26,7 @@ struct RsPlanDev {
 struct FastKernelTable {
     void* fn[17][kMaxMT + 1][3][3];
     void* ua[17][kMaxMT + 1][3];  // unaligned-layout variants [K][MT][NT], D = 1
+    void* ua_crc[17][kMaxMT + 1];  // the same with fused per-chunk CRC-16 (auto cache policy)
 };
 
 // Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1);
@@ -50,5 +51,6 @@ constexpr int kCrcUWords = 16 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
 constexpr int kCrcTableWords = kCrcPWords + kCrcUWords + kCrcNWords;
 void* crc16_rows_kernel(bool aligned, int fold);
+void* crc16_combine_kernel();
 
 }  // namespace rsmi

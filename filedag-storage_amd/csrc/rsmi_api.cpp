@@ -69,6 +69,8 @@ struct rsmi_ctx {
     uint32_t* d_crc_tbl = nullptr;  // CRC-16 device tables (crc16.hpp), uploaded on first use
     uint8_t* d_crc = nullptr;       // raw row CRCs (u32) of host batch calls
     size_t crc_cap = 0;
+    uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
+    size_t chunks_cap = 0;
     // options
     int opt_d = 1;
     int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
@@ -266,21 +268,33 @@ const char* kernel_label(int K, int MT, int D, int NT, bool fast) {
 int auto_cache_policy(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
 
 // Launch every tile of a plan over nblocks blocks.
+// Fused per-chunk CRC output of a launch (rs_fast_kernel CRC variants): chunk values of every
+// row the plan reads or writes, at out[(block * slots + shard) * cpb + chunk].
+struct CrcFuse {
+    const uint32_t* tbl = nullptr;
+    uint16_t* out = nullptr;
+    uint32_t slots = 0, out_slot0 = 0;
+};
+
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
-                uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream) {
+                uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
+                const CrcFuse* fuse = nullptr) {
     if (nblocks == 0 || S == 0) return RSMI_OK;
     const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
                          in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (uint64_t(1) << 31);
     // any other layout with rows of at least 16 bytes: the unaligned-window variant (D = 1)
-    const bool ua = !aligned && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
+    const bool ua = (!aligned || fuse) && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
+    if (fuse && !ua) return RSMI_ERR_INVALID_ARG;  // callers fall back to the separate CRC pass
     for (const DevTile& t : plan.tiles) {
         const int D = ua ? 1 : c->opt_d;
         int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
         if (ua && NT == 0) NT = auto_cache_policy(t.K, t.MT);  // UA variants exist for policies 1 and 2
         void* fn = nullptr;
         if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
-        if (ua && t.K <= 16) fn = fast_kernels().ua[t.K][t.MT][NT];
+        if (ua && t.K <= 16) fn = fuse ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().ua[t.K][t.MT][NT];
+        if (fuse && !fn) return RSMI_ERR_INVALID_ARG;
+        if (fuse) NT = auto_cache_policy(t.K, t.MT);  // the one policy the fused variants have
         int pf_label = 0, ts_label = 0;
         if (fn && !ua && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
             const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
@@ -310,12 +324,17 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 const RsPlanDev* pd = t.dev;
                 const uint8_t* inb = in + b0 * in_bs;
                 uint8_t* outb = out + b0 * out_bs;
-                void* args[] = {&pd, &inb, &outb, &in_bs, &in_rs, &out_bs, &out_rs, &S32, &cpb32, &tpb32, &ntiles};
+                const uint32_t* ctbl = fuse ? fuse->tbl : nullptr;
+                uint16_t* cout = fuse ? fuse->out + b0 * fuse->slots * tpb * kWave : nullptr;
+                uint32_t cslots = fuse ? fuse->slots : 0, cslot0 = fuse ? fuse->out_slot0 : 0;
+                void* args[] = {&pd,    &inb,    &outb,  &in_bs, &in_rs, &out_bs, &out_rs, &S32,
+                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + 3) / 4, uint64_t(wg_cap));
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
             }
             c->last_kernel = kernel_label(t.K, t.MT, D, NT, true);
             if (ua) c->last_kernel += ",UA";
+            if (fuse) c->last_kernel += ",CRC";
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
             if (ts_label) c->last_kernel += ",TS=1";
         } else {
@@ -429,6 +448,7 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->h_small) (void)hipHostFree(c->h_small);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
+            if (c->d_chunks) (void)hipFree(c->d_chunks);
         }
     }
     delete c;
@@ -751,10 +771,40 @@ static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size
         out_bs = m * S;
     }
     if (!in || !out) return RSMI_ERR_DEVICE;
+    uint32_t* hraw = nullptr;
+    if (raw_out && S >= 16 && k <= 16) {
+        // fused: the encode stores per-chunk CRCs of every row it reads and writes (the shard
+        // bytes cross PCIe once), then one wave per row combines them into R(row) and stores
+        // it straight into the page-locked staging
+        const size_t n = k + m, cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
+        int rc = ensure_crc_tables(c);
+        if (rc) return rc;
+        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
+        CrcFuse fz;
+        fz.tbl = c->d_crc_tbl;
+        fz.out = reinterpret_cast<uint16_t*>(c->d_chunks);
+        fz.slots = uint32_t(n);
+        fz.out_slot0 = uint32_t(k);
+        if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st, &fz))) return rc;
+        hraw = reinterpret_cast<uint32_t*>(hs + nblocks * n * S);
+        uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, nblocks * n * 4));
+        if (!draw) return RSMI_ERR_DEVICE;
+        const uint16_t* ch = fz.out;
+        uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
+        uint64_t S64 = S, rows = nblocks * n;
+        const uint32_t* tb = c->d_crc_tbl;
+        void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &draw};
+        const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
+        HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (stage_out)
+            for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
+        std::memcpy(raw_out, hraw, nblocks * n * 4);
+        return RSMI_OK;
+    }
     int rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st);
     if (rc) return rc;
-    uint32_t* hraw = nullptr;
-    if (raw_out) {
+    if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
         // R(shard) of the rows where they lie (host memory, read back over PCIe), summed in
         // device memory, then stored into the page-locked staging by a copy kernel
         const size_t n = k + m;
@@ -789,7 +839,12 @@ static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_
     rc = encode_plan(c, plan);
     if (rc) return rc;
     const size_t k = size_t(c->k), m = size_t(c->m);
-    if (nblocks * (k + m) * S <= size_t(c->opt_small_bytes))
+    // pageable input is staged by CPU copies: above half the limit the copy engines win
+    // (tools/latency.cpp, 1 MiB blocks: 107 us staged against 99 us)
+    const size_t total = nblocks * (k + m) * S;
+    if (total <= size_t(c->opt_small_bytes) &&
+        (2 * total <= size_t(c->opt_small_bytes) ||
+         host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S)))
         return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
     const size_t Sp = rsmi_recommended_pitch(S);
     const size_t in_bs = k * Sp, out_bs = m * Sp;
