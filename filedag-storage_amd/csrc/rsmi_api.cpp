@@ -749,36 +749,39 @@ static uint8_t* small_stage(rsmi_ctx* c, size_t need) {
 
 static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
                         size_t S, size_t nblocks, uint32_t* raw_out) {
-    const size_t k = size_t(c->k), m = size_t(c->m);
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     hipStream_t st = c->staging[0].stream;
     const uint8_t* in = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * dbs + k * S);
     uint8_t* out = host_alias(parity, (nblocks - 1) * pbs + m * S);
     size_t in_bs = dbs, out_bs = pbs;
+    // page-locked staging, only the parts needed: [data rows | parity rows | raw CRCs]
+    const bool stage_in = in == nullptr, stage_out = out == nullptr;
+    const size_t in_sz = stage_in ? nblocks * k * S : 0, out_sz = stage_out ? nblocks * m * S : 0;
+    const size_t raw_sz = raw_out ? nblocks * n * 4 : 0;
     uint8_t* hs = nullptr;
-    if (!in || !out || raw_out) {  // staging also lands the raw CRCs, after the shard bytes
-        hs = small_stage(c, nblocks * (k + m) * S + nblocks * (k + m) * 4);
+    if (in_sz + out_sz + raw_sz) {
+        hs = small_stage(c, in_sz + out_sz + raw_sz);
         if (!hs) return RSMI_ERR_DEVICE;
     }
-    if (!in) {
+    if (stage_in) {
         for (size_t b = 0; b < nblocks; b++) std::memcpy(hs + b * k * S, data + b * dbs, k * S);
-        in = host_alias(hs, nblocks * k * S);
+        in = host_alias(hs, in_sz);
         in_bs = k * S;
     }
-    uint8_t* hout = hs ? hs + nblocks * k * S : nullptr;
-    const bool stage_out = out == nullptr;
+    uint8_t* hout = hs ? hs + in_sz : nullptr;
     if (stage_out) {
-        out = host_alias(hout, nblocks * m * S);
+        out = host_alias(hout, out_sz);
         out_bs = m * S;
     }
+    uint32_t* hraw = raw_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz) : nullptr;
     if (!in || !out) return RSMI_ERR_DEVICE;
-    uint32_t* hraw = nullptr;
+    int rc;
     if (raw_out && S >= 16 && k <= 16) {
         // fused: the encode stores per-chunk CRCs of every row it reads and writes (the shard
         // bytes cross PCIe once), then one wave per row combines them into R(row) and stores
         // it straight into the page-locked staging
-        const size_t n = k + m, cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
-        int rc = ensure_crc_tables(c);
-        if (rc) return rc;
+        const size_t cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
+        if ((rc = ensure_crc_tables(c))) return rc;
         if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
         CrcFuse fz;
         fz.tbl = c->d_crc_tbl;
@@ -786,8 +789,7 @@ static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size
         fz.slots = uint32_t(n);
         fz.out_slot0 = uint32_t(k);
         if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st, &fz))) return rc;
-        hraw = reinterpret_cast<uint32_t*>(hs + nblocks * n * S);
-        uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, nblocks * n * 4));
+        uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, raw_sz));
         if (!draw) return RSMI_ERR_DEVICE;
         const uint16_t* ch = fz.out;
         uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
@@ -796,32 +798,23 @@ static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size
         void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &draw};
         const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
         HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (stage_out)
-            for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
-        std::memcpy(raw_out, hraw, nblocks * n * 4);
-        return RSMI_OK;
-    }
-    int rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st);
-    if (rc) return rc;
-    if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
-        // R(shard) of the rows where they lie (host memory, read back over PCIe), summed in
-        // device memory, then stored into the page-locked staging by a copy kernel
-        const size_t n = k + m;
-        if ((rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
-        uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc);
-        HIP_TRY(hipMemsetAsync(cr, 0, nblocks * n * 4, st));
-        if ((rc = launch_crc(c, in, S, in_bs, uint32_t(k), S, nblocks, cr, n, st, false))) return rc;
-        if ((rc = launch_crc(c, out, S, out_bs, uint32_t(m), S, nblocks, cr + k, n, st, false))) return rc;
-        hraw = reinterpret_cast<uint32_t*>(hs + nblocks * n * S);
-        if ((rc = repitch(host_alias(hraw, nblocks * n * 4), nblocks * n * 4, reinterpret_cast<uint8_t*>(cr),
-                          nblocks * n * 4, nblocks * n * 4, 1, st)))
-            return rc;
+    } else {
+        if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
+        if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
+            if ((rc = reserve(c->d_crc, c->crc_cap, raw_sz))) return rc;
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc);
+            HIP_TRY(hipMemsetAsync(cr, 0, raw_sz, st));
+            if ((rc = launch_crc(c, in, S, in_bs, uint32_t(k), S, nblocks, cr, n, st, false))) return rc;
+            if ((rc = launch_crc(c, out, S, out_bs, uint32_t(m), S, nblocks, cr + k, n, st, false))) return rc;
+            if ((rc = repitch(host_alias(hraw, raw_sz), raw_sz, reinterpret_cast<uint8_t*>(cr), raw_sz, raw_sz, 1,
+                              st)))
+                return rc;
+        }
     }
     HIP_TRY(hipStreamSynchronize(st));
     if (stage_out)
         for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
-    if (raw_out) std::memcpy(raw_out, hraw, nblocks * (k + m) * 4);
+    if (raw_out) std::memcpy(raw_out, hraw, raw_sz);
     return RSMI_OK;
 }
 
@@ -839,12 +832,16 @@ static int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_
     rc = encode_plan(c, plan);
     if (rc) return rc;
     const size_t k = size_t(c->k), m = size_t(c->m);
-    // pageable input is staged by CPU copies: above half the limit the copy engines win
-    // (tools/latency.cpp, 1 MiB blocks: 107 us staged against 99 us)
+    // One zero-copy kernel (encode_small) when both sides are page-locked, whatever the size
+    // (tools/hostsweep.py "direct": equal to the copy-engine pipeline for encode, +8-18% for
+    // reconstruct), or when the call is small; pageable input is staged by CPU copies, and
+    // above half the small-call limit the copy engines win (tools/latency.cpp, 1 MiB blocks:
+    // 107 us staged against 99 us).
     const size_t total = nblocks * (k + m) * S;
-    if (total <= size_t(c->opt_small_bytes) &&
-        (2 * total <= size_t(c->opt_small_bytes) ||
-         host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S)))
+    const bool in_pinned = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S);
+    const bool pinned = in_pinned && host_alias(parity, (nblocks - 1) * parity_block_stride + m * S);
+    if ((c->opt_zero_copy && pinned) ||
+        (total <= size_t(c->opt_small_bytes) && (2 * total <= size_t(c->opt_small_bytes) || in_pinned)))
         return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
     const size_t Sp = rsmi_recommended_pitch(S);
     const size_t in_bs = k * Sp, out_bs = m * Sp;
@@ -1165,7 +1162,10 @@ static int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stri
     std::shared_ptr<Plan> plan;
     rc = reconstruct_plan(c, present, want, plan);
     if (rc) return rc;
-    if (nblocks * size_t(c->n) * S <= size_t(c->opt_small_bytes))
+    // zero-copy in place when the shards are page-locked (hostsweep "direct": +8-18% over the
+    // pipeline) or the call is small (see encode_host_impl)
+    if ((c->opt_zero_copy && host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)) ||
+        nblocks * size_t(c->n) * S <= size_t(c->opt_small_bytes))
         return reconstruct_small(c, *plan, shards, block_stride, S, nblocks, present, want);
     // rows to ship: the k survivors in; the missing rows the plan writes, out
     std::vector<int> in_rows, out_rows;

@@ -198,11 +198,10 @@ int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t
 /* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache
  * policy: -1 auto per output width (default), 0 default loads and stores, 1 nontemporal loads
  * and stores, 2 nontemporal loads only), "waves_per_cu" (grid cap, 0 = occupancy),
- * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: for shard
- * sizes that are not a multiple of 8 and page-locked host buffers (rsmi_host_alloc), the
- * host batch calls write results with kernel stores over PCIe instead of a device->host
- * copy, and reconstruct reads its k input rows with kernel loads; 2 = encode also uploads
- * by kernel loads (A/B); 0 = always copy), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
+ * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: host batch calls whose buffers are page-locked
+(rsmi_host_alloc) run as one kernel that reads and writes them in place over PCIe, at any
+size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
+same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
 (default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
 table fields into SGPRs by scalar loads instead of LDS (A/B)), "coalesce_us" / "coalesce_max"
 (rsmi_encode_block_coalesced), "small_call_bytes" (host calls moving at most this many shard

@@ -30,8 +30,16 @@ def main():
         present = [i not in lost for i in range(n)]
         c = rsmi.Codec(k, m)
         res = {}
-        for zc in (0, 1, 2, 0, 1, 2):
-            c.set_option("zero_copy", zc)
+        # zero_copy 0/1/2 on the copy-engine pipeline; "direct" = one zero-copy UA kernel for
+        # the whole call (small_call_bytes above the batch size)
+        modes = (0, 1, 2, "direct")
+        for zc in modes + modes:
+            if zc == "direct":
+                c.set_option("zero_copy", 1)
+                c.set_option("small_call_bytes", 1 << 40)
+            else:
+                c.set_option("small_call_bytes", 0)
+                c.set_option("zero_copy", zc)
             c.encode_batch_host_ptr(din, k * S, dpar, m * S, S, nb)
             t0 = time.perf_counter()
             for _ in range(3):
@@ -44,7 +52,7 @@ def main():
         for zc, v in res.items():
             e = max(x[0] for x in v)
             r = max(x[1] for x in v)
-            print(f"RS({k},{m}) {kib:5d} KiB S={S:7d} zero_copy={zc}: encode {e:6.2f} GiB/s, "
+            print(f"RS({k},{m}) {kib:5d} KiB S={S:7d} zero_copy={zc!s:6s}: encode {e:6.2f} GiB/s, "
                   f"reconstruct{lost} {r:6.2f} GiB/s", flush=True)
         c.close()
         for p in (din, dpar, dsh):
