@@ -747,6 +747,31 @@ static uint8_t* small_stage(rsmi_ctx* c, size_t need) {
     return c->h_small;
 }
 
+// Encode with fused per-chunk CRCs, then R(row) of all k+m rows of every block into
+// raw[b * (k+m) + row] (device or page-locked host memory).  Needs S >= 16 and k <= 16.
+static int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                             size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+    const size_t k = size_t(c->k), n = size_t(c->n);
+    const size_t cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
+    int rc;
+    if ((rc = ensure_crc_tables(c))) return rc;
+    if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
+    CrcFuse fz;
+    fz.tbl = c->d_crc_tbl;
+    fz.out = reinterpret_cast<uint16_t*>(c->d_chunks);
+    fz.slots = uint32_t(n);
+    fz.out_slot0 = uint32_t(k);
+    if ((rc = launch_plan(c, plan, in, in_rs, in_bs, out, out_rs, out_bs, S, nblocks, st, &fz))) return rc;
+    const uint16_t* ch = fz.out;
+    uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
+    uint64_t S64 = S, rows = nblocks * n;
+    const uint32_t* tb = c->d_crc_tbl;
+    void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &raw};
+    const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
+    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+    return RSMI_OK;
+}
+
 static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
                         size_t S, size_t nblocks, uint32_t* raw_out) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
@@ -780,24 +805,9 @@ static int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size
         // fused: the encode stores per-chunk CRCs of every row it reads and writes (the shard
         // bytes cross PCIe once), then one wave per row combines them into R(row) and stores
         // it straight into the page-locked staging
-        const size_t cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
-        if ((rc = ensure_crc_tables(c))) return rc;
-        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
-        CrcFuse fz;
-        fz.tbl = c->d_crc_tbl;
-        fz.out = reinterpret_cast<uint16_t*>(c->d_chunks);
-        fz.slots = uint32_t(n);
-        fz.out_slot0 = uint32_t(k);
-        if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st, &fz))) return rc;
         uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, raw_sz));
         if (!draw) return RSMI_ERR_DEVICE;
-        const uint16_t* ch = fz.out;
-        uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
-        uint64_t S64 = S, rows = nblocks * n;
-        const uint32_t* tb = c->d_crc_tbl;
-        void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &draw};
-        const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
-        HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+        if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, draw, st))) return rc;
     } else {
         if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
         if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
@@ -1094,6 +1104,36 @@ long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
     if (!std::strcmp(key, "coalesced_calls")) return long(c->stat_coal_calls.load());
     if (!std::strcmp(key, "coalesced_batches")) return long(c->stat_coal_batches.load());
     return -1;
+}
+
+int rsmi_encode_batch_dev_crc(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_stride, size_t data_block_stride,
+                              uint8_t* d_parity, size_t parity_shard_stride, size_t parity_block_stride, size_t S,
+                              size_t nblocks, uint32_t* d_raw_out, void* stream) {
+    if (!c || !d_data || !d_parity || !d_raw_out) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    if (data_shard_stride < S || parity_shard_stride < S) return RSMI_ERR_INVALID_ARG;
+    if (nblocks == 0) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    std::shared_ptr<Plan> plan;
+    if ((rc = encode_plan(c, plan))) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    if (S >= 16 && k <= 16)
+        return launch_encode_crc(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
+                                 parity_block_stride, S, nblocks, d_raw_out, st);
+    // S < 16 or k > 16: the encode, then the CRC pass over both row sets
+    if ((rc = launch_plan(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
+                          parity_block_stride, S, nblocks, st)))
+        return rc;
+    HIP_TRY(hipMemsetAsync(d_raw_out, 0, nblocks * n * 4, st));
+    if ((rc = launch_crc(c, d_data, data_shard_stride, data_block_stride, uint32_t(k), S, nblocks, d_raw_out, n, st,
+                         false)))
+        return rc;
+    return launch_crc(c, d_parity, parity_shard_stride, parity_block_stride, uint32_t(m), S, nblocks, d_raw_out + k, n,
+                      st, false);
 }
 
 int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,

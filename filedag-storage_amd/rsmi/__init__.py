@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_encode_batch_host_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
                                                       ctypes.c_void_p]),
         "rsmi_encode_block_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
+        "rsmi_encode_batch_dev_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size,
+                                                     c_size, ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
@@ -240,6 +242,11 @@ class Codec:
                                   nblocks: int, raw_ptr: int) -> None:
         _check(lib().rsmi_encode_batch_host_crc(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
                                                 raw_ptr))
+
+    def encode_batch_dev_crc(self, d_data: int, data_rs: int, data_bs: int, d_parity: int, parity_rs: int,
+                             parity_bs: int, S: int, nblocks: int, d_raw: int, stream: int = 0) -> None:
+        _check(lib().rsmi_encode_batch_dev_crc(self._h, d_data, data_rs, data_bs, d_parity, parity_rs, parity_bs, S,
+                                               nblocks, d_raw, stream or None))
 
     def crc16_rows_dev(self, d_rows: int, rs: int, bs: int, nrows: int, S: int, nblocks: int, d_out: int,
                        out_bs: int, stream: int = 0) -> None:

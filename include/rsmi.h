@@ -190,6 +190,15 @@ int rsmi_crc16_rows_dev(rsmi_ctx* ctx, const uint8_t* d_rows, size_t shard_strid
 int rsmi_encode_batch_host_crc(rsmi_ctx* ctx, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out);
 
+/* rsmi_encode_batch_dev with the CRC fused into the encode pass: every row the kernel reads
+ * or writes is folded into per-chunk CRC-16 values on the way, and a combine pass writes
+ * d_raw_out[b*(k+m) + r] = R(shard r of block b) (device memory).  The SURVEY.md 8(f) rank 2
+ * form: no second pass over the shard bytes.  Stream-ordered. */
+int rsmi_encode_batch_dev_crc(rsmi_ctx* ctx, const uint8_t* d_data, size_t data_shard_stride,
+                              size_t data_block_stride, uint8_t* d_parity, size_t parity_shard_stride,
+                              size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* d_raw_out,
+                              void* stream);
+
 /* rsmi_encode_block plus raw_out[r] = R(shard r), r < k+m. */
 int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out);
 

@@ -289,3 +289,38 @@ def test_coalesced_reconstruct_concurrent_callers():
                 assert np.array_equal(got[r], sh[r]), (lost, data_only, r)
             else:
                 assert not got[r].any()  # ReconstructData leaves missing parity alone
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,S,nb,layout", [(10, 4, 26215, 64, "pitched"), (10, 4, 26215, 9, "split"),
+                                             (4, 2, 65536, 8, "pitched"), (16, 4, 4097, 5, "split"),
+                                             (3, 2, 7, 6, "split"), (20, 4, 333, 3, "split")])
+def test_encode_batch_dev_crc_fused(k, m, S, nb, layout):
+    """Device-resident encode with the CRC fused into the encode pass: parity and every row's
+    R(row) equal the oracle's (S < 16 and k > 16 take the separate CRC pass)."""
+    import torch
+
+    n = k + m
+    rs = rsmi.recommended_pitch(S) if layout == "pitched" else S
+    data = np.random.default_rng(S + k).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+    host = np.zeros((nb, n, rs), dtype=np.uint8)
+    host[:, :k, :S] = data
+    d = torch.from_numpy(host.reshape(-1).copy()).cuda()
+    raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+    base = d.data_ptr()
+    with rsmi.Codec(k, m) as c:
+        c.encode_batch_dev_crc(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, raw.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        kern = c.last_kernel()
+    got = d.cpu().numpy().reshape(nb, n, rs)
+    want = orc.encode_fast(k, m, data)
+    assert np.array_equal(got[:, k:, :S], want)
+    if S >= 16 and k <= 16:
+        assert ",CRC" in kern
+    r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    for b in range(nb):
+        rows = list(data[b]) + list(want[b])
+        for i in range(n):
+            assert r[b, i] < 0x10000
+            assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (b, i)

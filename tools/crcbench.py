@@ -44,5 +44,47 @@ def main():
             c.close()
 
 
+def fused_vs_separate():
+    """The bench layout: encode then a separate R(row) pass, against the encode with the CRC
+    fused (rsmi_encode_batch_dev_crc)."""
+    st = torch.cuda.current_stream()
+    k, m, B, nb = 10, 4, 262144, 4096
+    n = k + m
+    S = (B + k - 1) // k
+    p = rsmi.recommended_pitch(S)
+    buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
+    raw = torch.empty((nb, n), dtype=torch.int32, device="cuda")
+    b = buf.data_ptr()
+    c = rsmi.Codec(k, m)
+    sh = st.cuda_stream
+    V = {
+        "encode only": lambda: c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh),
+        "encode + separate CRC pass": lambda: (c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh),
+                                               c.crc16_rows_dev(b, p, n * p, n, S, nb, raw.data_ptr(), n, sh)),
+        "encode with fused CRC": lambda: c.encode_batch_dev_crc(b, p, n * p, b + k * p, p, n * p, S, nb,
+                                                                raw.data_ptr(), sh),
+    }
+    t_end = time.perf_counter() + 0.2
+    while time.perf_counter() < t_end:
+        for f in V.values():
+            f()
+        torch.cuda.synchronize()
+    ts = {x: [] for x in V}
+    for _ in range(7):
+        for name, f in V.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            f()
+            e1.record(st)
+            e1.synchronize()
+            ts[name].append(e0.elapsed_time(e1))
+    for name in V:
+        med = statistics.median(ts[name])
+        print(f"RS(10,4) 256 KiB x {nb}: {name:28s} {med * 1e3:8.1f} us  "
+              f"{nb * n * S / med / 1e6:8.1f} GB/s of shard bytes", flush=True)
+    c.close()
+
+
 if __name__ == "__main__":
+    fused_vs_separate()
     main()
