@@ -104,8 +104,16 @@ Status DagNode::New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNo
     d->device_ = device;
     d->slots_.assign(kClusterSlots / 8, 0);
     for (auto& c : clients) d->nodes_.push_back(StorageNode{c, false});
+    d->fan_.reset(new FanOut(int(n) - 1));  // the calling thread runs one share itself
     *out = std::move(d);
     return Status::Ok();
+}
+
+void DagNode::fan(int count, const std::function<void(int)>& f, size_t shard_bytes) {
+    if (parallel_ && fan_ && shard_bytes >= fanout_min_ && active_.load() <= 1)
+        fan_->run(count, f);
+    else
+        for (int i = 0; i < count; i++) f(i);
 }
 
 DagNode::~DagNode() { Close(); }
@@ -177,20 +185,20 @@ Status DagNode::get_meta_info(const std::string& key, Meta* meta, std::vector<St
     const size_t n = nodes_.size();
     std::vector<Meta> metas(n);
     std::vector<Status> errs(n);
-    for (size_t i = 0; i < n; i++) {  // readAllMeta (node.go:450-489)
+    fan(int(n), [&](int i) {  // readAllMeta (node.go:450-489): one goroutine per datanode
         Bytes mb;
         Status s = nodes_[i].client->GetMeta(key, &mb);
         if (!s.ok()) {
             errs[i] = s;
-            continue;
+            return;
         }
         if (mb.size() < 4) {
             errs[i] = Status::Error("unexpected EOF");
-            continue;
+            return;
         }
         metas[i].block_size = int32_t(uint32_t(mb[0]) | uint32_t(mb[1]) << 8 | uint32_t(mb[2]) << 16 |
                                       uint32_t(mb[3]) << 24);
-    }
+    }, last_shard_.load());  // GetMeta checks the whole entry's CRC: cost follows the shard size
     const int read_quorum = EntryQuorum().first;
     Status r = reduce_quorum_errs(errs, read_quorum, kErrReadQuorum);
     if (!r.ok()) return r;
@@ -205,6 +213,7 @@ Status DagNode::get_meta_info(const std::string& key, Meta* meta, std::vector<St
 }
 
 Status DagNode::GetSize(const std::string& key, int* size) {
+    Active act(active_);
     Meta meta;
     Status s = get_meta_info(key, &meta, nullptr);
     *size = meta.block_size;
@@ -220,6 +229,7 @@ Status DagNode::Has(const std::string& key, bool* has) {
 
 // ------------------------------------------------------------------ write path
 Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:358-408
+    Active act(active_);
     const Bytes meta = encode_meta(int32_t(block.size()));
     Erasure enc;
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
@@ -229,15 +239,21 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     s = gpu_checksums_ ? enc.EncodeDataWithCrc(block, &shards, &raw) : enc.EncodeData(block, &shards);
     if (!s.ok()) return s;
     const int wq = EntryQuorum().second;
+    std::vector<Status> res(nodes_.size());
+    const size_t S = shards.empty() ? 0 : shards[0].size();
+    last_shard_ = S;
+    fan(int(nodes_.size()), [&](int i) {  // one goroutine per datanode, no cancel
+        res[i] = raw.empty() ? nodes_[i].client->Put(key, meta, shards[i])
+                             : nodes_[i].client->PutWithChecksum(key, meta, shards[i],
+                                                                 entry_checksum(meta, shards[i].size(), raw[i]));
+    }, S);
     QuorumWait w(wq, int(nodes_.size()) - wq + 1);
-    for (size_t i = 0; i < nodes_.size(); i++)  // no cancel
-        w.add(raw.empty() ? nodes_[i].client->Put(key, meta, shards[i])
-                          : nodes_[i].client->PutWithChecksum(key, meta, shards[i],
-                                                              entry_checksum(meta, shards[i].size(), raw[i])));
+    for (const Status& r : res) w.add(r);
     return w.result("Write failed. Insufficient number of nodes online");
 }
 
 Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<Bytes>& blocks) {
+    Active act(active_);
     if (keys.size() != blocks.size()) return Status::Error("keys and blocks differ in length");
     const int k = config_.data_blocks, m = config_.parity_blocks, n = k + m;
     std::vector<Status> results(blocks.size());
@@ -286,15 +302,16 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 continue;
             }
             for (size_t j = 0; j < nb; j++) {
-                QuorumWait w(wq, n - wq + 1);
                 const uint8_t* base = flat + j * n * S;
-                for (int i = 0; i < n; i++) {
+                std::vector<Status> res(static_cast<size_t>(n));
+                fan(n, [&](int i) {
                     Bytes shard(base + size_t(i) * S, base + size_t(i + 1) * S);
-                    w.add(gpu_checksums_
-                              ? nodes_[i].client->PutWithChecksum(keys[idx[j]], meta, shard,
-                                                                  entry_checksum(meta, S, raw[j * n + i]))
-                              : nodes_[i].client->Put(keys[idx[j]], meta, shard));
-                }
+                    res[i] = gpu_checksums_ ? nodes_[i].client->PutWithChecksum(keys[idx[j]], meta, shard,
+                                                                                entry_checksum(meta, S, raw[j * n + i]))
+                                            : nodes_[i].client->Put(keys[idx[j]], meta, shard);
+                }, S);
+                QuorumWait w(wq, n - wq + 1);
+                for (const Status& r : res) w.add(r);
                 results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
             }
         }
@@ -304,9 +321,12 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
 }
 
 Status DagNode::DeleteBlock(const std::string& key) {  // node.go:191-208
+    Active act(active_);
     const int wq = EntryQuorum().second;
+    std::vector<Status> res(nodes_.size());
+    fan(int(nodes_.size()), [&](int i) { res[i] = nodes_[i].client->Delete(key); }, 0);  // cheap: stays serial
     QuorumWait w(wq, int(nodes_.size()) - wq + 1);
-    for (auto& sn : nodes_) w.add(sn.client->Delete(key));
+    for (const Status& r : res) w.add(r);
     return w.result("Write failed. Insufficient number of nodes online");
 }
 
@@ -319,6 +339,14 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
     f->shards.assign(static_cast<size_t>(n), Bytes());
     f->repair.clear();
     QuorumWait w(rq, n - rq + 1);
+    // Node i's fetch result, replayed in node order exactly as the sequential loop would use
+    // it.  Fetches run concurrently in waves: when node i is reached unfetched, the next
+    // (successes still needed) online nodes are fetched at once.  A fetch the replay never
+    // reaches (the quorum was decided first) is a cancelled goroutine: dropped, no repair.
+    std::vector<Bytes> data(static_cast<size_t>(n));
+    std::vector<Status> got(static_cast<size_t>(n));
+    std::vector<char> fetched(static_cast<size_t>(n), 0);
+    int succ = 0;
     for (int i = 0; i < n; i++) {
         if (!online[i]) {
             // runs even after the quorum is met: the goroutine returns before its first RPC
@@ -327,13 +355,23 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
             continue;
         }
         if (w.decided()) continue;  // cancelOther: later fetches are cancelled, no repair
-        Bytes m, data;
-        Status g = online[i]->client->Get(key, &m, &data);
-        if (!g.ok())
+        if (!fetched[i]) {
+            std::vector<int> wave;
+            for (int j = i; j < n && int(wave.size()) < std::max(1, rq - succ); j++)
+                if (online[j] && !fetched[j]) wave.push_back(j);
+            fan(int(wave.size()), [&](int t) {
+                Bytes m;
+                got[wave[t]] = online[wave[t]]->client->Get(key, &m, &data[wave[t]]);
+            }, size_t(ceil_frac(f->meta.block_size, config_.data_blocks)));
+            for (int j : wave) fetched[j] = 1;
+        }
+        if (!got[i].ok()) {
             f->repair.push_back(i);  // any non-cancel error (node.go:254-258)
-        else
-            f->shards[i] = std::move(data);
-        w.add(g);
+        } else {
+            f->shards[i] = std::move(data[i]);
+            succ++;
+        }
+        w.add(got[i]);
     }
     std::sort(f->repair.begin(), f->repair.end());
     return w.result(kErrReadQuorum);
@@ -365,6 +403,7 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
 }
 
 Status DagNode::Get(const std::string& key, Bytes* block) {
+    Active act(active_);
     Fetched f;
     Status s = fetch_for_get(key, &f);
     if (!s.ok()) return s;
@@ -373,6 +412,7 @@ Status DagNode::Get(const std::string& key, Bytes* block) {
 
 void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* blocks, std::vector<Status>* statuses,
                       size_t batch) {
+    Active act(active_);
     const int k = config_.data_blocks, m = config_.parity_blocks, n = k + m;
     if (batch == 0) batch = 1;
     blocks->assign(keys.size(), Bytes());
@@ -527,15 +567,32 @@ Status DagNode::fetch_for_repair(const std::string& key, int repair_index, std::
     const int n = int(nodes_.size()), rq = EntryQuorum().first;
     shards->assign(size_t(n), Bytes());
     QuorumWait w(rq, n - rq + 1);
+    // waves of concurrent fetches replayed in node order, as in fetch_for_get
+    std::vector<Bytes> data(static_cast<size_t>(n));
+    std::vector<Status> got(static_cast<size_t>(n));
+    std::vector<char> fetched(static_cast<size_t>(n), 0);
+    int succ = 0;
     for (int i = 0; i < n && !w.decided(); i++) {
         if (i == repair_index) {
             w.add(Status::Error("there is no data in this node"));
             continue;
         }
-        Bytes m, data;
-        Status g = nodes_[i].client->Get(key, &m, &data);
-        if (g.ok() && data.empty()) g = Status::Error("there is no data in this node");
-        if (g.ok()) (*shards)[i] = std::move(data);
+        if (!fetched[i]) {
+            std::vector<int> wave;
+            for (int j = i; j < n && int(wave.size()) < std::max(1, rq - succ); j++)
+                if (j != repair_index && !fetched[j]) wave.push_back(j);
+            fan(int(wave.size()), [&](int t) {
+                Bytes m;
+                got[wave[t]] = nodes_[wave[t]].client->Get(key, &m, &data[wave[t]]);
+            }, last_shard_.load());
+            for (int j : wave) fetched[j] = 1;
+        }
+        Status g = got[i];
+        if (g.ok() && data[i].empty()) g = Status::Error("there is no data in this node");
+        if (g.ok()) {
+            (*shards)[i] = std::move(data[i]);
+            succ++;
+        }
         w.add(g);
     }
     return w.result(kErrReadQuorum);

@@ -36,6 +36,7 @@
 
 #include "datanode.hpp"
 #include "erasure.hpp"
+#include "fanout.hpp"
 
 namespace rsmi {
 namespace host {
@@ -106,6 +107,14 @@ public:
     // instead of leaving the byte-serial CRC to the datanode.  On by
     // default; the stored entries are byte-identical either way.
     void SetGpuChecksums(bool v) { gpu_checksums_ = v; }
+    // The k+m datanode calls of one block run concurrently, like node.go's goroutine per
+    // datanode (fanout.hpp); results are replayed in node order, so every quorum outcome,
+    // repair list and error equals the sequential one.  On by default.
+    void SetParallelFanout(bool v) { parallel_ = v; }
+    // ... but only where it pays: a lone caller (concurrent callers already keep the cores
+    // busy) and shards of at least this many bytes (in-process datanode calls on small
+    // shards cost less than a thread hand-off).  Default 128 KiB (tools/bench_dagnode).
+    void SetFanoutMinBytes(size_t v) { fanout_min_ = v; }
     std::pair<int, int> EntryQuorum() const;  // (read, write)
     size_t RepairQueueLen();
 
@@ -131,6 +140,17 @@ private:
     int num_slots_ = 0;
     int device_ = 0;
     bool gpu_checksums_ = true;
+    bool parallel_ = true;
+    size_t fanout_min_ = size_t(128) << 10;
+    std::atomic<int> active_{0};          // caller threads inside the public calls
+    std::atomic<size_t> last_shard_{0};   // shard size of the latest Put / Get (for GetMeta)
+    std::unique_ptr<FanOut> fan_;
+    void fan(int count, const std::function<void(int)>& f, size_t shard_bytes);
+    struct Active {  // counts a caller for the fan-out policy
+        std::atomic<int>& a;
+        explicit Active(std::atomic<int>& x) : a(x) { a++; }
+        ~Active() { a--; }
+    };
 
     std::mutex q_mu_;
     std::condition_variable q_cv_;
