@@ -83,8 +83,10 @@ constexpr int default_prefetch() {
 // store them as u16 at crc_out[(block * crc_slots + shard) * tpb * 64 + chunk]; input row c is
 // shard in_row[c], output row j is shard crc_out_slot0 + out_row[j].  rs_crc16_combine_kernel
 // turns them into R(row).  The small host path uses this so the shard bytes cross PCIe once.
+// SH64: build the shifted selector words of two dwords with one 64-bit shift each
+// (v_lshrrev_b64; the bits that cross from the high dword land in masked-off positions).
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false>
+          bool UA = false, bool CRC = false, bool SH64 = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -241,13 +243,26 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
             for (int f = 0; f < 5; f++) T[f] = Tn[f];
 #pragma unroll
-            for (int d = 0; d < D; d++)
+            for (int d = 0; d < D; d++) {
+                uint32_t sh3[4], sh6[4];
+                if constexpr (SH64) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint64_t xx = (uint64_t(u4get(v[slot][d], 2 * h + 1)) << 32) | u4get(v[slot][d], 2 * h);
+                        uint64_t a = xx >> 3, b = xx >> 6;
+                        asm volatile("" : "+v"(a), "+v"(b));  // keep them 64-bit shifts
+                        sh3[2 * h] = uint32_t(a);
+                        sh3[2 * h + 1] = uint32_t(a >> 32);
+                        sh6[2 * h] = uint32_t(b);
+                        sh6[2 * h + 1] = uint32_t(b >> 32);
+                    }
+                }
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     const uint32_t x = u4get(v[slot][d], w);
                     const uint32_t s1 = x & 0x07070707u;
-                    const uint32_t s2 = (x >> 3) & 0x07070707u;
-                    const uint32_t s3 = (x >> 6) & 0x03030303u;
+                    const uint32_t s2 = (SH64 ? sh3[w] : x >> 3) & 0x07070707u;
+                    const uint32_t s3 = (SH64 ? sh6[w] : x >> 6) & 0x03030303u;
 #pragma unroll
                     for (int j = 0; j < MT; j++) {
 #ifndef RSMI_DIAG_NOMATH
@@ -280,6 +295,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                         }
                     }
                 }
+            }
             if constexpr (CRC) crc_store(v[slot][0], plan->in_row[c]);
             if (c + P < K) load_col(c + P, v[slot]);
             if (c + 1 < K) load_tables(c + 1, Tn);
@@ -610,9 +626,9 @@ void* crc16_rows_kernel(bool aligned, int fold) {
 
 // ------------------------------------------------------------------ dispatch table
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false>
+          bool UA = false, bool CRC = false, bool SH64 = false>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC, SH64>);
 }
 
 // fused chunk-CRC variants: UA, D = 1, the auto cache policy of the shape
@@ -675,6 +691,8 @@ const ExpKernelTable& exp_kernels() {
         x.fn[1][2] = fast_ptr<10, 1, 1, 1, 10>();
         x.fn[0][3] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 1>();
         x.fn[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 1>();
+        x.fn[0][4] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, true>();
+        x.fn[1][4] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, true>();
         return x;
     }();
     return t;

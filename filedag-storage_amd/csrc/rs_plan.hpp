@@ -33,7 +33,7 @@ struct FastKernelTable {
 // v 0/1/2 = 4/8/10 rows in flight (NT=1); v 3 = split table source (TS=1; NT 1 for MT4,
 // 2 for MT1, the auto policy's choices).
 struct ExpKernelTable {
-    void* fn[2][4];
+    void* fn[2][5];  // v 4 = 64-bit selector shifts (SH64)
 };
 
 const FastKernelTable& fast_kernels();

@@ -300,10 +300,10 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][pi];
             pf_label = c->opt_prefetch;
-        } else if (fn && !ua && c->opt_tables == 1 && t.K == 10 && D == 1 &&
+        } else if (fn && !ua && c->opt_tables >= 1 && t.K == 10 && D == 1 &&
                    ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
-            fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][3];
-            ts_label = 1;
+            fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][c->opt_tables == 1 ? 3 : 4];
+            ts_label = c->opt_tables;
         }
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
@@ -336,7 +336,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             if (ua) c->last_kernel += ",UA";
             if (fuse) c->last_kernel += ",CRC";
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
-            if (ts_label) c->last_kernel += ",TS=1";
+            if (ts_label) c->last_kernel += ts_label == 1 ? ",TS=1" : ",SH64";
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -524,7 +524,7 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
     } else if (!std::strcmp(key, "tables")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
     } else if (!std::strcmp(key, "small_call_bytes")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
