@@ -166,7 +166,6 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         }
         auto crc_store = [&](u32x4 x, uint32_t shard) {
             if constexpr (CRC) {
-                const uint32_t ch = ch0;
                 {
                     x &= keep;
                     const uint8_t* nbt = reinterpret_cast<const uint8_t*>(s_crc);

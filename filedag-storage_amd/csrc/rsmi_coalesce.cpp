@@ -1,0 +1,163 @@
+// rsmi_coalesce.cpp -- group commit of concurrent single-block calls (see rsmi_impl.hpp).
+//
+// DagNode.Put hands the engine one block per call (node.go:358-408), from many goroutines at
+// once.  Group commit turns those calls into GPU batches without a thread of our own: a
+// caller that finds no batch executing becomes the executor, takes every request queued so
+// far (optionally waiting coalesce_us for more), runs them grouped by key (kind, shard size
+// and, for reconstruct, the erasure pattern) through the host batch paths, and wakes their
+// callers.  Requests that arrive while a batch runs form the next batch.  A lone caller
+// never waits: its batch is itself.
+
+#include "rsmi_impl.hpp"
+
+using namespace rsmi;
+using namespace rsmi::impl;
+
+namespace rsmi {
+namespace impl {
+
+// page-locked staging of the executing batch (only the executor touches it)
+uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
+    if (c->h_coal_cap >= need) return c->h_coal;
+    if (c->h_coal) (void)hipHostFree(c->h_coal);
+    c->h_coal = nullptr;
+    c->h_coal_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_coal), need, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    c->h_coal_cap = need;
+    return c->h_coal;
+}
+
+// One group of a coalesced batch: same request key, i.e. same kind and shard size (and,
+// for reconstruct, the same survivor pattern and requested rows).
+void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    const std::string& key = rq[0]->key;
+    const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
+    uint8_t* h = coal_stage(c, nb * n * S);
+    if (!h) {
+        for (size_t j = 0; j < nb; j++) rq[j]->rc = RSMI_ERR_DEVICE;
+        return;
+    }
+    if (key[0] == 'E') {
+        bool want_raw = false;
+        for (size_t j = 0; j < nb; j++) {
+            uint8_t* dst = h + j * n * S;
+            std::memcpy(dst, rq[j]->block, rq[j]->B);
+            std::memset(dst + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
+            want_raw |= rq[j]->raw != nullptr;
+        }
+        std::vector<uint32_t> raw(want_raw ? nb * n : 0);
+        const int rc = encode_host_impl(c, h, n * S, h + k * S, n * S, S, nb, want_raw ? raw.data() : nullptr);
+        for (size_t j = 0; j < nb; j++) {
+            rq[j]->rc = rc;
+            if (rc) continue;
+            std::memcpy(rq[j]->out, h + j * n * S, n * S);
+            if (rq[j]->raw) std::memcpy(rq[j]->raw, raw.data() + j * n, n * 4);
+        }
+        return;
+    }
+    // 'R': key = "R<S>:<n flags present><n flags want>"
+    const char* f = key.c_str() + key.find(':') + 1;
+    std::vector<uint8_t> present(n), want(n);
+    for (size_t i = 0; i < n; i++) {
+        present[i] = uint8_t(f[i] == '1');
+        want[i] = uint8_t(f[n + i] == '1');
+    }
+    for (size_t j = 0; j < nb; j++) std::memcpy(h + j * n * S, rq[j]->out, n * S);
+    const int rc = reconstruct_host_impl(c, h, n * S, S, nb, present.data(), want.data());
+    for (size_t j = 0; j < nb; j++) {
+        rq[j]->rc = rc;
+        if (rc) continue;
+        for (size_t i = 0; i < n; i++)
+            if (!present[i] && want[i]) std::memcpy(rq[j]->out + i * S, h + (j * n + i) * S, S);
+    }
+}
+
+void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
+    const size_t n = size_t(c->n);
+    std::map<std::string, std::vector<rsmi_ctx::CoalReq*>> groups;
+    for (auto* r : batch) groups[r->key].push_back(r);
+    for (auto& g : groups) {
+        const std::string& key = g.first;
+        const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
+        const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
+        for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk)
+            run_coalesced_group(c, g.second.data() + j0, std::min(chunk, g.second.size() - j0));
+    }
+}
+
+// Queue a request and either wait for the executor or become it (group commit).
+int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        int rc = ensure_device(c);
+        if (rc) return rc;
+    }
+    c->stat_coal_calls++;
+    std::unique_lock<std::mutex> lk(c->q_mu);
+    c->q_pending.push_back(&req);
+    c->q_cv.notify_all();  // an executor waiting out coalesce_us may now have enough
+    while (!req.done) {
+        if (c->q_executing) {
+            c->q_cv.wait(lk);
+            continue;
+        }
+        c->q_executing = true;
+        const size_t cap = size_t(c->opt_coalesce_max);
+        if (c->opt_coalesce_us > 0 && c->q_pending.size() < cap)
+            c->q_cv.wait_for(lk, std::chrono::microseconds(c->opt_coalesce_us),
+                             [&] { return c->q_pending.size() >= cap; });
+        const size_t take = std::min(cap, c->q_pending.size());
+        std::vector<rsmi_ctx::CoalReq*> batch(c->q_pending.begin(), c->q_pending.begin() + take);
+        c->q_pending.erase(c->q_pending.begin(), c->q_pending.begin() + take);
+        lk.unlock();
+        run_coalesced(c, batch);
+        c->stat_coal_batches++;
+        lk.lock();
+        for (auto* r : batch) r->done = true;
+        c->q_executing = false;
+        c->q_cv.notify_all();
+    }
+    return req.rc;
+}
+
+}  // namespace impl
+}  // namespace rsmi
+
+extern "C" {
+
+int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                uint32_t* raw_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+    rsmi_ctx::CoalReq req{block, B, shards_out, raw_out, "E" + std::to_string(rsmi_shard_size(B, c->k)) + ":",
+                          RSMI_OK, false};
+    return coalesce(c, req);
+}
+
+int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+    if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    const std::vector<uint8_t> want = want_mask(c, present, data_only);
+    int pre = reconstruct_precheck(c, present, want.data());
+    if (pre < 0) return -pre;
+    if (pre == 1) return RSMI_OK;
+    std::string key = "R" + std::to_string(S) + ":";
+    for (int i = 0; i < c->n; i++) key.push_back(present[i] ? '1' : '0');
+    for (int i = 0; i < c->n; i++) key.push_back(want[i] ? '1' : '0');
+    rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, std::move(key), RSMI_OK, false};
+    return coalesce(c, req);
+}
+
+long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
+    if (!c || !key) return -1;
+    if (!std::strcmp(key, "coalesced_calls")) return long(c->stat_coal_calls.load());
+    if (!std::strcmp(key, "coalesced_batches")) return long(c->stat_coal_batches.load());
+    return -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// rsmi_crc.cpp -- the datanode entry checksum (dag/node/datanode/server.go:58-75) on the GPU:
+// the R(row) pass, the encode with the CRC fused in, and the host-side header fold
+// (crc16.hpp has the algebra; rsmi_impl.hpp the file map).
+#include "rsmi_impl.hpp"
+
+using namespace rsmi;
+using namespace rsmi::impl;
+
+namespace rsmi {
+namespace impl {
+
+// CRC-16 device tables, uploaded once per context (caller holds ctx->mu)
+int ensure_crc_tables(rsmi_ctx* c) {
+    if (c->d_crc_tbl) return RSMI_OK;
+    const Crc16Tables& t = crc16_tables();
+    static_assert(sizeof(t.P) + sizeof(t.U) + sizeof(t.N) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
+    std::memcpy(h.data(), t.P, sizeof(t.P));
+    std::memcpy(h.data() + kCrcPWords * 2, t.U, sizeof(t.U));
+    std::memcpy(h.data() + (kCrcPWords + kCrcUWords) * 2, t.N, sizeof(t.N));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
+    HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    return RSMI_OK;
+}
+
+// R(row) of nrows rows per block into out[b*out_bs + r] (zeroed first), stream-ordered.
+int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
+               uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream, bool zero) {
+    if (!nblocks || !nrows) return RSMI_OK;
+    int rc = ensure_crc_tables(c);
+    if (rc) return rc;
+    if (zero) HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
+    if (S == 0) return RSMI_OK;  // R(empty) = 0
+    const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
+    void* fn = crc16_rows_kernel(aligned, c->opt_crc_fold);
+    const uint64_t tile = uint64_t(kWave) * 16;
+    uint32_t tpb = uint32_t((S + tile - 1) / tile);
+    uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
+    uint64_t nitems = nblocks * nrows * nseg;
+    int& occ = c->occupancy[fn];
+    if (occ <= 0) {
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
+        if (occ <= 0) occ = 1;
+    }
+    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
+    const uint32_t* tb = c->d_crc_tbl;
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
+    HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
+    return RSMI_OK;
+}
+
+// Encode with fused per-chunk CRCs, then R(row) of all k+m rows of every block into
+// raw[b * (k+m) + row] (device or page-locked host memory).  Needs S >= 16 and k <= 16.
+int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                             size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+    const size_t k = size_t(c->k), n = size_t(c->n);
+    const size_t cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
+    int rc;
+    if ((rc = ensure_crc_tables(c))) return rc;
+    if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
+    CrcFuse fz;
+    fz.tbl = c->d_crc_tbl;
+    fz.out = reinterpret_cast<uint16_t*>(c->d_chunks);
+    fz.slots = uint32_t(n);
+    fz.out_slot0 = uint32_t(k);
+    if ((rc = launch_plan(c, plan, in, in_rs, in_bs, out, out_rs, out_bs, S, nblocks, st, &fz))) return rc;
+    const uint16_t* ch = fz.out;
+    uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
+    uint64_t S64 = S, rows = nblocks * n;
+    const uint32_t* tb = c->d_crc_tbl;
+    void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &raw};
+    const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
+    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+    return RSMI_OK;
+}
+
+}  // namespace impl
+}  // namespace rsmi
+
+extern "C" {
+
+int rsmi_encode_batch_dev_crc(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_stride, size_t data_block_stride,
+                              uint8_t* d_parity, size_t parity_shard_stride, size_t parity_block_stride, size_t S,
+                              size_t nblocks, uint32_t* d_raw_out, void* stream) {
+    if (!c || !d_data || !d_parity || !d_raw_out) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    if (data_shard_stride < S || parity_shard_stride < S) return RSMI_ERR_INVALID_ARG;
+    if (nblocks == 0) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    std::shared_ptr<Plan> plan;
+    if ((rc = encode_plan(c, plan))) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    if (S >= 16 && k <= 16)
+        return launch_encode_crc(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
+                                 parity_block_stride, S, nblocks, d_raw_out, st);
+    // S < 16 or k > 16: the encode, then the CRC pass over both row sets
+    if ((rc = launch_plan(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
+                          parity_block_stride, S, nblocks, st)))
+        return rc;
+    HIP_TRY(hipMemsetAsync(d_raw_out, 0, nblocks * n * 4, st));
+    if ((rc = launch_crc(c, d_data, data_shard_stride, data_block_stride, uint32_t(k), S, nblocks, d_raw_out, n, st,
+                         false)))
+        return rc;
+    return launch_crc(c, d_parity, parity_shard_stride, parity_block_stride, uint32_t(m), S, nblocks, d_raw_out + k, n,
+                      st, false);
+}
+
+int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) {
+    if (!c || !d_rows || !d_raw_out || nrows < 0 || out_block_stride < size_t(nrows)) return RSMI_ERR_INVALID_ARG;
+    if (nrows > 1 && shard_stride < S) return RSMI_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    rc = launch_crc(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
+                    static_cast<hipStream_t>(stream));
+    if (rc) return rc;
+    c->last_kernel = "rs_crc16_rows_kernel";
+    return hip_status(hipGetLastError());
+}
+
+uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
+
+uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
+    return crc16_entry(head, head_len, raw, data_len);
+}
+
+}  // extern "C"

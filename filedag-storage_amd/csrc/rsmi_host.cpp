@@ -1,0 +1,442 @@
+// rsmi_host.cpp -- host-memory entry points of include/rsmi.h (see rsmi_impl.hpp).
+//
+// Host-memory calls.  Page-locked buffers of any size, and small pageable calls staged by CPU
+// copies, run as one unaligned-window kernel in place over PCIe (encode_small /
+// reconstruct_small).  Larger pageable calls take the copy-engine pipeline: chunks of blocks
+// round-robin over 3 streams, each with its own device buffers: H2D -> kernel -> D2H.  When S
+// is a multiple of 8 the DMA engines move rows straight between the contiguous host layout
+// (pitch S) and the pitched device layout with 2-D copies at full PCIe rate.  Odd-width 2-D
+// copies crawl (3-9 GB/s measured, tools/copyprobe.py), so for other S the PCIe copies stay
+// linear and rs_repitch_kernel re-lays rows out on the device (HBM-speed, ~1% of the PCIe
+// time).
+
+#include "rsmi_impl.hpp"
+
+using namespace rsmi;
+using namespace rsmi::impl;
+
+namespace rsmi {
+namespace impl {
+
+bool dma_2d_ok(size_t S) { return S % 8 == 0; }
+
+int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width, size_t rows,
+            hipStream_t stream) {
+    if (!rows || !width) return RSMI_OK;
+    uint64_t sp = spitch, dp = dpitch, w = width, r = rows;
+    const uint64_t dwords = ((w + 6) / 4 + 1) * r;
+    const uint32_t grid = uint32_t(std::min<uint64_t>((dwords + kWG - 1) / kWG, 8192));
+    void* args[] = {&src, &sp, &dst, &dp, &w, &r};
+    HIP_TRY(hipLaunchKernel(repitch_kernel(), dim3(grid), dim3(kWG), args, 0, stream));
+    return RSMI_OK;
+}
+
+// Device-visible alias of the page-locked host range [p, p + len) (hipHostMalloc /
+// rsmi_host_alloc memory), or nullptr when the range is pageable memory.  On the odd-S
+// (linear copy) path, results bound for such a range are written by the repitch kernel
+// straight over PCIe: the copy engines were measured running the linear host->device and
+// device->host transfers one after the other, and taking the write-back off them lets it
+// overlap the next chunk's upload (tools/hostsweep.py, RS(10,4) 256 KiB: encode 41.7 -> 47.6
+// GiB/s).  Reconstruct also uploads by kernel loads from such memory (below).  With 2-D
+// DMA rows (S % 8 == 0) the engines already overlap, so that path keeps its copies.
+uint8_t* host_alias(void* p, size_t len) {
+    auto alias = [](void* q) -> uint8_t* {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: not an error for the caller
+            return nullptr;
+        }
+        if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+        return static_cast<uint8_t*>(a.devicePointer) + (static_cast<uint8_t*>(q) - static_cast<uint8_t*>(a.hostPointer));
+    };
+    uint8_t* first = alias(p);
+    if (!first || len == 0) return first;
+    uint8_t* last = alias(static_cast<uint8_t*>(p) + len - 1);
+    return last == first + (len - 1) ? first : nullptr;  // one allocation end to end
+}
+
+// ---------------------------------------------------------------- small host calls
+// A per-block call (DagNode.Put / Get, one 256 KiB block) is latency-bound: the copy-engine
+// path pays a DMA setup on each side of the kernel.  Small calls instead run ONE kernel that
+// reads its input rows from page-locked host memory and writes its output rows back over
+// PCIe (the unaligned-window kernels take the Split layout's odd row pitch as is).  Pageable
+// callers (Go slices over cgo) are staged through a page-locked buffer by CPU copies.
+// Caller holds ctx->mu.
+uint8_t* small_stage(rsmi_ctx* c, size_t need) {
+    if (c->h_small_cap >= need) return c->h_small;
+    if (c->h_small) (void)hipHostFree(c->h_small);
+    c->h_small = nullptr;
+    c->h_small_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_small), std::max<size_t>(need, 1 << 20), hipHostMallocDefault) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    c->h_small_cap = std::max<size_t>(need, 1 << 20);
+    return c->h_small;
+}
+
+int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
+                        size_t S, size_t nblocks, uint32_t* raw_out) {
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    hipStream_t st = c->staging[0].stream;
+    const uint8_t* in = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * dbs + k * S);
+    uint8_t* out = host_alias(parity, (nblocks - 1) * pbs + m * S);
+    size_t in_bs = dbs, out_bs = pbs;
+    // page-locked staging, only the parts needed: [data rows | parity rows | raw CRCs]
+    const bool stage_in = in == nullptr, stage_out = out == nullptr;
+    const size_t in_sz = stage_in ? nblocks * k * S : 0, out_sz = stage_out ? nblocks * m * S : 0;
+    const size_t raw_sz = raw_out ? nblocks * n * 4 : 0;
+    uint8_t* hs = nullptr;
+    if (in_sz + out_sz + raw_sz) {
+        hs = small_stage(c, in_sz + out_sz + raw_sz);
+        if (!hs) return RSMI_ERR_DEVICE;
+    }
+    if (stage_in) {
+        for (size_t b = 0; b < nblocks; b++) std::memcpy(hs + b * k * S, data + b * dbs, k * S);
+        in = host_alias(hs, in_sz);
+        in_bs = k * S;
+    }
+    uint8_t* hout = hs ? hs + in_sz : nullptr;
+    if (stage_out) {
+        out = host_alias(hout, out_sz);
+        out_bs = m * S;
+    }
+    uint32_t* hraw = raw_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz) : nullptr;
+    if (!in || !out) return RSMI_ERR_DEVICE;
+    int rc;
+    if (raw_out && S >= 16 && k <= 16) {
+        // fused: the encode stores per-chunk CRCs of every row it reads and writes (the shard
+        // bytes cross PCIe once), then one wave per row combines them into R(row) and stores
+        // it straight into the page-locked staging
+        uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, raw_sz));
+        if (!draw) return RSMI_ERR_DEVICE;
+        if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, draw, st))) return rc;
+    } else {
+        if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
+        if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
+            if ((rc = reserve(c->d_crc, c->crc_cap, raw_sz))) return rc;
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc);
+            HIP_TRY(hipMemsetAsync(cr, 0, raw_sz, st));
+            if ((rc = launch_crc(c, in, S, in_bs, uint32_t(k), S, nblocks, cr, n, st, false))) return rc;
+            if ((rc = launch_crc(c, out, S, out_bs, uint32_t(m), S, nblocks, cr + k, n, st, false))) return rc;
+            if ((rc = repitch(host_alias(hraw, raw_sz), raw_sz, reinterpret_cast<uint8_t*>(cr), raw_sz, raw_sz, 1,
+                              st)))
+                return rc;
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (stage_out)
+        for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
+    if (raw_out) std::memcpy(raw_out, hraw, raw_sz);
+    return RSMI_OK;
+}
+
+int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
+    if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    if (data_block_stride < size_t(c->k) * S || parity_block_stride < size_t(c->m) * S) return RSMI_ERR_INVALID_ARG;
+    if (nblocks == 0) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    std::shared_ptr<Plan> plan;
+    rc = encode_plan(c, plan);
+    if (rc) return rc;
+    const size_t k = size_t(c->k), m = size_t(c->m);
+    // One zero-copy kernel (encode_small) when both sides are page-locked, whatever the size
+    // (tools/hostsweep.py "direct": equal to the copy-engine pipeline for encode, +8-18% for
+    // reconstruct), or when the call is small; pageable input is staged by CPU copies, and
+    // above half the small-call limit the copy engines win (tools/latency.cpp, 1 MiB blocks:
+    // 107 us staged against 99 us).
+    const size_t total = nblocks * (k + m) * S;
+    const bool in_pinned = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S);
+    const bool pinned = in_pinned && host_alias(parity, (nblocks - 1) * parity_block_stride + m * S);
+    if ((c->opt_zero_copy && pinned) ||
+        (total <= size_t(c->opt_small_bytes) && (2 * total <= size_t(c->opt_small_bytes) || in_pinned)))
+        return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+    const size_t Sp = rsmi_recommended_pitch(S);
+    const size_t in_bs = k * Sp, out_bs = m * Sp;
+    const bool d2 = dma_2d_ok(S);
+    const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (in_bs + out_bs));
+    const int ns = nblocks > chunk ? 3 : 1;
+    // odd S: parity straight into page-locked host memory when it is one contiguous
+    // [block][row][S] run (host_alias); 2-D DMA rows stay faster than kernel stores
+    uint8_t* zc = c->opt_zero_copy && !d2 ? host_alias(parity, (nblocks - 1) * parity_block_stride + m * S) : nullptr;
+    // zero_copy 2 (A/B only): the upload by kernel loads too (RS(10,4) 256 KiB: 47.6 -> 34.6
+    // GiB/s; the copy engine uploads a whole data block faster than kernel loads do)
+    const uint8_t* zin = c->opt_zero_copy == 2 && !d2
+                             ? host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * data_block_stride + k * S)
+                             : nullptr;
+    const size_t n = k + m;
+    if (raw_out && (rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
+    for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
+        Staging& st = c->staging[i % ns];
+        const size_t nb = std::min(chunk, nblocks - b0);
+        if ((rc = reserve(st.d_in, st.in_cap, nb * in_bs))) return rc;
+        if ((rc = reserve(st.d_out, st.out_cap, nb * out_bs))) return rc;
+        if (!d2 && !zin && (rc = reserve(st.d_lin, st.lin_cap, nb * k * S))) return rc;
+        const uint8_t* src = data + b0 * data_block_stride;
+        uint8_t* dst = parity + b0 * parity_block_stride;
+        // host -> device
+        if (zin) {
+            for (size_t r = 0; r < k; r++)
+                if ((rc = repitch(st.d_in + r * Sp, in_bs, zin + b0 * data_block_stride + r * S, data_block_stride, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2 && data_block_stride == k * S) {
+            HIP_TRY(hipMemcpy2DAsync(st.d_in, Sp, src, S, S, nb * k, hipMemcpyHostToDevice, st.stream));
+        } else if (d2) {
+            for (size_t b = 0; b < nb; b++)
+                HIP_TRY(hipMemcpy2DAsync(st.d_in + b * in_bs, Sp, src + b * data_block_stride, S, S, k,
+                                         hipMemcpyHostToDevice, st.stream));
+        } else {
+            if (data_block_stride == k * S)
+                HIP_TRY(hipMemcpyAsync(st.d_lin, src, nb * k * S, hipMemcpyHostToDevice, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(st.d_lin + b * k * S, src + b * data_block_stride, k * S,
+                                           hipMemcpyHostToDevice, st.stream));
+            if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * k, st.stream))) return rc;
+        }
+        if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
+        if (raw_out) {  // R(shard) of the k data rows and the m parity rows, [block][row]
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n;
+            HIP_TRY(hipMemsetAsync(cr, 0, nb * n * 4, st.stream));
+            if ((rc = launch_crc(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream, false))) return rc;
+            if ((rc = launch_crc(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream, false)))
+                return rc;
+        }
+        // device -> host
+        if (zc && parity_block_stride == m * S) {
+            if ((rc = repitch(zc + b0 * m * S, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
+        } else if (zc) {
+            for (size_t r = 0; r < m; r++)
+                if ((rc = repitch(zc + b0 * parity_block_stride + r * S, parity_block_stride, st.d_out + r * Sp, out_bs,
+                                  S, nb, st.stream)))
+                    return rc;
+        } else if (d2 && parity_block_stride == m * S) {
+            HIP_TRY(hipMemcpy2DAsync(dst, S, st.d_out, Sp, S, nb * m, hipMemcpyDeviceToHost, st.stream));
+        } else if (d2) {
+            for (size_t b = 0; b < nb; b++)
+                HIP_TRY(hipMemcpy2DAsync(dst + b * parity_block_stride, S, st.d_out + b * out_bs, Sp, S, m,
+                                         hipMemcpyDeviceToHost, st.stream));
+        } else {
+            // reuse d_lin (its H2D contents are consumed by the repitch above, in stream order)
+            if ((rc = repitch(st.d_lin, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
+            if (parity_block_stride == m * S)
+                HIP_TRY(hipMemcpyAsync(dst, st.d_lin, nb * m * S, hipMemcpyDeviceToHost, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(dst + b * parity_block_stride, st.d_lin + b * m * S, m * S,
+                                           hipMemcpyDeviceToHost, st.stream));
+        }
+    }
+    for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
+    if (raw_out) HIP_TRY(hipMemcpy(raw_out, c->d_crc, nblocks * n * 4, hipMemcpyDeviceToHost));
+    return RSMI_OK;
+}
+
+// Small reconstruct calls in place over PCIe (see encode_small): page-locked shards are
+// read and rebuilt where they lie; pageable ones are staged (survivor rows in, rebuilt rows
+// back).  Caller holds ctx->mu.
+int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                             const uint8_t* present, const uint8_t* want) {
+    const size_t n = size_t(c->n);
+    hipStream_t st = c->staging[0].stream;
+    uint8_t* dev = host_alias(shards, (nblocks - 1) * bs + n * S);
+    size_t dbs = bs;
+    uint8_t* hs = nullptr;
+    if (!dev) {
+        hs = small_stage(c, nblocks * n * S);
+        if (!hs) return RSMI_ERR_DEVICE;
+        for (size_t b = 0; b < nblocks; b++)
+            for (size_t i = 0; i < n; i++)
+                if (present[i]) std::memcpy(hs + (b * n + i) * S, shards + b * bs + i * S, S);
+        dev = host_alias(hs, nblocks * n * S);
+        dbs = n * S;
+        if (!dev) return RSMI_ERR_DEVICE;
+    }
+    int rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hs)
+        for (size_t b = 0; b < nblocks; b++)
+            for (size_t i = 0; i < n; i++)
+                if (!present[i] && want[i]) std::memcpy(shards + b * bs + i * S, hs + (b * n + i) * S, S);
+    return RSMI_OK;
+}
+
+int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                 const uint8_t* present, const uint8_t* want) {
+    if (!c || !shards || !present || !want) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    if (block_stride < size_t(c->n) * S) return RSMI_ERR_INVALID_ARG;
+    int pre = reconstruct_precheck(c, present, want);
+    if (pre < 0) return -pre;
+    if (pre == 1 || nblocks == 0) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    std::shared_ptr<Plan> plan;
+    rc = reconstruct_plan(c, present, want, plan);
+    if (rc) return rc;
+    // zero-copy in place when the shards are page-locked (hostsweep "direct": +8-18% over the
+    // pipeline) or the call is small (see encode_host_impl)
+    if ((c->opt_zero_copy && host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)) ||
+        nblocks * size_t(c->n) * S <= size_t(c->opt_small_bytes))
+        return reconstruct_small(c, *plan, shards, block_stride, S, nblocks, present, want);
+    // rows to ship: the k survivors in; the missing rows the plan writes, out
+    std::vector<int> in_rows, out_rows;
+    for (int i = 0; i < c->n && int(in_rows.size()) < c->k; i++)
+        if (present[i]) in_rows.push_back(i);
+    for (int i = 0; i < c->n; i++)
+        if (!present[i] && want[i]) out_rows.push_back(i);
+    const size_t n = size_t(c->n), nr = out_rows.size();
+    const size_t Sp = rsmi_recommended_pitch(S);
+    const size_t bs = n * Sp;
+    const bool d2 = dma_2d_ok(S);
+    const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / bs);
+    const int ns = nblocks > chunk ? 3 : 1;
+    // odd S: rebuilt rows straight into page-locked host memory (see host_alias)
+    uint8_t* zc = c->opt_zero_copy && !d2 ? host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)
+                                          : nullptr;
+    // the upload by kernel loads too: only the k rows the plan reads cross PCIe, where the
+    // linear copy would ship whole blocks (RS(10,4) 256 KiB batches: 35.5 -> 42.9 GiB/s).
+    // One launch per row, so small calls keep the single linear copy (tools/latency.cpp:
+    // a 4 KiB block took 59 us this way against 26 us with the copy).
+    const uint8_t* zin = nblocks * size_t(c->n) * S >= (size_t(4) << 20) ? zc : nullptr;
+    if (!d2 && !zc) {  // pinned landing area for the rebuilt rows, scattered on the host at the end
+        const size_t need = nblocks * nr * S;
+        if (c->h_stage_cap < need) {
+            if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
+            c->h_stage = nullptr;
+            c->h_stage_cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), need, hipHostMallocDefault));
+            c->h_stage_cap = need;
+        }
+    }
+    for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
+        Staging& st = c->staging[i % ns];
+        const size_t nb = std::min(chunk, nblocks - b0);
+        if ((rc = reserve(st.d_in, st.in_cap, nb * bs))) return rc;
+        uint8_t* h = shards + b0 * block_stride;
+        if (zin) {  // only the k rows the plan reads cross PCIe
+            for (int r : in_rows)
+                if ((rc = repitch(st.d_in + size_t(r) * Sp, bs, zin + b0 * block_stride + size_t(r) * S, block_stride, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2) {
+            for (int r : in_rows)
+                HIP_TRY(hipMemcpy2DAsync(st.d_in + size_t(r) * Sp, bs, h + size_t(r) * S, block_stride, S, nb,
+                                         hipMemcpyHostToDevice, st.stream));
+        } else {
+            // whole blocks move linearly (missing rows ride along as don't-care bytes)
+            if ((rc = reserve(st.d_lin, st.lin_cap, nb * n * S))) return rc;
+            if (block_stride == n * S)
+                HIP_TRY(hipMemcpyAsync(st.d_lin, h, nb * n * S, hipMemcpyHostToDevice, st.stream));
+            else
+                for (size_t b = 0; b < nb; b++)
+                    HIP_TRY(hipMemcpyAsync(st.d_lin + b * n * S, h + b * block_stride, n * S, hipMemcpyHostToDevice,
+                                           st.stream));
+            if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * n, st.stream))) return rc;
+        }
+        if ((rc = launch_plan(c, *plan, st.d_in, Sp, bs, st.d_in, Sp, bs, S, nb, st.stream))) return rc;
+        if (zc) {
+            for (int r : out_rows)
+                if ((rc = repitch(zc + b0 * block_stride + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S,
+                                  nb, st.stream)))
+                    return rc;
+        } else if (d2) {
+            for (int r : out_rows)
+                HIP_TRY(hipMemcpy2DAsync(h + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S, nb,
+                                         hipMemcpyDeviceToHost, st.stream));
+        } else {
+            // gather rebuilt rows compactly as [row][block][S], then one linear D2H
+            for (size_t j = 0; j < nr; j++)
+                if ((rc = repitch(st.d_lin + j * nb * S, S, st.d_in + size_t(out_rows[j]) * Sp, bs, S, nb,
+                                  st.stream)))
+                    return rc;
+            HIP_TRY(hipMemcpyAsync(c->h_stage + b0 * nr * S, st.d_lin, nb * nr * S, hipMemcpyDeviceToHost,
+                                   st.stream));
+        }
+    }
+    for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
+    if (!d2 && !zc) {
+        for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
+            const size_t nb = std::min(chunk, nblocks - b0);
+            const uint8_t* hs = c->h_stage + b0 * nr * S;
+            for (size_t j = 0; j < nr; j++)
+                for (size_t b = 0; b < nb; b++)
+                    std::memcpy(shards + (b0 + b) * block_stride + size_t(out_rows[j]) * S, hs + (j * nb + b) * S, S);
+        }
+    }
+    return RSMI_OK;
+}
+
+}  // namespace impl
+}  // namespace rsmi
+
+extern "C" {
+
+// ---------------------------------------------------------------- host memory, one block
+int rsmi_encode(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
+    if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    return rsmi_encode_batch_host(c, data, size_t(c->k) * S, parity, size_t(c->m) * S, S, 1);
+}
+
+int rsmi_encode_block(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;  // upstream Split checks this first
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+    const size_t S = rsmi_shard_size(B, c->k);
+    std::memcpy(shards_out, block, B);
+    std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
+    return rsmi_encode(c, shards_out, shards_out + size_t(c->k) * S, S);
+}
+
+int rsmi_reconstruct(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+    if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    return rsmi_reconstruct_batch_host(c, shards, size_t(c->n) * S, S, 1, present, data_only);
+}
+
+int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                           size_t parity_block_stride, size_t S, size_t nblocks) {
+    return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, nullptr);
+}
+
+int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                               size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
+    if (!raw_out) return RSMI_ERR_INVALID_ARG;
+    return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+}
+
+int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out || !raw_out) return RSMI_ERR_INVALID_ARG;
+    const size_t S = rsmi_shard_size(B, c->k);
+    std::memcpy(shards_out, block, B);
+    std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
+    return encode_host_impl(c, shards_out, size_t(c->k) * S, shards_out + size_t(c->k) * S, size_t(c->m) * S, S, 1,
+                            raw_out);
+}
+
+int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                const uint8_t* present, int data_only) {
+    if (!c || !present) return RSMI_ERR_INVALID_ARG;
+    const std::vector<uint8_t> w = want_mask(c, present, data_only);
+    return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, w.data());
+}
+
+int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                     const uint8_t* present, const uint8_t* required) {
+    return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required);
+}
+
+}  // extern "C"

@@ -1,0 +1,175 @@
+// rsmi_impl.hpp -- internals shared by the C-ABI implementation files (include/rsmi.h):
+//   rsmi_core.cpp      contexts, coding plans, kernel dispatch, options, device-resident calls
+//   rsmi_host.cpp      host-memory calls: zero-copy single kernel, copy-engine pipeline
+//   rsmi_crc.cpp       datanode CRC-16 on the GPU (separate pass and fused into the encode)
+//   rsmi_coalesce.cpp  group commit of concurrent single-block calls
+// No CPU compute path anywhere: every byte of parity, reconstructed data or CRC comes out of
+// the HIP kernels in rs_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rsmi.h"
+#include "crc16.hpp"
+#include "gf256.hpp"
+#include "rs_plan.hpp"
+
+namespace rsmi {
+namespace impl {
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+
+struct DevTile {
+    RsPlanDev* dev = nullptr;
+    int K = 0, MT = 0;
+};
+
+struct Plan {
+    std::vector<DevTile> tiles;
+    int device = -1;
+    ~Plan() {
+        if (device >= 0) {
+            (void)hipSetDevice(device);
+            for (auto& t : tiles)
+                if (t.dev) (void)hipFree(t.dev);
+        }
+    }
+};
+
+struct Staging {
+    hipStream_t stream = nullptr;
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint8_t* d_lin = nullptr;  // linear (pitch S) landing buffer for odd S
+    size_t in_cap = 0, out_cap = 0, lin_cap = 0;
+};
+
+// Launch every tile of a plan over nblocks blocks.
+// Fused per-chunk CRC output of a launch (rs_fast_kernel CRC variants): chunk values of every
+// row the plan reads or writes, at out[(block * slots + shard) * cpb + chunk].
+struct CrcFuse {
+    const uint32_t* tbl = nullptr;
+    uint16_t* out = nullptr;
+    uint32_t slots = 0, out_slot0 = 0;
+};
+
+}  // namespace impl
+}  // namespace rsmi
+
+struct rsmi_ctx {
+    int k = 0, m = 0, n = 0, device = 0;
+    rsmi::Matrix M;  // n x k
+    std::mutex mu;
+    bool dev_ready = false;
+    int dev_status = RSMI_OK;
+    int num_cu = 256;
+    std::map<std::string, std::shared_ptr<rsmi::impl::Plan>> plans;
+    std::map<void*, int> occupancy;
+    std::vector<rsmi::impl::Staging> staging;  // [0] single-block calls, [0..2] batch pipeline
+    uint8_t* h_stage = nullptr;    // pinned landing area for rebuilt rows (odd S)
+    size_t h_stage_cap = 0;
+    uint32_t* d_crc_tbl = nullptr;  // CRC-16 device tables (crc16.hpp), uploaded on first use
+    uint8_t* d_crc = nullptr;       // raw row CRCs (u32) of host batch calls
+    size_t crc_cap = 0;
+    uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
+    size_t chunks_cap = 0;
+    // options
+    int opt_d = 1;
+    int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
+    long opt_waves_per_cu = 0;
+    int opt_prefetch = 0;
+    int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
+    int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
+    int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
+    long opt_small_bytes = 2L << 20;  // host calls up to this many shard bytes run zero-copy
+    uint8_t* h_small = nullptr;       // page-locked staging of small calls (pageable callers)
+    size_t h_small_cap = 0;
+    long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
+    long opt_coalesce_max = 256;  // blocks per coalesced batch
+    std::string last_kernel;
+    // group commit for rsmi_encode_block_coalesced (see there)
+    struct CoalReq {
+        // encode: block/B in, out = (k+m)*S shards, raw optional; reconstruct: out = n*S
+        // shards in place, present / want flags (group key covers S, pattern, want)
+        const uint8_t* block;
+        size_t B;
+        uint8_t* out;
+        uint32_t* raw;
+        std::string key;
+        int rc;
+        bool done;
+    };
+    std::mutex q_mu;
+    std::condition_variable q_cv;
+    std::vector<CoalReq*> q_pending;
+    bool q_executing = false;
+    uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
+    size_t h_coal_cap = 0;
+    std::atomic<uint64_t> stat_coal_calls{0}, stat_coal_batches{0};
+};
+
+namespace rsmi {
+namespace impl {
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_status(_e);    \
+    } while (0)
+
+int hip_status(hipError_t e);
+int ensure_device(rsmi_ctx* c);
+int make_plan(rsmi_ctx* c, const Matrix& coef, const std::vector<int>& in_rows, const std::vector<int>& out_rows,
+              std::shared_ptr<Plan>& out);
+int encode_plan(rsmi_ctx* c, std::shared_ptr<Plan>& out);
+int decode_rows(const rsmi_ctx* c, const uint8_t* present, Matrix& dec, std::vector<int>& used);
+int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, const uint8_t* want, std::shared_ptr<Plan>& out);
+std::vector<uint8_t> want_mask(const rsmi_ctx* c, const uint8_t* present, int data_only);
+const char* kernel_label(int K, int MT, int D, int NT, bool fast);
+int auto_cache_policy(int K, int MT);
+int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
+                uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
+                const CrcFuse* fuse = nullptr);
+int reserve(uint8_t*& p, size_t& cap, size_t need);
+int count_present(const rsmi_ctx* c, const uint8_t* present, int& np, int& dp);
+int reconstruct_precheck(const rsmi_ctx* c, const uint8_t* present, const uint8_t* want);
+int reconstruct_dev_impl(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride, size_t S,
+                                size_t nblocks, const uint8_t* present, const uint8_t* want, void* stream);
+bool dma_2d_ok(size_t S);
+int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width, size_t rows,
+            hipStream_t stream);
+uint8_t* host_alias(void* p, size_t len);
+uint8_t* small_stage(rsmi_ctx* c, size_t need);
+int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
+                        size_t S, size_t nblocks, uint32_t* raw_out);
+int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out);
+int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                             const uint8_t* present, const uint8_t* want);
+int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                 const uint8_t* present, const uint8_t* want);
+int ensure_crc_tables(rsmi_ctx* c);
+int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
+               uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream, bool zero = true);
+int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                             size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
+uint8_t* coal_stage(rsmi_ctx* c, size_t need);
+void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb);
+void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch);
+int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req);
+
+}  // namespace impl
+}  // namespace rsmi

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic A/B: cache policy (rsmi option "nontemporal" 0/1/2) per output width, over the
-BASELINE shapes, interleaved in one process.  Feeds auto_cache_policy in rsmi_api.cpp."""
+BASELINE shapes, interleaved in one process.  Feeds auto_cache_policy in rsmi_core.cpp."""
 import os
 import statistics
 import sys
