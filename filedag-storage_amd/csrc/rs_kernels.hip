@@ -25,36 +25,10 @@
 #include <cstdint>
 
 #include "crc16.hpp"
+#include "rs_device.hpp"
 #include "rs_plan.hpp"
 
 namespace rsmi {
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));  // any byte alignment
-
-__device__ __forceinline__ uint32_t u4get(const u32x4& v, int i) { return v[i]; }
-
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-// Byte-aligned 16-byte access: the ROCm runtime runs gfx9+ in unaligned access mode, so this
-// is still one global_load/store_dwordx4 (the memory pipeline splits it as needed).
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16u(const uint8_t* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
-    else return *reinterpret_cast<const u32x4u*>(p);
-}
-template <bool NT>
-__device__ __forceinline__ void st16u(uint8_t* p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4u*>(p));
-    else *reinterpret_cast<u32x4u*>(p) = v;
-}
 
 // Default rows in flight per lane for the software pipeline.
 // Narrow outputs (MT <= 2) keep every input row in flight (registers are cheap there,

@@ -36,7 +36,15 @@ struct ExpKernelTable {
     void* fn[2][5];  // v 4 = 64-bit selector shifts (SH64)
 };
 
+// LDS-DMA staged variants (rs_lds_kernels.hip, option lds_dma): [0] RS(10,4) encode and
+// [1] 1-row reconstruct with 4 waves per workgroup, [2]/[3] the same with 2
+struct LdsKernelTable {
+    void* fn[4];
+    int wpg[4];
+};
+
 const FastKernelTable& fast_kernels();
+const LdsKernelTable& lds_kernels();
 const ExpKernelTable& exp_kernels();
 void* generic_kernel();
 void* repitch_kernel();

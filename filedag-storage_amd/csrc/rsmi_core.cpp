@@ -190,16 +190,24 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][c->opt_tables == 1 ? 3 : 4];
             ts_label = c->opt_tables;
         }
+        int wpg = kWG / kWave, lds_label = 0;
+        if (fn && !ua && c->opt_lds >= 1 && c->opt_lds <= 2 && t.K == 10 && D == 1 &&
+            ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
+            const int i = (t.MT == 4 ? 0 : 1) + (c->opt_lds == 2 ? 2 : 0);
+            fn = lds_kernels().fn[i];
+            wpg = lds_kernels().wpg[i];
+            lds_label = wpg;
+        }
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
             const uint64_t tpb = (cpb + uint64_t(kWave * D) - 1) / uint64_t(kWave * D);
             int& occ = c->occupancy[fn];  // queried once per kernel, not per launch
             if (occ <= 0) {
-                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpg * kWave, 0));
                 if (occ <= 0) occ = 1;
             }
             long wg_cap = long(c->num_cu) * occ;
-            if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / (kWG / kWave));
+            if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / wpg);
             // split into launches whose tile count fits 32 bits
             const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / tpb);
             for (uint64_t b0 = 0; b0 < nblocks; b0 += max_blocks) {
@@ -214,14 +222,15 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 uint32_t cslots = fuse ? fuse->slots : 0, cslot0 = fuse ? fuse->out_slot0 : 0;
                 void* args[] = {&pd,    &inb,    &outb,  &in_bs, &in_rs, &out_bs, &out_rs, &S32,
                                 &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0};
-                const uint64_t wgs = std::min<uint64_t>((ntiles + 3) / 4, uint64_t(wg_cap));
-                HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
+                const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));
+                HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
             }
             c->last_kernel = kernel_label(t.K, t.MT, D, NT, true);
             if (ua) c->last_kernel += ",UA";
             if (fuse) c->last_kernel += ",CRC";
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
             if (ts_label) c->last_kernel += ts_label == 1 ? ",TS=1" : ",SH64";
+            if (lds_label) c->last_kernel += ",LDS,WPG=" + std::to_string(lds_label);
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -430,6 +439,11 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "tables")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
+    } else if (!std::strcmp(key, "lds_dma")) {
+        // 1/2 = LDS-DMA staged kernel with 4/2 waves per workgroup (rs_lds_kernels.hip; aligned
+        // RS(10,4) encode and 1-row reconstruct shapes)
+        if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
+        c->opt_lds = int(value);
     } else if (!std::strcmp(key, "small_call_bytes")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_small_bytes = value;

@@ -212,7 +212,9 @@ int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t
 size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
 same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
 (default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
-table fields into SGPRs by scalar loads instead of LDS (A/B)), "coalesce_us" / "coalesce_max"
+table fields into SGPRs by scalar loads instead of LDS (A/B)), "lds_dma" (1|2 = RS(10,4)
+aligned encode and 1-row reconstruct run the LDS-DMA staged kernel with 4|2 waves per
+workgroup (A/B)), "coalesce_us" / "coalesce_max"
 (rsmi_encode_block_coalesced), "small_call_bytes" (host calls moving at most this many shard
 bytes, default 2 MiB, run as one kernel that reads and writes page-locked host memory in
 place over PCIe -- pageable buffers are staged through a page-locked one by CPU copies --
