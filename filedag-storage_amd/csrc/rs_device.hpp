@@ -34,4 +34,31 @@ __device__ __forceinline__ void st16u(uint8_t* p, u32x4 v) {
     else *reinterpret_cast<u32x4u*>(p) = v;
 }
 
+// 16 bytes of a row at byte offset off; bytes at or past S read as zero (CRC passes: zero
+// bytes past the end only move the reference point, which the caller's shift accounts for)
+template <bool ALIGNED>
+__device__ __forceinline__ u32x4 crc_chunk_load(const uint8_t* row, uint64_t off, uint64_t S) {
+    u32x4 v = {0, 0, 0, 0};
+    if (off >= S) return v;
+    if constexpr (ALIGNED) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+        if (off + 16 > S) {
+            const int valid = int(S - off);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int nb = valid - 4 * w;
+                const uint32_t mask = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+                v[w] &= mask;
+            }
+        }
+    } else if (off + 16 <= S) {
+        v = ld16u<true>(row + off);  // byte-aligned 16-byte load (also over PCIe from host memory)
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (off + q < S) v[q >> 2] |= uint32_t(row[off + q]) << (8 * (q & 3));
+    }
+    return v;
+}
+
 }  // namespace rsmi

@@ -432,31 +432,6 @@ __device__ __forceinline__ uint32_t crc_pow(const uint16_t* sP, int i, uint32_t 
     return uint32_t(sP[i * 512 + (s & 0xFF)]) ^ uint32_t(sP[i * 512 + 256 + (s >> 8)]);
 }
 
-template <bool ALIGNED>
-__device__ __forceinline__ u32x4 crc_chunk_load(const uint8_t* row, uint64_t off, uint64_t S) {
-    u32x4 v = {0, 0, 0, 0};
-    if (off >= S) return v;
-    if constexpr (ALIGNED) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-        if (off + 16 > S) {
-            const int valid = int(S - off);
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const int nb = valid - 4 * w;
-                const uint32_t mask = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
-                v[w] &= mask;
-            }
-        }
-    } else if (off + 16 <= S) {
-        v = ld16u<true>(row + off);  // byte-aligned 16-byte load (also over PCIe from host memory)
-    } else {
-#pragma unroll
-        for (int q = 0; q < 16; q++)
-            if (off + q < S) v[q >> 2] |= uint32_t(row[off + q]) << (8 * (q & 3));
-    }
-    return v;
-}
-
 template <bool ALIGNED, int FOLD>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,

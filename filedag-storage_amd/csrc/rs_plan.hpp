@@ -58,7 +58,12 @@ constexpr int kCrcPWords = 15 * 2 * 256 / 2;
 constexpr int kCrcUWords = 16 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
 constexpr int kCrcTableWords = kCrcPWords + kCrcUWords + kCrcNWords;
+// CRC-32 (crc32.hpp) device tables: N[32][16] | PN[32][8][16] | QN[10][8][16], u32 words
+constexpr int kCrc32NWords = 32 * 16;
+constexpr int kCrc32PowWords = 8 * 16;  // one nibble-sliced power
+constexpr int kCrc32TableWords = kCrc32NWords + (32 + 10) * kCrc32PowWords;
 void* crc16_rows_kernel(bool aligned, int fold);
 void* crc16_combine_kernel();
+void* crc32_rows_kernel(bool aligned);
 
 }  // namespace rsmi

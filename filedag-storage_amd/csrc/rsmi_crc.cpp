@@ -1,6 +1,7 @@
 // rsmi_crc.cpp -- the datanode entry checksum (dag/node/datanode/server.go:58-75) on the GPU:
 // the R(row) pass, the encode with the CRC fused in, and the host-side header fold
-// (crc16.hpp has the algebra; rsmi_impl.hpp the file map).
+// (crc16.hpp has the algebra; rsmi_impl.hpp the file map); and the mutcask value checksum
+// (CRC-32 IEEE, kv/mutcask/cask.go:73-97; crc32.hpp) as an R(row) pass.
 #include "rsmi_impl.hpp"
 
 using namespace rsmi;
@@ -44,6 +45,45 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     }
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
     const uint32_t* tb = c->d_crc_tbl;
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
+    HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
+    return RSMI_OK;
+}
+
+// CRC-32 device tables (crc32.hpp), uploaded once per context (caller holds ctx->mu)
+int ensure_crc32_tables(rsmi_ctx* c) {
+    if (c->d_crc32_tbl) return RSMI_OK;
+    const Crc32Tables& t = crc32_tables();
+    static_assert(sizeof(t.N) + sizeof(t.PN) + sizeof(t.QN) == size_t(kCrc32TableWords) * 4, "CRC-32 table layout");
+    std::vector<uint32_t> h(static_cast<size_t>(kCrc32TableWords));
+    std::memcpy(h.data(), t.N, sizeof(t.N));
+    std::memcpy(h.data() + kCrc32NWords, t.PN, sizeof(t.PN));
+    std::memcpy(h.data() + kCrc32NWords + sizeof(t.PN) / 4, t.QN, sizeof(t.QN));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc32_tbl), h.size() * 4));
+    HIP_TRY(hipMemcpy(c->d_crc32_tbl, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    return RSMI_OK;
+}
+
+// CRC-32 R(row) of nrows rows per block, XORed into out[b*out_bs + r] (the caller zeroes
+// it), stream-ordered.  Rows may lie in device or page-locked host memory.
+int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
+                 uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream) {
+    if (!nblocks || !nrows || S == 0) return RSMI_OK;  // R(empty) = 0
+    int rc = ensure_crc32_tables(c);
+    if (rc) return rc;
+    const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
+    void* fn = crc32_rows_kernel(aligned);
+    const uint64_t tile = uint64_t(kWave) * 16;
+    uint32_t tpb = uint32_t((S + tile - 1) / tile);
+    uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
+    uint64_t nitems = nblocks * nrows * nseg;
+    int& occ = c->occupancy[fn];
+    if (occ <= 0) {
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
+        if (occ <= 0) occ = 1;
+    }
+    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
+    const uint32_t* tb = c->d_crc32_tbl;
     void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
     return RSMI_OK;
@@ -124,7 +164,31 @@ int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     return hip_status(hipGetLastError());
 }
 
+int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) {
+    if (!c || !d_rows || !d_raw_out || nrows < 0 || out_block_stride < size_t(nrows)) return RSMI_ERR_INVALID_ARG;
+    if (nrows > 1 && shard_stride < S) return RSMI_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (nblocks && nrows)
+        HIP_TRY(hipMemset2DAsync(d_raw_out, out_block_stride * 4, 0, size_t(nrows) * 4, nblocks, st));
+    rc = launch_crc32(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
+                      st);
+    if (rc) return rc;
+    c->last_kernel = "rs_crc32_rows_kernel";
+    return hip_status(hipGetLastError());
+}
+
 uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
+
+uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n) { return crc32_checksum(p, n); }
+
+uint32_t rsmi_crc32_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
+    return crc32_entry(head, head_len, raw, data_len);
+}
 
 uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
     return crc16_entry(head, head_len, raw, data_len);

@@ -77,19 +77,19 @@ uint8_t* small_stage(rsmi_ctx* c, size_t need) {
 }
 
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
-                        size_t S, size_t nblocks, uint32_t* raw_out) {
+                        size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     hipStream_t st = c->staging[0].stream;
     const uint8_t* in = host_alias(const_cast<uint8_t*>(data), (nblocks - 1) * dbs + k * S);
     uint8_t* out = host_alias(parity, (nblocks - 1) * pbs + m * S);
     size_t in_bs = dbs, out_bs = pbs;
-    // page-locked staging, only the parts needed: [data rows | parity rows | raw CRCs]
+    // page-locked staging, only the parts needed: [data rows | parity rows | raw CRCs | CRC-32s]
     const bool stage_in = in == nullptr, stage_out = out == nullptr;
     const size_t in_sz = stage_in ? nblocks * k * S : 0, out_sz = stage_out ? nblocks * m * S : 0;
-    const size_t raw_sz = raw_out ? nblocks * n * 4 : 0;
+    const size_t raw_sz = raw_out ? nblocks * n * 4 : 0, raw32_sz = raw32_out ? nblocks * n * 4 : 0;
     uint8_t* hs = nullptr;
-    if (in_sz + out_sz + raw_sz) {
-        hs = small_stage(c, in_sz + out_sz + raw_sz);
+    if (in_sz + out_sz + raw_sz + raw32_sz) {
+        hs = small_stage(c, in_sz + out_sz + raw_sz + raw32_sz);
         if (!hs) return RSMI_ERR_DEVICE;
     }
     if (stage_in) {
@@ -103,6 +103,7 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
         out_bs = m * S;
     }
     uint32_t* hraw = raw_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz) : nullptr;
+    uint32_t* hraw32 = raw32_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz + raw_sz) : nullptr;
     if (!in || !out) return RSMI_ERR_DEVICE;
     int rc;
     if (raw_out && S >= 16 && k <= 16) {
@@ -125,15 +126,26 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
                 return rc;
         }
     }
+    if (raw32_out) {  // CRC-32 R(row): a second read of the rows where they lie
+        if ((rc = reserve(c->d_crc32, c->crc32_cap, raw32_sz))) return rc;
+        uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc32);
+        HIP_TRY(hipMemsetAsync(cr, 0, raw32_sz, st));
+        if ((rc = launch_crc32(c, in, S, in_bs, uint32_t(k), S, nblocks, cr, n, st))) return rc;
+        if ((rc = launch_crc32(c, out, S, out_bs, uint32_t(m), S, nblocks, cr + k, n, st))) return rc;
+        uint8_t* d32 = host_alias(reinterpret_cast<uint8_t*>(hraw32), raw32_sz);
+        if (!d32) return RSMI_ERR_DEVICE;
+        if ((rc = repitch(d32, raw32_sz, reinterpret_cast<uint8_t*>(cr), raw32_sz, raw32_sz, 1, st))) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(st));
     if (stage_out)
         for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
     if (raw_out) std::memcpy(raw_out, hraw, raw_sz);
+    if (raw32_out) std::memcpy(raw32_out, hraw32, raw32_sz);
     return RSMI_OK;
 }
 
 int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
+                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (data_block_stride < size_t(c->k) * S || parity_block_stride < size_t(c->m) * S) return RSMI_ERR_INVALID_ARG;
@@ -156,7 +168,8 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
     const bool pinned = in_pinned && host_alias(parity, (nblocks - 1) * parity_block_stride + m * S);
     if ((c->opt_zero_copy && pinned) ||
         (total <= size_t(c->opt_small_bytes) && (2 * total <= size_t(c->opt_small_bytes) || in_pinned)))
-        return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+        return encode_small(c, *plan, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out,
+                            raw32_out);
     const size_t Sp = rsmi_recommended_pitch(S);
     const size_t in_bs = k * Sp, out_bs = m * Sp;
     const bool d2 = dma_2d_ok(S);
@@ -172,6 +185,7 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
                              : nullptr;
     const size_t n = k + m;
     if (raw_out && (rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
+    if (raw32_out && (rc = reserve(c->d_crc32, c->crc32_cap, nblocks * n * 4))) return rc;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
@@ -209,6 +223,12 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
             if ((rc = launch_crc(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream, false)))
                 return rc;
         }
+        if (raw32_out) {
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc32) + b0 * n;
+            HIP_TRY(hipMemsetAsync(cr, 0, nb * n * 4, st.stream));
+            if ((rc = launch_crc32(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream))) return rc;
+            if ((rc = launch_crc32(c, st.d_out, Sp, out_bs, uint32_t(m), S, nb, cr + k, n, st.stream))) return rc;
+        }
         // device -> host
         if (zc && parity_block_stride == m * S) {
             if ((rc = repitch(zc + b0 * m * S, S, st.d_out, Sp, S, nb * m, st.stream))) return rc;
@@ -236,6 +256,7 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
     if (raw_out) HIP_TRY(hipMemcpy(raw_out, c->d_crc, nblocks * n * 4, hipMemcpyDeviceToHost));
+    if (raw32_out) HIP_TRY(hipMemcpy(raw32_out, c->d_crc32, nblocks * n * 4, hipMemcpyDeviceToHost));
     return RSMI_OK;
 }
 
@@ -414,6 +435,13 @@ int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_blo
                                size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
     if (!raw_out) return RSMI_ERR_INVALID_ARG;
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+}
+
+int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                                size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
+                                uint32_t* raw32_out) {
+    return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw16_out,
+                            raw32_out);
 }
 
 int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out) {

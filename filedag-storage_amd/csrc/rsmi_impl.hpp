@@ -23,6 +23,7 @@
 
 #include "../../include/rsmi.h"
 #include "crc16.hpp"
+#include "crc32.hpp"
 #include "gf256.hpp"
 #include "rs_plan.hpp"
 
@@ -84,6 +85,9 @@ struct rsmi_ctx {
     uint32_t* d_crc_tbl = nullptr;  // CRC-16 device tables (crc16.hpp), uploaded on first use
     uint8_t* d_crc = nullptr;       // raw row CRCs (u32) of host batch calls
     size_t crc_cap = 0;
+    uint32_t* d_crc32_tbl = nullptr;  // CRC-32 device tables (crc32.hpp), uploaded on first use
+    uint8_t* d_crc32 = nullptr;       // raw row CRC-32s of host batch calls
+    size_t crc32_cap = 0;
     uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
     size_t chunks_cap = 0;
     // options
@@ -155,14 +159,17 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
 uint8_t* host_alias(void* p, size_t len);
 uint8_t* small_stage(rsmi_ctx* c, size_t need);
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
-                        size_t S, size_t nblocks, uint32_t* raw_out);
+                        size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out = nullptr);
 int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out);
+                            size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out = nullptr);
 int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
                              const uint8_t* present, const uint8_t* want);
 int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                  const uint8_t* present, const uint8_t* want);
 int ensure_crc_tables(rsmi_ctx* c);
+int ensure_crc32_tables(rsmi_ctx* c);
+int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
+                 uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream);
 int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
                uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream, bool zero = true);
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,

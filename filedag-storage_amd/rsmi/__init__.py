@@ -91,6 +91,12 @@ def lib() -> ctypes.CDLL:
         "rsmi_encode_block_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
         "rsmi_encode_batch_dev_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size,
                                                      c_size, ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_crc32_ieee": (ctypes.c_uint32, [u8p, c_size]),
+        "rsmi_crc32_entry": (ctypes.c_uint32, [u8p, c_size, ctypes.c_uint32, c_size]),
+        "rsmi_crc32_rows_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, ctypes.c_int, c_size, c_size,
+                                               ctypes.c_void_p, c_size, ctypes.c_void_p]),
+        "rsmi_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
+                                                       ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
@@ -253,6 +259,17 @@ class Codec:
         _check(lib().rsmi_crc16_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
                                          stream or None))
 
+    def crc32_rows_dev(self, d_rows: int, rs: int, bs: int, nrows: int, S: int, nblocks: int, d_out: int,
+                       out_bs: int, stream: int = 0) -> None:
+        """R32(row) of the mutcask value checksum (CRC-32 IEEE, raw) for every row, on the device."""
+        _check(lib().rsmi_crc32_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
+                                         stream or None))
+
+    def encode_batch_host_crcs_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
+                                   nblocks: int, raw16_ptr: Optional[int], raw32_ptr: Optional[int]) -> None:
+        _check(lib().rsmi_encode_batch_host_crcs(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
+                                                 raw16_ptr or None, raw32_ptr or None))
+
     # -- device memory (raw pointers, e.g. torch tensor.data_ptr()); stream = hipStream_t
     def encode_batch_dev(self, d_data: int, data_rs: int, data_bs: int, d_parity: int, parity_rs: int,
                          parity_bs: int, S: int, nblocks: int, stream: int = 0) -> None:
@@ -366,6 +383,18 @@ def crc16_entry(head: bytes, raw: int, data_len: int) -> int:
     """Checksum(head || D) from R(D) = raw and |D| (include/rsmi.h rsmi_crc16_entry)."""
     h = bytearray(head)
     return lib().rsmi_crc16_entry(ctypes.addressof(_buf(h)) if h else None, len(h), raw, data_len)
+
+
+def crc32_ieee(data: bytes) -> int:
+    """Go crc32.ChecksumIEEE(data) (the mutcask value checksum, kv/mutcask/cask.go:75), host side."""
+    b = bytearray(data)
+    return lib().rsmi_crc32_ieee(ctypes.addressof(_buf(b)) if b else None, len(b))
+
+
+def crc32_entry(head: bytes, raw: int, data_len: int) -> int:
+    """ChecksumIEEE(head || D) from R32(D) = raw and |D| (include/rsmi.h rsmi_crc32_entry)."""
+    h = bytearray(head)
+    return lib().rsmi_crc32_entry(ctypes.addressof(_buf(h)) if h else None, len(h), raw, data_len)
 
 
 def recommended_pitch(S: int) -> int:

@@ -202,6 +202,37 @@ int rsmi_encode_batch_dev_crc(rsmi_ctx* ctx, const uint8_t* d_data, size_t data_
 /* rsmi_encode_block plus raw_out[r] = R(shard r), r < k+m. */
 int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out);
 
+/* ------------------------------------------------------------------ mutcask CRC-32 */
+
+/* The mutcask KV engine under a datanode (kv/mutcask/cask.go:73-97, selected by
+ * server.go:207) stores every value as |crc32 (4 LE)|value| with crc32 = Go
+ * crc32.ChecksumIEEE(value) (the zlib CRC-32), and re-checks it on every read (cask.go:250).
+ * The value is the datanode's whole entry, so the shard bytes get a second byte-serial pass
+ * on every Put and Get.  "Raw" R32(D) = the CRC-32 register after D from a zero register,
+ * no complement (reflected polynomial 0xEDB88320). */
+
+/* crc32.ChecksumIEEE(p) on the host. */
+uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n);
+
+/* ChecksumIEEE(head || D) from R32(D) and |D|: with head = the datanode entry's first 12 + meta
+ * bytes (|crc16 (4 LE)|meta size|data size|meta|) this is the mutcask value checksum of a
+ * shard D's entry.  head may be empty. */
+uint32_t rsmi_crc32_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len);
+
+/* R32(row) for nrows rows of S bytes per block on the device, laid out as in
+ * rsmi_crc16_rows_dev (d_raw_out[b*out_block_stride + r], zeroed first).  Stream-ordered. */
+int rsmi_crc32_rows_dev(rsmi_ctx* ctx, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream);
+
+/* rsmi_encode_batch_host with either or both raw checksums of every shard it touched:
+ * raw16_out[b*(k+m) + r] = R(shard) (CRC-16, as rsmi_encode_batch_host_crc) and
+ * raw32_out[b*(k+m) + r] = R32(shard) (CRC-32), each optional (NULL).  The CRC-32 pass reads
+ * the rows where the encode left them (device staging, or page-locked host memory on the
+ * zero-copy path).  DagNode.PutMany hands both to mutcask-backed datanodes. */
+int rsmi_encode_batch_host_crcs(rsmi_ctx* ctx, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+                                size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
+                                uint32_t* raw32_out);
+
 /* ------------------------------------------------------------------ tuning / introspection */
 
 /* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache

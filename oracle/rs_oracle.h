@@ -39,6 +39,12 @@ int rs_oracle_selftest(void);
 uint16_t rs_oracle_crc16_ibm(const uint8_t* p, size_t n);
 uint32_t rs_oracle_datanode_entry_crc(const uint8_t* meta, size_t meta_len, const uint8_t* data, size_t data_len);
 
+/* mutcask value checksum (crc32_oracle.c): Go crc32.ChecksumIEEE(p), and the checksum
+ * kv/mutcask/cask.go:73-79 stores for a datanode entry (entry_crc16 = its server.go:70 sum) */
+uint32_t rs_oracle_crc32_ieee(const uint8_t* p, size_t n);
+uint32_t rs_oracle_mutcask_entry_crc(uint32_t entry_crc16, const uint8_t* meta, size_t meta_len, const uint8_t* data,
+                                     size_t data_len);
+
 /* fast multi-threaded CPU path (rs_cpu_fast.c): same results, used only as bench.py's
  * cpu_baseline and cross-checked against the scalar path in tests */
 int rs_cpu_encode_batch(int k, int m, const uint8_t* data, size_t data_block_stride,

@@ -40,6 +40,10 @@ def lib():
         L.rs_oracle_crc16_ibm.argtypes = [vp, sz]
         L.rs_oracle_datanode_entry_crc.restype = ctypes.c_uint32
         L.rs_oracle_datanode_entry_crc.argtypes = [vp, sz, vp, sz]
+        L.rs_oracle_crc32_ieee.restype = ctypes.c_uint32
+        L.rs_oracle_crc32_ieee.argtypes = [vp, sz]
+        L.rs_oracle_mutcask_entry_crc.restype = ctypes.c_uint32
+        L.rs_oracle_mutcask_entry_crc.argtypes = [ctypes.c_uint32, vp, sz, vp, sz]
         _L = L
     return _L
 
@@ -116,6 +120,20 @@ def datanode_entry_crc(meta, data) -> int:
     d = np.frombuffer(bytes(data), dtype=np.uint8).copy()
     return int(lib().rs_oracle_datanode_entry_crc(ptr(m) if m.size else None, m.size,
                                                   ptr(d) if d.size else None, d.size))
+
+
+def crc32_ieee(data) -> int:
+    """Go crc32.ChecksumIEEE(data) via the bit-serial oracle (crc32_oracle.c)."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return int(lib().rs_oracle_crc32_ieee(ptr(a) if a.size else None, a.size))
+
+
+def mutcask_entry_crc(entry_crc16: int, meta, data) -> int:
+    """The value checksum kv/mutcask/cask.go:73-79 stores for a datanode entry (meta, data)."""
+    m = np.frombuffer(bytes(meta), dtype=np.uint8).copy()
+    d = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+    return int(lib().rs_oracle_mutcask_entry_crc(entry_crc16, ptr(m) if m.size else None, m.size,
+                                                 ptr(d) if d.size else None, d.size))
 
 
 def entry_head(meta, data_len: int) -> bytes:

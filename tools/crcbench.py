@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: rs_crc16_rows_kernel bandwidth (R(row) of every shard row, the datanode entry
-checksum's device half) over the bench layout: 4096 RS(10,4) 256 KiB blocks, 14 rows of
+"""Diagnostic: rs_crc16_rows_kernel / rs_crc32_rows_kernel bandwidth (R(row) of every shard row,
+the datanode entry checksum's and the mutcask value checksum's device halves) over the bench layout: 4096 RS(10,4) 256 KiB blocks, 14 rows of
 S = 26215 at 32 KiB pitch; and 1 MiB / 4 MiB shapes.  Bytes counted: rows x S read."""
 import os
 import statistics
@@ -22,10 +22,13 @@ def main():
         p = rsmi.recommended_pitch(S)
         buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
         out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
-        for fold in (1, 0):
+        for fold in (1, 0, "crc32"):
             c = rsmi.Codec(k, m)
-            c.set_option("crc_fold", fold)
-            f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
+            if fold == "crc32":
+                f = lambda: c.crc32_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
+            else:
+                c.set_option("crc_fold", fold)
+                f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             t_end = time.perf_counter() + 0.2
             while time.perf_counter() < t_end:
                 f()
@@ -39,7 +42,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
-            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} fold={'nibble' if fold else 'byte'}: "
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 fold=' + ('nibble' if fold else 'byte')}: "
                   f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
             c.close()
 
