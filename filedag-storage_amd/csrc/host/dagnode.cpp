@@ -181,6 +181,18 @@ uint16_t DagNode::entry_checksum(const Bytes& meta, size_t S, uint32_t raw) {
     return rsmi_crc16_entry(head.data(), head.size(), raw, S);
 }
 
+uint32_t DagNode::value_checksum(const Bytes& meta, size_t S, uint16_t crc16, uint32_t raw32) {
+    // the whole entry |crc16 (4 LE)|meta size|data size|meta| precedes the shard in the value
+    Bytes head(12 + meta.size());
+    for (int i = 0; i < 4; i++) {
+        head[i] = uint8_t(uint32_t(crc16) >> (8 * i));
+        head[4 + i] = uint8_t(uint32_t(meta.size()) >> (8 * i));
+        head[8 + i] = uint8_t(uint32_t(S) >> (8 * i));
+    }
+    std::copy(meta.begin(), meta.end(), head.begin() + 12);
+    return rsmi_crc32_entry(head.data(), head.size(), raw32, S);
+}
+
 Status DagNode::get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online) {
     const size_t n = nodes_.size();
     std::vector<Meta> metas(n);
@@ -276,7 +288,10 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         const size_t chunk = staging_blocks(size_t(n) * S);
         const Bytes meta = encode_meta(int32_t(B));
         const int wq = EntryQuorum().second;
-        std::vector<uint32_t> raw;
+        // datanodes over mutcask keep a CRC-32 of every value: the GPU pass supplies it too
+        bool want32 = false;
+        for (auto& sn : nodes_) want32 |= sn.client->WantsValueChecksum();
+        std::vector<uint32_t> raw, raw32;
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
             const size_t* idx = g.second.data() + c0;
@@ -292,8 +307,9 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             }
             if (gpu_checksums_) {
                 raw.resize(nb * size_t(n));
-                rc = rsmi_encode_batch_host_crc(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb,
-                                                raw.data());
+                raw32.resize(want32 ? nb * size_t(n) : 0);
+                rc = rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb,
+                                                 raw.data(), want32 ? raw32.data() : nullptr);
             } else {
                 rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
             }
@@ -306,9 +322,16 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 std::vector<Status> res(static_cast<size_t>(n));
                 fan(n, [&](int i) {
                     Bytes shard(base + size_t(i) * S, base + size_t(i + 1) * S);
-                    res[i] = gpu_checksums_ ? nodes_[i].client->PutWithChecksum(keys[idx[j]], meta, shard,
-                                                                                entry_checksum(meta, S, raw[j * n + i]))
-                                            : nodes_[i].client->Put(keys[idx[j]], meta, shard);
+                    DataNodeClient& cl = *nodes_[i].client;
+                    if (!gpu_checksums_) {
+                        res[i] = cl.Put(keys[idx[j]], meta, shard);
+                        return;
+                    }
+                    const uint16_t c16 = entry_checksum(meta, S, raw[j * n + i]);
+                    res[i] = want32 && cl.WantsValueChecksum()
+                                 ? cl.PutWithChecksums(keys[idx[j]], meta, shard, c16,
+                                                       value_checksum(meta, S, c16, raw32[j * n + i]))
+                                 : cl.PutWithChecksum(keys[idx[j]], meta, shard, c16);
                 }, S);
                 QuorumWait w(wq, n - wq + 1);
                 for (const Status& r : res) w.add(r);

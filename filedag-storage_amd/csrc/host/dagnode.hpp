@@ -133,6 +133,9 @@ private:
     static Bytes encode_meta(int32_t size);
     // server.go:70's checksum of the entry (meta, S-byte shard) from the shard's R(shard)
     static uint16_t entry_checksum(const Bytes& meta, size_t S, uint32_t raw);
+    // the mutcask value checksum (cask.go:73-79) of the entry holding a shard with entry
+    // checksum crc16 and CRC-32 R32(shard) = raw32
+    static uint32_t value_checksum(const Bytes& meta, size_t S, uint16_t crc16, uint32_t raw32);
 
     DagNodeConfig config_;
     std::vector<StorageNode> nodes_;

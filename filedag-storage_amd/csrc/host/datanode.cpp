@@ -1,4 +1,5 @@
-// datanode.cpp -- entry framing + CRC-16 shard store (see datanode.hpp).
+// datanode.cpp -- entry framing + CRC-16 shard store, with the mutcask engine's CRC-32 value
+// framing (see datanode.hpp).
 #include "datanode.hpp"
 
 #include <array>
@@ -25,6 +26,20 @@ struct IbmTables {
     }
 };
 
+// Slice-by-8 tables for the reflected polynomial 0xEDB88320 (Go crc32 IEEE / zlib)
+struct IeeeTables {
+    uint32_t t[8][256];
+    IeeeTables() {
+        for (int i = 0; i < 256; i++) {
+            uint32_t c = uint32_t(i);
+            for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+            t[0][i] = c;
+        }
+        for (int s = 1; s < 8; s++)
+            for (int i = 0; i < 256; i++) t[s][i] = t[0][t[s - 1][i] & 0xFF] ^ (t[s - 1][i] >> 8);
+    }
+};
+
 void put_le32(uint8_t* p, uint32_t v) {
     for (int i = 0; i < 4; i++) p[i] = uint8_t(v >> (8 * i));
 }
@@ -34,15 +49,15 @@ uint32_t get_le32(const uint8_t* p) {
 
 Status not_found() { return Status::Error("Key not found"); }
 
-// parse + crc check shared by Get and GetMeta (server.go:83-124)
-Status unpack(const Bytes& e, Bytes* meta, Bytes* data) {
-    if (e.size() < size_t(kHeaderSize)) return Status::Error("unexpected EOF");
-    const uint32_t crc = get_le32(e.data());
-    const uint32_t msz = get_le32(e.data() + 4), dsz = get_le32(e.data() + 8);
-    if (crc != crc16_ibm(e.data() + 4, e.size() - 4)) return Status::Error("checking crc failed");
-    if (size_t(kHeaderSize) + msz + dsz > e.size()) return Status::Error("unexpected EOF");
-    if (meta) meta->assign(e.begin() + kHeaderSize, e.begin() + kHeaderSize + msz);
-    if (data) data->assign(e.begin() + kHeaderSize + msz, e.begin() + kHeaderSize + msz + dsz);
+// parse + crc check shared by Get and GetMeta (server.go:83-124), over an entry of n bytes
+Status unpack(const uint8_t* e, size_t n, Bytes* meta, Bytes* data) {
+    if (n < size_t(kHeaderSize)) return Status::Error("unexpected EOF");
+    const uint32_t crc = get_le32(e);
+    const uint32_t msz = get_le32(e + 4), dsz = get_le32(e + 8);
+    if (crc != crc16_ibm(e + 4, n - 4)) return Status::Error("checking crc failed");
+    if (size_t(kHeaderSize) + msz + dsz > n) return Status::Error("unexpected EOF");
+    if (meta) meta->assign(e + kHeaderSize, e + kHeaderSize + msz);
+    if (data) data->assign(e + kHeaderSize + msz, e + kHeaderSize + msz + dsz);
     return Status::Ok();
 }
 
@@ -62,39 +77,78 @@ uint16_t crc16_ibm(const uint8_t* p, size_t n, uint16_t crc) {
     return uint16_t(~crc);
 }
 
-Status DataNodeServer::store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc) {
+uint32_t crc32_ieee(const uint8_t* p, size_t n) {
+    static const IeeeTables T;
+    const auto& t = T.t;
+    uint32_t crc = ~0u;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint32_t lo = crc ^ get_le32(p + i);
+        crc = t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^ t[3][p[i + 4]] ^
+              t[2][p[i + 5]] ^ t[1][p[i + 6]] ^ t[0][p[i + 7]];
+    }
+    for (; i < n; i++) crc = t[0][(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+    return ~crc;
+}
+
+Status DataNodeServer::store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc,
+                             const uint32_t* value_crc) {
     if (key.empty()) return Status::Error("Key cannot be empty");  // badger, server_test.go:14-22
-    Bytes e(size_t(kHeaderSize) + meta.size() + data.size());
-    put_le32(e.data() + 4, uint32_t(meta.size()));
-    put_le32(e.data() + 8, uint32_t(data.size()));
-    if (!meta.empty()) std::memcpy(e.data() + kHeaderSize, meta.data(), meta.size());
-    if (!data.empty()) std::memcpy(e.data() + kHeaderSize + meta.size(), data.data(), data.size());
-    put_le32(e.data(), crc ? *crc : crc16_ibm(e.data() + 4, e.size() - 4));  // server.go:70-75
+    const size_t pre = prefix();  // mutcask: | crc32 (4 LE) | entry |  (cask.go:73-79)
+    Bytes v(pre + size_t(kHeaderSize) + meta.size() + data.size());
+    uint8_t* e = v.data() + pre;
+    put_le32(e + 4, uint32_t(meta.size()));
+    put_le32(e + 8, uint32_t(data.size()));
+    if (!meta.empty()) std::memcpy(e + kHeaderSize, meta.data(), meta.size());
+    if (!data.empty()) std::memcpy(e + kHeaderSize + meta.size(), data.data(), data.size());
+    put_le32(e, crc ? *crc : crc16_ibm(e + 4, v.size() - pre - 4));  // server.go:70-75
+    if (pre) put_le32(v.data(), value_crc ? *value_crc : crc32_ieee(e, v.size() - pre));
     std::lock_guard<std::mutex> g(mu_);
-    kv_[key] = std::move(e);
+    kv_[key] = std::move(v);
+    return Status::Ok();
+}
+
+// the KV engine's read: mutcask re-checks its value checksum on every read (cask.go:250)
+Status DataNodeServer::read_entry(const std::string& key, const Bytes** entry) {
+    auto it = kv_.find(key);
+    if (it == kv_.end()) return not_found();
+    const Bytes& v = it->second;
+    if (engine_ == KvEngine::Mutcask) {
+        if (v.size() <= 4) return Status::Error("mutcask: invalid value format");
+        if (get_le32(v.data()) != crc32_ieee(v.data() + 4, v.size() - 4))
+            return Status::Error("mutcask: data may be rotted");
+    }
+    *entry = &v;
     return Status::Ok();
 }
 
 Status DataNodeServer::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
-    return store(key, meta, data, nullptr);
+    return store(key, meta, data, nullptr, nullptr);
 }
 
 Status DataNodeServer::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
-    return store(key, meta, data, &crc);
+    return store(key, meta, data, &crc, nullptr);
+}
+
+Status DataNodeServer::PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+                                        uint32_t value_crc) {
+    return store(key, meta, data, &crc, &value_crc);
 }
 
 Status DataNodeServer::Get(const std::string& key, Bytes* meta, Bytes* data) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = kv_.find(key);
-    if (it == kv_.end()) return not_found();
-    return unpack(it->second, meta, data);
+    const Bytes* v = nullptr;
+    Status s = read_entry(key, &v);
+    if (!s.ok()) return s;
+    return unpack(v->data() + prefix(), v->size() - prefix(), meta, data);
 }
 
 Status DataNodeServer::GetMeta(const std::string& key, Bytes* meta) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = kv_.find(key);
-    if (it == kv_.end()) return not_found();
-    return unpack(it->second, meta, nullptr);
+    const Bytes* v = nullptr;
+    Status s = read_entry(key, &v);
+    if (!s.ok()) return s;
+    return unpack(v->data() + prefix(), v->size() - prefix(), meta, nullptr);
 }
 
 Status DataNodeServer::Delete(const std::string& key) {
@@ -107,7 +161,8 @@ Status DataNodeServer::Size(const std::string& key, int64_t* size) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
     if (it == kv_.end()) return not_found();
-    *size = int64_t(it->second.size());  // HeaderSize + meta + data (server_test.go:147-152)
+    *size = int64_t(it->second.size() - prefix());  // HeaderSize + meta + data (server_test.go:147-152;
+                                                      // mutcask Size = VSize - 4, cask.go:235)
     return Status::Ok();
 }
 
@@ -122,14 +177,22 @@ bool DataNodeServer::RawEntry(const std::string& key, Bytes* entry) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
     if (it == kv_.end()) return false;
-    *entry = it->second;
+    entry->assign(it->second.begin() + long(prefix()), it->second.end());
+    return true;
+}
+
+bool DataNodeServer::RawValue(const std::string& key, Bytes* value) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = kv_.find(key);
+    if (it == kv_.end()) return false;
+    *value = it->second;
     return true;
 }
 
 void DataNodeServer::CorruptByte(const std::string& key, size_t offset) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
-    if (it != kv_.end() && offset < it->second.size()) it->second[offset] ^= 0x5A;
+    if (it != kv_.end() && prefix() + offset < it->second.size()) it->second[prefix() + offset] ^= 0x5A;
 }
 
 void DataNodeServer::Wipe() {
@@ -144,6 +207,10 @@ Status InProcDataNode::Put(const std::string& key, const Bytes& meta, const Byte
 }
 Status InProcDataNode::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
     return offline_ ? down() : server_.PutWithChecksum(key, meta, data, crc);
+}
+Status InProcDataNode::PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+                                        uint32_t value_crc) {
+    return offline_ ? down() : server_.PutWithChecksums(key, meta, data, crc, value_crc);
 }
 Status InProcDataNode::Get(const std::string& key, Bytes* meta, Bytes* data) {
     return offline_ ? down() : server_.Get(key, meta, data);

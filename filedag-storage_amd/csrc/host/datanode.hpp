@@ -4,8 +4,11 @@
 //   | crc (4 B LE) | meta size (4 B LE) | data size (4 B LE) | meta | data |     (server.go:40-41)
 // whose crc is CRC-16 "IBM" over every byte after the crc field (server.go:70), checked on
 // Get/GetMeta (server.go:93-97, :115-119).  The KV engine below it (badger / mutcask,
-// server.go:183-238) is out of scope; an in-memory map stands in, with badger's rule
-// that keys must be non-empty.  DataNodeClient mirrors proto.DataNodeClient
+// server.go:183-238) is out of scope as storage; an in-memory map stands in, with badger's
+// rule that keys must be non-empty.  Its checksum is not: with the mutcask engine
+// (server.go:207) every value is stored as | crc32 (4 B LE) | entry | (kv/mutcask/cask.go:73-79,
+// Go crc32.ChecksumIEEE) and re-checked on every read (cask.go:81-97, :250), a second
+// byte-serial pass over each shard that a sender can precompute (PutWithChecksums).  DataNodeClient mirrors proto.DataNodeClient
 // (dag/proto/datanode.proto:9-17) so the DagNode talks to any implementation, and an
 // in-process client can be switched offline to exercise the quorum paths.
 #pragma once
@@ -33,6 +36,11 @@ struct Status {
 // polynomial 0xA001, register complemented on entry and exit (CRC-16/USB; check value
 // 0xB4C8).  The upstream source is absent, so this variant is parity-unpinned.
 uint16_t crc16_ibm(const uint8_t* p, size_t n, uint16_t crc = 0);
+// Go crc32.ChecksumIEEE (the zlib CRC-32), slice-by-8
+uint32_t crc32_ieee(const uint8_t* p, size_t n);
+
+// server.go:29-35 KVType: the engine under the datanode
+enum class KvEngine { Badger, Mutcask };
 
 constexpr int kHeaderSize = 12;  // server.go:37
 
@@ -47,6 +55,14 @@ public:
         (void)crc;
         return Put(key, meta, data);
     }
+    // ... and with the mutcask value checksum of that entry as well (cask.go:73-79), for a
+    // datanode whose engine keeps one (WantsValueChecksum); others drop it
+    virtual Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+                                    uint32_t value_crc) {
+        (void)value_crc;
+        return PutWithChecksum(key, meta, data, crc);
+    }
+    virtual bool WantsValueChecksum() const { return false; }
     virtual Status Get(const std::string& key, Bytes* meta, Bytes* data) = 0;
     virtual Status GetMeta(const std::string& key, Bytes* meta) = 0;
     virtual Status Delete(const std::string& key) = 0;
@@ -59,22 +75,33 @@ public:
 // server.go's `server` over an in-memory KV.
 class DataNodeServer {
 public:
+    explicit DataNodeServer(KvEngine engine = KvEngine::Badger) : engine_(engine) {}
+    KvEngine engine() const { return engine_; }
     Status Put(const std::string& key, const Bytes& meta, const Bytes& data);
     // the same entry, with the sender's checksum in place of the server.go:70 CRC pass; Get
     // and GetMeta still verify it, so a wrong sender checksum fails the read like corruption
     Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc);
+    // mutcask: the value checksum too (a wrong one fails later reads with "data may be rotted")
+    Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+                            uint32_t value_crc);
     Status Get(const std::string& key, Bytes* meta, Bytes* data);
     Status GetMeta(const std::string& key, Bytes* meta);
     Status Delete(const std::string& key);
     Status Size(const std::string& key, int64_t* size);
     Status AllKeys(std::vector<std::string>* keys);
-    // test hooks
+    // test hooks: the datanode entry, the KV engine's stored value (mutcask: crc32 + entry),
+    // and a flipped byte at an entry offset
     bool RawEntry(const std::string& key, Bytes* entry);
+    bool RawValue(const std::string& key, Bytes* value);
     void CorruptByte(const std::string& key, size_t offset);
     void Wipe();
 
 private:
-    Status store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc);
+    Status store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc,
+                 const uint32_t* value_crc);
+    Status read_entry(const std::string& key, const Bytes** entry);  // caller holds mu_
+    size_t prefix() const { return engine_ == KvEngine::Mutcask ? 4 : 0; }
+    KvEngine engine_;
     std::mutex mu_;
     std::map<std::string, Bytes> kv_;
 };
@@ -82,9 +109,13 @@ private:
 // An in-process client; Offline(true) makes every call fail like a dead gRPC peer.
 class InProcDataNode : public DataNodeClient {
 public:
-    explicit InProcDataNode(std::string addr) : addr_(std::move(addr)) {}
+    explicit InProcDataNode(std::string addr, KvEngine engine = KvEngine::Badger)
+        : addr_(std::move(addr)), server_(engine) {}
     Status Put(const std::string& key, const Bytes& meta, const Bytes& data) override;
     Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) override;
+    Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+                            uint32_t value_crc) override;
+    bool WantsValueChecksum() const override { return server_.engine() == KvEngine::Mutcask; }
     Status Get(const std::string& key, Bytes* meta, Bytes* data) override;
     Status GetMeta(const std::string& key, Bytes* meta) override;
     Status Delete(const std::string& key) override;

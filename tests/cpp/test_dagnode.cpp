@@ -4,7 +4,8 @@
 //   test_dagnode cpu   datanode framing/CRC, quorum helpers, slots, config checks (no GPU)
 //   test_dagnode gpu   TestDagNode "123456" round trip, RS(10,4) failure/quorum matrix,
 //                      read-repair, RepairDataNode (per key and batched), PutMany batch,
-//                      GetMany (batched degraded reads), RS(10,4) -> RS(4,2) migration;
+//                      GetMany (batched degraded reads), RS(10,4) -> RS(4,2) migration,
+//                      GPU entry (CRC-16) and mutcask value (CRC-32) checksums;
 //                      every stored shard is compared with the CPU oracle (test-only).
 #include <cstdio>
 #include <cstdlib>
@@ -50,7 +51,7 @@ static Bytes rand_bytes(std::mt19937_64& r, size_t n) {
 struct Cluster {
     std::vector<std::shared_ptr<InProcDataNode>> dn;
     std::unique_ptr<DagNode> node;
-    Cluster(int k, int m) {
+    explicit Cluster(int k, int m, KvEngine engine = KvEngine::Badger) {
         DagNodeConfig cfg;
         cfg.name = "dag_node1";
         cfg.data_blocks = k;
@@ -58,7 +59,7 @@ struct Cluster {
         std::vector<std::shared_ptr<DataNodeClient>> clients;
         for (int i = 0; i < k + m; i++) {
             cfg.nodes.push_back("127.0.0.1:" + std::to_string(9011 + i));
-            dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back()));
+            dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back(), engine));
             clients.push_back(dn.back());
         }
         Status s = DagNode::New(cfg, clients, &node);
@@ -139,6 +140,51 @@ static void test_datanode_sender_checksum() {
     Status st = s.Get("c", &m2, &d2);
     CHECK(!st.ok() && st.err == "checking crc failed");
     CHECK(rs_oracle_datanode_entry_crc(meta.data(), meta.size(), data.data(), data.size()) == good);
+}
+
+static uint32_t le32(const Bytes& b, size_t off) {
+    return uint32_t(b[off]) | uint32_t(b[off + 1]) << 8 | uint32_t(b[off + 2]) << 16 | uint32_t(b[off + 3]) << 24;
+}
+
+// kv/mutcask/cask.go:73-97 under the datanode (server.go:207): the stored value is
+// |crc32 (4 LE)|entry|, re-checked on every read; Size stays the entry size (cask.go:235)
+static void test_datanode_mutcask() {
+    const char* cv = "mutation of bitcask";  // cask_test.go TestValueEncodeDecode's value
+    CHECK(crc32_ieee(reinterpret_cast<const uint8_t*>(cv), std::strlen(cv)) ==
+          rs_oracle_crc32_ieee(reinterpret_cast<const uint8_t*>(cv), std::strlen(cv)));
+    CHECK(crc32_ieee(reinterpret_cast<const uint8_t*>("123456789"), 9) == 0xCBF43926u);
+    DataNodeServer s(KvEngine::Mutcask);
+    const Bytes meta = {6, 0, 0, 0}, data = str("123456");
+    CHECK_OK(s.Put("key", meta, data));
+    Bytes v, e, m2, d2;
+    CHECK(s.RawValue("key", &v) && s.RawEntry("key", &e));
+    CHECK(v.size() == e.size() + 4 && Bytes(v.begin() + 4, v.end()) == e);
+    CHECK(le32(v, 0) == rs_oracle_crc32_ieee(e.data(), e.size()));
+    CHECK(le32(v, 0) == rs_oracle_mutcask_entry_crc(le32(e, 0), meta.data(), 4, data.data(), data.size()));
+    CHECK(le32(e, 0) == rs_oracle_datanode_entry_crc(meta.data(), 4, data.data(), data.size()));
+    CHECK_OK(s.Get("key", &m2, &d2));
+    CHECK(m2 == meta && d2 == data);
+    int64_t sz = 0;
+    CHECK_OK(s.Size("key", &sz));
+    CHECK(sz == kHeaderSize + 4 + 6);
+    // the sender's pair of checksums gives the same stored value; a wrong value checksum is
+    // caught by the engine before the datanode's own check
+    CHECK_OK(s.PutWithChecksums("k2", meta, data, uint16_t(le32(e, 0)), le32(v, 0)));
+    Bytes v2;
+    CHECK(s.RawValue("k2", &v2) && v2 == v);
+    CHECK_OK(s.PutWithChecksums("k3", meta, data, uint16_t(le32(e, 0)), le32(v, 0) ^ 1));
+    Status g = s.Get("k3", &m2, &d2);
+    CHECK(!g.ok() && g.err == "mutcask: data may be rotted");
+    CHECK(!s.GetMeta("k3", &m2).ok());
+    s.CorruptByte("key", kHeaderSize + 4 + 2);  // a data byte of the entry
+    g = s.Get("key", &m2, &d2);
+    CHECK(!g.ok() && g.err == "mutcask: data may be rotted");
+    // a client over badger drops the value checksum and keeps the entry byte-identical
+    InProcDataNode b("b");
+    CHECK(!b.WantsValueChecksum() && InProcDataNode("m", KvEngine::Mutcask).WantsValueChecksum());
+    CHECK_OK(b.PutWithChecksums("key", meta, data, uint16_t(le32(e, 0)), 12345));
+    Bytes eb;
+    CHECK(b.server().RawEntry("key", &eb) && b.server().RawValue("key", &v2) && eb == e && v2 == e);
 }
 
 static void test_quorum_helpers() {
@@ -492,6 +538,63 @@ static void test_gpu_entry_checksums() {
     }
 }
 
+// Mutcask-backed datanodes: PutMany hands every datanode both checksums from the GPU pass
+// (R(shard) CRC-16 and R32(shard) CRC-32, rsmi_encode_batch_host_crcs); the stored values --
+// |crc32|crc16|sizes|meta|shard| -- are byte-identical to the ones the datanodes compute
+// themselves, and both checksums equal the oracle's.  Single Puts leave the CRC-32 to the
+// datanode.  Reads verify both.
+static void test_gpu_value_checksums() {
+    for (auto km : {std::make_pair(2, 1), std::make_pair(10, 4), std::make_pair(16, 4)}) {
+        const int k = km.first, m = km.second, n = k + m;
+        Cluster gpu(k, m, KvEngine::Mutcask), host(k, m, KvEngine::Mutcask);
+        host.node->SetGpuChecksums(false);
+        std::mt19937_64 r(91 + k);
+        std::vector<std::string> keys;
+        std::vector<Bytes> blocks;
+        for (size_t sz : {size_t(6), size_t(4099), size_t(262144)}) {
+            keys.push_back("single-" + std::to_string(sz));
+            blocks.push_back(rand_bytes(r, sz));
+            CHECK_OK(gpu.node->Put(keys.back(), blocks.back()));
+            CHECK_OK(host.node->Put(keys.back(), blocks.back()));
+        }
+        for (size_t sz : {size_t(17), size_t(262144), size_t(1048590)}) {
+            std::vector<std::string> bk;
+            std::vector<Bytes> bb;
+            for (int i = 0; i < 9; i++) {
+                bk.push_back("batch-" + std::to_string(sz) + "-" + std::to_string(i));
+                bb.push_back(rand_bytes(r, sz));
+            }
+            CHECK_OK(gpu.node->PutMany(bk, bb));
+            CHECK_OK(host.node->PutMany(bk, bb));
+            keys.insert(keys.end(), bk.begin(), bk.end());
+            blocks.insert(blocks.end(), bb.begin(), bb.end());
+        }
+        for (size_t j = 0; j < keys.size(); j++) {
+            auto want = oracle_shards(k, m, blocks[j]);
+            Bytes meta(4);
+            for (int b = 0; b < 4; b++) meta[b] = uint8_t(uint32_t(blocks[j].size()) >> (8 * b));
+            for (int i = 0; i < n; i++) {
+                Bytes vg, vh;
+                CHECK(gpu.dn[i]->server().RawValue(keys[j], &vg));
+                CHECK(host.dn[i]->server().RawValue(keys[j], &vh));
+                CHECK(vg == vh);
+                const uint32_t c16 = rs_oracle_datanode_entry_crc(meta.data(), 4, want[i].data(), want[i].size());
+                CHECK(le32(vg, 4) == c16);
+                CHECK(le32(vg, 0) == rs_oracle_mutcask_entry_crc(c16, meta.data(), 4, want[i].data(), want[i].size()));
+            }
+            Bytes got;
+            CHECK_OK(gpu.node->Get(keys[j], &got));
+            CHECK(got == blocks[j]);
+        }
+        // a rotted value on one datanode: the read treats that shard as missing and
+        // reconstructs from the others (node.go:254-258), then read-repair rewrites it
+        gpu.dn[0]->server().CorruptByte(keys.back(), kHeaderSize + 4 + 1);
+        Bytes got;
+        CHECK_OK(gpu.node->Get(keys.back(), &got));
+        CHECK(got == blocks.back());
+    }
+}
+
 // Concurrent DagNode.Put from many threads (the reference's goroutine-per-request Dag Pool):
 // the per-block encodes coalesce into GPU batches (rsmi_encode_block_coalesced), and every
 // stored shard and entry checksum still equals the oracle's.
@@ -565,6 +668,7 @@ int main(int argc, char** argv) {
     }
     test_datanode_server();
     test_datanode_sender_checksum();
+    test_datanode_mutcask();
     test_quorum_helpers();
     test_config_and_slots();
     if (mode == "gpu") {
@@ -578,6 +682,7 @@ int main(int argc, char** argv) {
         test_batches_span_staging_chunks();
         test_migrate();
         test_gpu_entry_checksums();
+        test_gpu_value_checksums();
         test_concurrent_puts();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);

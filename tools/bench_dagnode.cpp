@@ -1,7 +1,8 @@
 // bench_dagnode.cpp -- end-to-end rates of the Dag Node mirror over in-process datanodes
 // (host memory in, framed+CRC'd shard entries out): per-block vs GPU-batched Put (entry
 // checksums from the GPU, and from the datanode's own CRC pass), Get with
-// a lost data shard, and RepairDataNode.  Diagnostic; numbers recorded in DESIGN.md.
+// a lost data shard, RepairDataNode, and PutMany over mutcask-backed datanodes (CRC-32 value
+// checksums from the GPU or the datanodes).  Diagnostic; numbers recorded in DESIGN.md.
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -129,6 +130,31 @@ int main(int argc, char** argv) {
     t0 = clk::now();
     d->RepairDataNodeBatched(0, 3, 256, &rep);
     const double repb = secs(t0);
+    // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
+    // entry (cask.go:73-79).  PutMany with both checksums from the GPU pass, against the
+    // datanodes computing both themselves.
+    double putm = 0, putmh = 0, c32 = 0;
+    {
+        DagNodeConfig mc = cfg;
+        std::vector<std::shared_ptr<DataNodeClient>> mcl;
+        for (int i = 0; i < k + m; i++) mcl.push_back(std::make_shared<InProcDataNode>(cfg.nodes[i], KvEngine::Mutcask));
+        std::unique_ptr<DagNode> md;
+        if (!DagNode::New(mc, mcl, &md).ok()) return 2;
+        md->HealthCheckAll();
+        md->PutMany({"warm"}, {blocks[0]});
+        md->SetGpuChecksums(false);
+        t0 = clk::now();
+        md->PutMany(keys, blocks);
+        putmh = secs(t0);
+        md->SetGpuChecksums(true);
+        t0 = clk::now();
+        md->PutMany(keys, blocks);
+        putm = secs(t0);
+        t0 = clk::now();
+        volatile uint32_t s32 = 0;
+        for (int i = 0; i < N; i++) s32 ^= crc32_ieee(blocks[i].data(), blocks[i].size());
+        c32 = secs(t0);
+    }
     std::printf("RS(%d,%d) %d blocks x %zu B (%.2f GiB payload), in-process datanodes\n", k, m, N, B, gib);
     std::printf("Put per block      %8.2f GiB/s (datanode CRC: %.2f)\n", gib / put1, gib / put1h);
     std::printf("PutMany (batched)  %8.2f GiB/s (datanode CRC: %.2f)\n", gib / putb, gib / putbh);
@@ -140,6 +166,8 @@ int main(int argc, char** argv) {
                 gcalls, gbatches);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);
+    std::printf("PutMany, mutcask   %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / putm, gib / putmh);
     std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes)\n", gib / crc);
+    std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, slice-by-8)\n", gib / c32);
     return 0;
 }
