@@ -247,17 +247,26 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
     if (!s.ok()) return s;
     std::vector<Bytes> shards;
-    std::vector<uint32_t> raw;
-    s = gpu_checksums_ ? enc.EncodeDataWithCrc(block, &shards, &raw) : enc.EncodeData(block, &shards);
+    std::vector<uint32_t> raw, raw32;
+    bool want32 = false;  // mutcask-backed datanodes keep a CRC-32 of every value as well
+    for (auto& sn : nodes_) want32 |= gpu_checksums_ && sn.client->WantsValueChecksum();
+    s = gpu_checksums_ ? enc.EncodeDataWithCrcs(block, &shards, &raw, want32 ? &raw32 : nullptr)
+                       : enc.EncodeData(block, &shards);
     if (!s.ok()) return s;
     const int wq = EntryQuorum().second;
     std::vector<Status> res(nodes_.size());
     const size_t S = shards.empty() ? 0 : shards[0].size();
     last_shard_ = S;
     fan(int(nodes_.size()), [&](int i) {  // one goroutine per datanode, no cancel
-        res[i] = raw.empty() ? nodes_[i].client->Put(key, meta, shards[i])
-                             : nodes_[i].client->PutWithChecksum(key, meta, shards[i],
-                                                                 entry_checksum(meta, shards[i].size(), raw[i]));
+        DataNodeClient& cl = *nodes_[i].client;
+        if (raw.empty()) {
+            res[i] = cl.Put(key, meta, shards[i]);
+            return;
+        }
+        const uint16_t c16 = entry_checksum(meta, S, raw[i]);
+        res[i] = !raw32.empty() && cl.WantsValueChecksum()
+                     ? cl.PutWithChecksums(key, meta, shards[i], c16, value_checksum(meta, S, c16, raw32[i]))
+                     : cl.PutWithChecksum(key, meta, shards[i], c16);
     }, S);
     QuorumWait w(wq, int(nodes_.size()) - wq + 1);
     for (const Status& r : res) w.add(r);

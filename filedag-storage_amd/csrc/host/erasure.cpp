@@ -103,9 +103,15 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
 }
 
 Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw) const {
+    return EncodeDataWithCrcs(data, shards, raw, nullptr);
+}
+
+Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw,
+                                   std::vector<uint32_t>* raw32) const {
     const int n = data_blocks_ + parity_blocks_;
     shards->assign(size_t(n), Bytes());
     raw->clear();
+    if (raw32) raw32->clear();
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
@@ -113,7 +119,9 @@ Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards,
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     Bytes flat(size_t(n) * S);
     raw->assign(size_t(n), 0);
-    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat.data(), raw->data());
+    if (raw32) raw32->assign(size_t(n), 0);
+    rc = rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat.data(), raw->data(),
+                                          raw32 ? raw32->data() : nullptr);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
     return Status::Ok();

@@ -62,6 +62,9 @@ public:
     // EncodeData plus R(shard) of every shard from the GPU (include/rsmi.h, datanode CRC-16);
     // raw is left empty for an empty block
     Status EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw) const;
+    // ... and, when raw32 is not null, R32(shard) for the mutcask value checksum (CRC-32)
+    Status EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw,
+                              std::vector<uint32_t>* raw32) const;
     Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
     Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;
     int64_t ShardSize() const { return ceil_frac(block_size_, data_blocks_); }

@@ -42,20 +42,23 @@ void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
         return;
     }
     if (key[0] == 'E') {
-        bool want_raw = false;
+        bool want_raw = false, want32 = false;
         for (size_t j = 0; j < nb; j++) {
             uint8_t* dst = h + j * n * S;
             std::memcpy(dst, rq[j]->block, rq[j]->B);
             std::memset(dst + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
             want_raw |= rq[j]->raw != nullptr;
+            want32 |= rq[j]->raw32 != nullptr;
         }
-        std::vector<uint32_t> raw(want_raw ? nb * n : 0);
-        const int rc = encode_host_impl(c, h, n * S, h + k * S, n * S, S, nb, want_raw ? raw.data() : nullptr);
+        std::vector<uint32_t> raw(want_raw ? nb * n : 0), raw32(want32 ? nb * n : 0);
+        const int rc = encode_host_impl(c, h, n * S, h + k * S, n * S, S, nb, want_raw ? raw.data() : nullptr,
+                                        want32 ? raw32.data() : nullptr);
         for (size_t j = 0; j < nb; j++) {
             rq[j]->rc = rc;
             if (rc) continue;
             std::memcpy(rq[j]->out, h + j * n * S, n * S);
             if (rq[j]->raw) std::memcpy(rq[j]->raw, raw.data() + j * n, n * 4);
+            if (rq[j]->raw32) std::memcpy(rq[j]->raw32, raw32.data() + j * n, n * 4);
         }
         return;
     }
@@ -129,14 +132,19 @@ int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
 
 extern "C" {
 
-int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
-                                uint32_t* raw_out) {
+int rsmi_encode_block_coalesced_crcs(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                     uint32_t* raw16_out, uint32_t* raw32_out) {
     if (!c) return RSMI_ERR_INVALID_ARG;
     if (B == 0) return RSMI_ERR_SHORT_DATA;
     if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
-    rsmi_ctx::CoalReq req{block, B, shards_out, raw_out, "E" + std::to_string(rsmi_shard_size(B, c->k)) + ":",
+    rsmi_ctx::CoalReq req{block, B, shards_out, raw16_out, raw32_out, "E" + std::to_string(rsmi_shard_size(B, c->k)) + ":",
                           RSMI_OK, false};
     return coalesce(c, req);
+}
+
+int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                uint32_t* raw_out) {
+    return rsmi_encode_block_coalesced_crcs(c, block, B, shards_out, raw_out, nullptr);
 }
 
 int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
@@ -149,7 +157,7 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     std::string key = "R" + std::to_string(S) + ":";
     for (int i = 0; i < c->n; i++) key.push_back(present[i] ? '1' : '0');
     for (int i = 0; i < c->n; i++) key.push_back(want[i] ? '1' : '0');
-    rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, std::move(key), RSMI_OK, false};
+    rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, nullptr, std::move(key), RSMI_OK, false};
     return coalesce(c, req);
 }
 

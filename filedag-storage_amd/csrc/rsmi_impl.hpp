@@ -113,6 +113,7 @@ struct rsmi_ctx {
         size_t B;
         uint8_t* out;
         uint32_t* raw;
+        uint32_t* raw32;  // encode: optional CRC-32 R32(shard) per shard
         std::string key;
         int rc;
         bool done;

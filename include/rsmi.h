@@ -150,6 +150,11 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
 int rsmi_encode_block_coalesced(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out,
                                 uint32_t* raw_out);
 
+/* rsmi_encode_block_coalesced with the mutcask CRC-32 as well: raw32_out[0..k+m) = R32(shard)
+ * when not NULL (see "mutcask CRC-32" below); raw16_out as raw_out above. */
+int rsmi_encode_block_coalesced_crcs(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                     uint32_t* raw16_out, uint32_t* raw32_out);
+
 /* rsmi_reconstruct (same arguments, results and errors), coalesced the same way.  When a
  * datanode is down every concurrent DagNode.Get misses the same shard (node.go:277-282), so
  * concurrent degraded reads share one erasure pattern and batch into one launch; requests

@@ -541,8 +541,8 @@ static void test_gpu_entry_checksums() {
 // Mutcask-backed datanodes: PutMany hands every datanode both checksums from the GPU pass
 // (R(shard) CRC-16 and R32(shard) CRC-32, rsmi_encode_batch_host_crcs); the stored values --
 // |crc32|crc16|sizes|meta|shard| -- are byte-identical to the ones the datanodes compute
-// themselves, and both checksums equal the oracle's.  Single Puts leave the CRC-32 to the
-// datanode.  Reads verify both.
+// themselves, and both checksums equal the oracle's.  Single Puts get both from the
+// coalesced encode (rsmi_encode_block_coalesced_crcs).  Reads verify both.
 static void test_gpu_value_checksums() {
     for (auto km : {std::make_pair(2, 1), std::make_pair(10, 4), std::make_pair(16, 4)}) {
         const int k = km.first, m = km.second, n = k + m;

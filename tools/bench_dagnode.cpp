@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
     // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
     // entry (cask.go:73-79).  PutMany with both checksums from the GPU pass, against the
     // datanodes computing both themselves.
-    double putm = 0, putmh = 0, c32 = 0;
+    double putm = 0, putmh = 0, put1m = 0, put1mh = 0, c32 = 0;
     {
         DagNodeConfig mc = cfg;
         std::vector<std::shared_ptr<DataNodeClient>> mcl;
@@ -144,9 +144,16 @@ int main(int argc, char** argv) {
         md->PutMany({"warm"}, {blocks[0]});
         md->SetGpuChecksums(false);
         t0 = clk::now();
+        for (int i = 0; i < N; i++) md->Put(keys[i], blocks[i]);
+        put1mh = secs(t0);
+        t0 = clk::now();
         md->PutMany(keys, blocks);
         putmh = secs(t0);
         md->SetGpuChecksums(true);
+        md->Put("warm", blocks[0]);
+        t0 = clk::now();
+        for (int i = 0; i < N; i++) md->Put(keys[i], blocks[i]);
+        put1m = secs(t0);
         t0 = clk::now();
         md->PutMany(keys, blocks);
         putm = secs(t0);
@@ -166,6 +173,7 @@ int main(int argc, char** argv) {
                 gcalls, gbatches);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);
+    std::printf("Put, mutcask       %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / put1m, gib / put1mh);
     std::printf("PutMany, mutcask   %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / putm, gib / putmh);
     std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes)\n", gib / crc);
     std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, slice-by-8)\n", gib / c32);
