@@ -116,6 +116,13 @@ void DagNode::fan(int count, const std::function<void(int)>& f, size_t shard_byt
         for (int i = 0; i < count; i++) f(i);
 }
 
+void DagNode::fan_keys(int count, const std::function<void(int)>& f) {
+    if (parallel_ && fan_ && active_.load() <= 1)
+        fan_->run(count, f);
+    else
+        for (int i = 0; i < count; i++) f(i);
+}
+
 DagNode::~DagNode() { Close(); }
 
 void DagNode::Close() {
@@ -326,8 +333,10 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
                 continue;
             }
-            for (size_t j = 0; j < nb; j++) {
-                const uint8_t* base = flat + j * n * S;
+            // the blocks' datanode writes run concurrently (the reference's concurrent Puts),
+            // each with its own node fan-out
+            fan_keys(int(nb), [&](int j) {
+                const uint8_t* base = flat + size_t(j) * n * S;
                 std::vector<Status> res(static_cast<size_t>(n));
                 fan(n, [&](int i) {
                     Bytes shard(base + size_t(i) * S, base + size_t(i + 1) * S);
@@ -345,7 +354,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 QuorumWait w(wq, n - wq + 1);
                 for (const Status& r : res) w.add(r);
                 results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
-            }
+            });
         }
     }
     // node.go:411-416 returns the error of the last Put
@@ -453,11 +462,13 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
     for (size_t k0 = 0; k0 < keys.size(); k0 += batch) {
         const size_t nk = std::min(batch, keys.size() - k0);
         std::vector<Fetched> fs(nk);
+        // the keys' fetches run concurrently, like the reference's concurrent Gets (one
+        // goroutine per dag pool request), each with its own node fan-out
+        fan_keys(int(nk), [&](int q) { (*statuses)[k0 + q] = fetch_for_get(keys[k0 + q], &fs[q]); });
         // (block size, survivor pattern) -> chunk positions of keys whose data shards need decoding
         std::map<std::pair<int32_t, std::string>, std::vector<size_t>> groups;
         for (size_t q = 0; q < nk; q++) {
-            Status& st = (*statuses)[k0 + q];
-            st = fetch_for_get(keys[k0 + q], &fs[q]);
+            const Status& st = (*statuses)[k0 + q];
             if (!st.ok()) continue;
             bool data_missing = false;
             for (int c = 0; c < k; c++) data_missing |= fs[q].shards[c].empty();
@@ -484,21 +495,24 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                 const size_t nb = std::min(chunk, g.second.size() - b0);
                 uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
                 if (!flat) continue;
-                for (size_t j = 0; j < nb; j++)
+                fan_keys(int(nb), [&](int j) {
                     for (int c = 0; c < n; c++)
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
+                });
                 if (rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
                     continue;  // leave these keys to the per-key path
-                for (size_t j = 0; j < nb; j++)
+                fan_keys(int(nb), [&](int j) {
                     for (int c = 0; c < k; c++)
                         if (!present[c]) {
                             const uint8_t* row = flat + (j * n + c) * S;
                             fs[g.second[b0 + j]].shards[c].assign(row, row + S);
                         }
+                });
             }
         }
-        for (size_t q = 0; q < nk; q++)
+        fan_keys(int(nk), [&](int q) {
             if ((*statuses)[k0 + q].ok()) (*statuses)[k0 + q] = finish_get(keys[k0 + q], fs[q], &(*blocks)[k0 + q]);
+        });
     }
 }
 
@@ -655,6 +669,7 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
 }
 
 Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* repaired) {
+    Active act(active_);
     if (from >= int(nodes_.size())) return Status::Error("index greater than max index of nodes");
     if (to >= int(nodes_.size())) return Status::Error("repair index greater than max index of nodes");
     if (batch == 0) batch = 1;
@@ -687,37 +702,62 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         rc = rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), required.data());
         if (rc) return rsmi_status(rc);
         const Bytes meta = encode_meta(size);
+        // the rebuilt rows go to the target concurrently; outcomes are taken in key order
+        std::vector<Status> ps(nb);
+        fan_keys(int(nb), [&](int j) {
+            const uint8_t* row = flat + (size_t(j) * n + size_t(to)) * S;
+            ps[j] = nodes_[to].client->Put(pend[j].key, meta, Bytes(row, row + S));
+        });
         for (size_t j = 0; j < nb; j++) {
-            const uint8_t* row = flat + (j * n + size_t(to)) * S;
-            Status ps = nodes_[to].client->Put(pend[j].key, meta, Bytes(row, row + S));
-            if (!ps.ok()) return ps;
+            if (!ps[j].ok()) return ps[j];
             done++;
         }
         pend.clear();
         return Status::Ok();
     };
-    for (const auto& key : keys) {
-        Bytes mb;
-        if (nodes_[to].client->GetMeta(key, &mb).ok()) continue;
-        int size;
-        if (!GetSize(key, &size).ok()) continue;
+    // Each key's checks and fetch (the target's GetMeta, the meta quorum, the k-of-n fetch) run
+    // concurrently over a window of keys; the results are then taken in key order, so the
+    // grouping, the flushes and the errors returned are those of the sequential loop.
+    struct Fetch {
+        bool use = false;
+        int size = 0;
         std::vector<Bytes> shards;
-        if (!fetch_for_repair(key, to, &shards).ok()) continue;
-        if (size <= 0) {  // empty block: the per-key path's error behaviour (ErrShardNoData)
-            Erasure enc;
-            s = Erasure::New(k, m, size, &enc, device_);
-            if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
-            if (!s.ok()) return s;
-            continue;
-        }
-        std::string pat(size_t(n), '0');
-        for (int i = 0; i < n; i++) pat[i] = shards[i].empty() ? '0' : '1';
-        auto gk = std::make_pair(size, pat);
-        auto& pend = groups[gk];
-        pend.push_back(Pending{key, std::move(shards)});
-        if (pend.size() >= std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(size), k)))) {
-            s = flush(gk, pend);
-            if (!s.ok()) return s;
+    };
+    const size_t window = std::min<size_t>(std::max<size_t>(batch, 1), 64);
+    for (size_t c0 = 0; c0 < keys.size(); c0 += window) {
+        const size_t nk = std::min(window, keys.size() - c0);
+        std::vector<Fetch> fr(nk);
+        fan_keys(int(nk), [&](int q) {
+            const std::string& key = keys[c0 + q];
+            Bytes mb;
+            if (nodes_[to].client->GetMeta(key, &mb).ok()) return;
+            int size;
+            if (!GetSize(key, &size).ok()) return;
+            if (!fetch_for_repair(key, to, &fr[q].shards).ok()) return;
+            fr[q].size = size;
+            fr[q].use = true;
+        });
+        for (size_t q = 0; q < nk; q++) {
+            if (!fr[q].use) continue;
+            const std::string& key = keys[c0 + q];
+            const int size = fr[q].size;
+            std::vector<Bytes>& shards = fr[q].shards;
+            if (size <= 0) {  // empty block: the per-key path's error behaviour (ErrShardNoData)
+                Erasure enc;
+                s = Erasure::New(k, m, size, &enc, device_);
+                if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
+                if (!s.ok()) return s;
+                continue;
+            }
+            std::string pat(size_t(n), '0');
+            for (int i = 0; i < n; i++) pat[i] = shards[i].empty() ? '0' : '1';
+            auto gk = std::make_pair(size, pat);
+            auto& pend = groups[gk];
+            pend.push_back(Pending{key, std::move(shards)});
+            if (pend.size() >= std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(size), k)))) {
+                s = flush(gk, pend);
+                if (!s.ok()) return s;
+            }
         }
     }
     for (auto& g : groups) {

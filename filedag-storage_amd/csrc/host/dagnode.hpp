@@ -149,6 +149,8 @@ private:
     std::atomic<size_t> last_shard_{0};   // shard size of the latest Put / Get (for GetMeta)
     std::unique_ptr<FanOut> fan_;
     void fan(int count, const std::function<void(int)>& f, size_t shard_bytes);
+    // whole-key tasks (GetMany): on the pool for a lone caller, whatever the shard size
+    void fan_keys(int count, const std::function<void(int)>& f);
     struct Active {  // counts a caller for the fan-out policy
         std::atomic<int>& a;
         explicit Active(std::atomic<int>& x) : a(x) { a++; }

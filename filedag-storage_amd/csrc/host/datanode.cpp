@@ -104,7 +104,15 @@ Status DataNodeServer::store(const std::string& key, const Bytes& meta, const By
     put_le32(e, crc ? *crc : crc16_ibm(e + 4, v.size() - pre - 4));  // server.go:70-75
     if (pre) put_le32(v.data(), value_crc ? *value_crc : crc32_ieee(e, v.size() - pre));
     std::lock_guard<std::mutex> g(mu_);
-    kv_[key] = std::move(v);
+    auto it = kv_.find(key);
+    if (it != kv_.end() && it->second.capacity() >= v.size()) {
+        // overwrite in place: the stored buffer may come from another thread's malloc arena
+        // (concurrent Puts), and freeing it here would leave this thread's arena to fault in
+        // fresh pages for every later entry
+        it->second.assign(v.begin(), v.end());
+    } else {
+        kv_[key] = std::move(v);
+    }
     return Status::Ok();
 }
 
