@@ -58,6 +58,8 @@ def parse():
                         "transient (DESIGN.md section 5); 0 = off")
     p.add_argument("--chunks-per-lane", type=int, default=0)
     p.add_argument("--nontemporal", type=int, default=-1)
+    p.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                   help="diagnostic: any rsmi_set_option knob, repeatable (A/B in the bench's own context)")
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal only: every rank uses cuda:0 (multi-rank path on a 1-GPU box)")
     p.add_argument("--copy-inclusive", action="store_true",
@@ -252,6 +254,9 @@ def main():
         codec.set_option("chunks_per_lane", a.chunks_per_lane)
     if a.nontemporal >= 0:
         codec.set_option("nontemporal", a.nontemporal)
+    for kv in a.option:
+        key, val = kv.split("=", 1)
+        codec.set_option(key, int(val))
     stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
 
@@ -336,6 +341,7 @@ def main():
             "row_pitch": rs,
             "settle": {"ms": a.settle_ms, "steps": settle_steps},
             "parallelism": f"independent blocks, {world} GPU(s), one process each, no collective",
+            **({"options": a.option} if a.option else {}),
         },
         "roofline": {
             "bound": "hbm",

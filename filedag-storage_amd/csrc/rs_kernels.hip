@@ -40,7 +40,10 @@ constexpr int default_prefetch() {
 }
 
 // K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row, NT cache policy (0 = default
-// loads and stores, 1 = nontemporal loads and stores, 2 = nontemporal loads, default stores),
+// loads and stores, 1 = nontemporal loads and stores, 2 = nontemporal loads, default stores,
+// 3 = nontemporal loads, write-through sc1 buffer stores that drop the line from the L2,
+// 4 = policy 1 with the stores as nontemporal buffer stores: 32-bit lane offsets against a
+// wave-uniform descriptor instead of 64-bit lane addresses),
 // PF rows in flight per lane (0 = default_prefetch), WPS waves per SIMD the register
 // allocation must allow.
 // TS: table source.  0 = all five field words per output from LDS (broadcast
@@ -59,8 +62,10 @@ constexpr int default_prefetch() {
 // turns them into R(row).  The small host path uses this so the shard bytes cross PCIe once.
 // SH64: build the shifted selector words of two dwords with one 64-bit shift each
 // (v_lshrrev_b64; the bits that cross from the high dword land in masked-off positions).
+// SP >= 0 (aligned layouts, A/B): whole output chunks leave by buffer stores with these cache
+// bits (aux: 1 = sc0, 2 = nt, 16 = sc1, 17 = sc0 sc1, 18 = nt sc1); -1 = the NT policy.
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false, bool SH64 = false>
+          bool UA = false, bool CRC = false, bool SH64 = false, int SP = -1>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -300,7 +305,11 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
                     for (int j = 0; j < MT; j++) {
                         u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
-                        if constexpr (NT == 1)
+                        constexpr int kSP = SP >= 0 ? SP : (NT == 3 ? 16 : NT == 4 ? 2 : -1);
+                        if constexpr (kSP >= 0) {
+                            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob + out_off[j], 0, 0x7FFFFFFF, 0x00020000);
+                            __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, int(boff), 0, kSP);
+                        } else if constexpr (NT == 1)
                             __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
                         else
                             *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
@@ -574,9 +583,9 @@ void* crc16_rows_kernel(bool aligned, int fold) {
 
 // ------------------------------------------------------------------ dispatch table
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false, bool SH64 = false>
+          bool UA = false, bool CRC = false, bool SH64 = false, int SP = -1>
 static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC, SH64>);
+    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC, SH64, SP>);
 }
 
 // fused chunk-CRC variants: UA, D = 1, the auto cache policy of the shape
@@ -641,6 +650,19 @@ const ExpKernelTable& exp_kernels() {
         x.fn[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 1>();
         x.fn[0][4] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, true>();
         x.fn[1][4] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, true>();
+        // store cache bits (option store_aux), in the order of kStoreAux
+        x.st[0][0] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 0>();
+        x.st[0][1] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 1>();
+        x.st[0][2] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 2>();
+        x.st[0][3] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 16>();
+        x.st[0][4] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 17>();
+        x.st[0][5] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 18>();
+        x.st[1][0] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 0>();
+        x.st[1][1] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 1>();
+        x.st[1][2] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 2>();
+        x.st[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 16>();
+        x.st[1][4] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 17>();
+        x.st[1][5] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 18>();
         return x;
     }();
     return t;
@@ -655,6 +677,10 @@ const FastKernelTable& fast_kernels() {
         fill_d<2, 1>(x);
         fill_d<1, 2>(x);
         fill_d<2, 2>(x);
+        fill_d<1, 3>(x);
+        fill_d<2, 3>(x);
+        fill_d<1, 4>(x);
+        fill_d<2, 4>(x);
         fill_ua<1>(x);
         fill_ua<2>(x);
         fill_ua<3>(x);

@@ -48,17 +48,20 @@ __device__ __forceinline__ void static_for(F&& f) {
 // its LDS-DMA tracking cannot tell the ring's slots apart and put a vmcnt(0) at the start of
 // every tile, which drains the very queue this kernel keeps full.  All waits on these loads
 // are explicit (wait_vmcnt); the loop issues no compiler-tracked vector loads.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; nothing else here uses it
 __device__ __forceinline__ void dma16_nt(const void* g, uint32_t lds) {
+    // M0 is compiler-reserved: saved and restored inside the statement that writes it; the
+    // s_nop covers the M0 write -> LDS-DMA read of M0 (one wait state on gfx9)
+    uint32_t keep;
     asm volatile(
-        "s_mov_b32 m0, %0\n\t"
-        "s_nop 0\n\t"  // M0 write -> LDS-DMA read of M0: one wait state on gfx9
-        "global_load_lds_dwordx4 %1, off nt" ::"s"(lds),
-        "v"(g)
-        : "memory", "m0");
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds)
+        : "memory");
 }
-#pragma clang diagnostic pop
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -24,7 +24,7 @@ struct RsPlanDev {
 // Instantiated fast kernels: fn[K][MT][D][NT] (null when K has no instantiation); NT is
 // the cache policy (0 default, 1 nontemporal loads + stores, 2 nontemporal loads only).
 struct FastKernelTable {
-    void* fn[17][kMaxMT + 1][3][3];
+    void* fn[17][kMaxMT + 1][3][5];  // [K][MT][D][cache policy 0..4]
     void* ua[17][kMaxMT + 1][3];  // unaligned-layout variants [K][MT][NT], D = 1
     void* ua_crc[17][kMaxMT + 1];  // the same with fused per-chunk CRC-16 (auto cache policy)
 };
@@ -34,7 +34,9 @@ struct FastKernelTable {
 // 2 for MT1, the auto policy's choices).
 struct ExpKernelTable {
     void* fn[2][5];  // v 4 = 64-bit selector shifts (SH64)
+    void* st[2][6];  // buffer stores with the cache bits kStoreAux[v] (option store_aux)
 };
+constexpr int kStoreAux[6] = {0, 1, 2, 16, 17, 18};
 
 // LDS-DMA staged variants (rs_lds_kernels.hip, option lds_dma): [0] RS(10,4) encode and
 // [1] 1-row reconstruct with 4 waves per workgroup, [2]/[3] the same with 2

@@ -174,7 +174,9 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
     for (const DevTile& t : plan.tiles) {
         const int D = ua ? 1 : c->opt_d;
         int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
-        if (ua && NT == 0) NT = auto_cache_policy(t.K, t.MT);  // UA variants exist for policies 1 and 2
+        // UA variants exist for policies 1 and 2 (sc1 buffer stores need aligned chunks)
+        if (ua && (NT == 0 || NT >= 3)) NT = t.K >= 4 * t.MT ? 2 : 1;
+        if (!ua && NT == 1 && c->opt_buffer_stores) NT = 4;
         void* fn = nullptr;
         if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
         if (ua && t.K <= 16) fn = fuse ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().ua[t.K][t.MT][NT];
@@ -190,6 +192,13 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][c->opt_tables == 1 ? 3 : 4];
             ts_label = c->opt_tables;
         }
+        int sp_label = -1;
+        if (fn && !ua && c->opt_store_aux >= 0 && t.K == 10 && D == 1 && ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2)))
+            for (int i = 0; i < 6; i++)
+                if (kStoreAux[i] == c->opt_store_aux) {
+                    fn = exp_kernels().st[t.MT == 4 ? 0 : 1][i];
+                    sp_label = c->opt_store_aux;
+                }
         int wpg = kWG / kWave, lds_label = 0;
         if (fn && !ua && c->opt_lds >= 1 && c->opt_lds <= 2 && t.K == 10 && D == 1 &&
             ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
@@ -231,6 +240,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
             if (ts_label) c->last_kernel += ts_label == 1 ? ",TS=1" : ",SH64";
             if (lds_label) c->last_kernel += ",LDS,WPG=" + std::to_string(lds_label);
+            if (sp_label >= 0) c->last_kernel += ",SP=" + std::to_string(sp_label);
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -428,7 +438,7 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         if (value != 1 && value != 2) return RSMI_ERR_INVALID_ARG;
         c->opt_d = int(value);
     } else if (!std::strcmp(key, "nontemporal")) {
-        if (value < -1 || value > 2) return RSMI_ERR_INVALID_ARG;
+        if (value < -1 || value > 4) return RSMI_ERR_INVALID_ARG;
         c->opt_nt = int(value);
     } else if (!std::strcmp(key, "prefetch")) {
         // 4/8/10 = rows in flight (A/B only; RS(10,4) encode and 1-row reconstruct, NT=1)
@@ -441,6 +451,15 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "tables")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
+    } else if (!std::strcmp(key, "buffer_stores")) {
+        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_buffer_stores = int(value);
+    } else if (!std::strcmp(key, "store_aux")) {
+        // buffer-store cache bits for the RS(10,4) encode / 1-row reconstruct shapes (A/B)
+        bool ok = value == -1;
+        for (int a : kStoreAux) ok |= value == a;
+        if (!ok) return RSMI_ERR_INVALID_ARG;
+        c->opt_store_aux = int(value);
     } else if (!std::strcmp(key, "lds_dma")) {
         // 1/2 = LDS-DMA staged kernel with 4/2 waves per workgroup (rs_lds_kernels.hip; aligned
         // RS(10,4) encode and 1-row reconstruct shapes)

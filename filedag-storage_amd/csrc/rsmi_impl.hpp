@@ -97,6 +97,8 @@ struct rsmi_ctx {
     int opt_prefetch = 0;
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     int opt_crc_fold = 1;   // CRC chunk fold: 1 = nibble tables, 0 = byte tables (A/B)
+    int opt_buffer_stores = 0;  // 1: aligned launches of policy 1 use policy 4 (buffer stores)
+    int opt_store_aux = -1;  // >= 0: RS(10,4) kernels store with these buffer cache bits (A/B)
     int opt_lds = 0;        // 1/2 = LDS-DMA staged kernel, 4/2 waves per workgroup (A/B)
     int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
     long opt_small_bytes = 2L << 20;  // host calls up to this many shard bytes run zero-copy

@@ -149,8 +149,8 @@ def test_null_arguments():
         assert L.rsmi_set_option(c._h, b"no_such_knob", 1) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"chunks_per_lane", 3) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"chunks_per_lane", 2) == rsmi.OK
-        assert L.rsmi_set_option(c._h, b"nontemporal", 3) == rsmi.ErrInvalidArg
-        for v in (-1, 0, 1, 2):
+        assert L.rsmi_set_option(c._h, b"nontemporal", 5) == rsmi.ErrInvalidArg
+        for v in (-1, 0, 1, 2, 3, 4):
             assert L.rsmi_set_option(c._h, b"nontemporal", v) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"prefetch", 505) == rsmi.ErrInvalidArg
         assert L.rsmi_set_option(c._h, b"zero_copy", 0) == rsmi.OK
@@ -161,7 +161,7 @@ def test_null_arguments():
 def test_new_options_and_stats_validate():
     L = rsmi.lib()
     with rsmi.Codec(10, 4) as c:
-        for key, good, bad in [(b"tables", 2, 3), (b"lds_dma", 2, 3), (b"crc_fold", 0, 2), (b"coalesce_us", 50, -1),
+        for key, good, bad in [(b"tables", 2, 3), (b"lds_dma", 2, 3), (b"store_aux", 16, 3), (b"buffer_stores", 1, 2), (b"crc_fold", 0, 2), (b"coalesce_us", 50, -1),
                                (b"coalesce_max", 16, 0)]:
             assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
             assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key

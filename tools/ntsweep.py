@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic A/B: cache policy (rsmi option "nontemporal" 0/1/2) per output width, over the
+"""Diagnostic A/B: cache policy (rsmi option "nontemporal" 1/2/3) per output width, over the
 BASELINE shapes, interleaved in one process.  Feeds auto_cache_policy in rsmi_core.cpp."""
 import os
 import statistics
@@ -30,7 +30,7 @@ def main():
             bufs[key] = (torch.randint(0, 256, (nb * n * p,), dtype=torch.uint8, device="cuda"), rsmi.Codec(k, m))
         buf, c = bufs[key]
         b = buf.data_ptr()
-        for nt in (0, 1, 2):
+        for nt in (1, 2, 3):
             if lost is None:
                 f = (lambda c=c, b=b, p=p, n=n, k=k, S=S, nb=nb, nt=nt:
                      (c.set_option("nontemporal", nt), c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh)))
