@@ -2,6 +2,8 @@
 // entry points of include/rsmi.h (see rsmi_impl.hpp for the file map).
 #include "rsmi_impl.hpp"
 
+#include <limits>
+
 using namespace rsmi;
 using namespace rsmi::impl;
 
@@ -210,12 +212,13 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
             const uint64_t tpb = (cpb + uint64_t(kWave * D) - 1) / uint64_t(kWave * D);
-            int& occ = c->occupancy[fn];  // queried once per kernel, not per launch
-            if (occ <= 0) {
-                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpg * kWave, 0));
-                if (occ <= 0) occ = 1;
-            }
-            long wg_cap = long(c->num_cu) * occ;
+            // One tile per wave: the hardware dispatcher hands each free slot the next workgroup,
+            // which balances the launch across CUs and XCDs of uneven effective bandwidth.  A
+            // persistent grid (occupancy x CUs, each wave striding over ~26 tiles) gives every CU
+            // the same share and waits for the slowest: measured 9-28 % slower on every BASELINE
+            // shape (tools/bench_ab.sh, profiles/r01/grid_ab.txt).  waves_per_cu > 0 caps the
+            // grid (A/B; the loop in the kernels strides over the remaining tiles).
+            long wg_cap = std::numeric_limits<long>::max();
             if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / wpg);
             // split into launches whose tile count fits 32 bits
             const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / tpb);

@@ -43,7 +43,9 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
         if (occ <= 0) occ = 1;
     }
-    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
+    uint64_t cap = uint64_t(c->num_cu) * uint64_t(occ);  // persistent: the LDS tables load once per workgroup
+    if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
+    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
     void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
@@ -82,7 +84,9 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
         if (occ <= 0) occ = 1;
     }
-    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, uint64_t(c->num_cu) * uint64_t(occ));
+    uint64_t cap = uint64_t(c->num_cu) * uint64_t(occ);  // persistent: the LDS tables load once per workgroup
+    if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
+    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;
     void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
