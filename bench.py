@@ -58,6 +58,7 @@ def parse():
                         "transient (DESIGN.md section 5); 0 = off")
     p.add_argument("--chunks-per-lane", type=int, default=0)
     p.add_argument("--nontemporal", type=int, default=-1)
+    p.add_argument("--pitch", type=int, default=0, help="diagnostic: row pitch in HBM (0 = rsmi_recommended_pitch)")
     p.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                    help="diagnostic: any rsmi_set_option knob, repeatable (A/B in the bench's own context)")
     p.add_argument("--share-device", action="store_true",
@@ -234,6 +235,9 @@ def main():
     B = bkib * 1024
     S = (B + k - 1) // k
     rs = rsmi.recommended_pitch(S)  # power-of-two shard slots in HBM (DESIGN.md "Layout")
+    if a.pitch:
+        assert a.pitch >= S and a.pitch % 16 == 0, "--pitch: a multiple of 16 bytes, at least the shard size"
+        rs = a.pitch
     bs = n * rs
     nb = a.blocks or nb_default
     lost = [int(x) for x in lost_s.split(",") if x != ""]

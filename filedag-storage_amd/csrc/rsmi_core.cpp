@@ -386,13 +386,16 @@ size_t rsmi_recommended_pitch(size_t S) {
     if (S == 0) return 0;
     size_t p = 16;
     while (p < S) p <<= 1;
-    // Measured on MI355X (tools/pitchsweep*.py, DESIGN.md "Layout"): a power-of-two row
-    // pitch is +13% for S = 26215 (32 KiB) and best for S = 262144 (itself a power of
-    // two), but the worst choice for S = 104858 (128 KiB: -4% vs 4 KiB granules).  Use
-    // powers of two for shards up to 64 KiB (padding <= 50%) and exact powers; otherwise
-    // 4 KiB granules.
+    // Measured on MI355X (tools/pitchsweep*.py; in bench.py's own context with --pitch,
+    // profiles/r01/pitch_ab.txt): a power-of-two row pitch is best for S = 26215 (32 KiB, far
+    // ahead of every 4 KiB step) and for S = 262144 (itself a power of two), and the worst
+    // choice for S = 104858 (128 KiB).  There 11/8 S in 4 KiB granules (144 KiB) is +7% over
+    // the 4 KiB-rounded 104 KiB (1 MiB RS(10,4) blocks: 6.14 against 5.72 TB/s).  Use powers
+    // of two for shards up to 64 KiB (padding <= 50%) and exact powers, 11/8 S between 96 and
+    // 128 KiB, and 4 KiB granules otherwise.
     if (p == S || p <= 4096) return p;
     if (S <= 65536 && p <= S + S / 2) return p;
+    if (S > 98304 && S < 131072) return round_up(S * 11 / 8, 4096);
     return round_up(S, 4096);
 }
 

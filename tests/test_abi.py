@@ -67,7 +67,9 @@ def test_shard_size(B, k):
 
 def test_recommended_pitch():
     p = rsmi.recommended_pitch
-    assert p(26215) == 32768 and p(65536) == 65536 and p(262144) == 262144 and p(104858) == 106496
+    assert p(26215) == 32768 and p(65536) == 65536 and p(262144) == 262144
+    assert p(104858) == 147456  # 11/8 S in 4 KiB granules between 96 and 128 KiB (+7% at 1 MiB blocks)
+    assert p(150000) == 151552  # 4 KiB granules above
     assert p(17) == 32 and p(1) == 16
     assert p(40000) == 40960  # next pow2 (65536) would waste > S/2
     assert p(1 << 22) == 1 << 22 and p(3000) == 4096

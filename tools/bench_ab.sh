@@ -12,7 +12,9 @@ shift
 for i in $(seq 1 "$R"); do
   for v in "$@"; do
     args=()
-    for kv in $v; do args+=(--option "$kv"); done
+    for kv in $v; do
+      case $kv in pitch=*) args+=(--pitch "${kv#pitch=}") ;; *) args+=(--option "$kv") ;; esac
+    done
     out=gpurun_out/ab_${CFG}_$(echo "${v:-default}" | tr ' =' '_-')_$i.json
     timeout -k 10 120 python bench.py --config "$CFG" --cpu-seconds 0 "${args[@]}" > "$out" 2>/dev/null || { echo "bench failed: $v"; exit 1; }
     python - "$out" "${v:-default}" <<'PY'

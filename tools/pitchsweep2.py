@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: XOR-ceiling and encode throughput vs row pitch for large shards."""
+"""Diagnostic: XOR-ceiling and encode throughput vs row pitch (full grids: one tile per wave)."""
 import ctypes
 import os
 import statistics
@@ -24,7 +24,8 @@ def run(k, m, S, nb, pitches, L, sh, rounds=3):
     V = {}
     for p in pitches:
         if (k, m) in ((10, 4), (16, 4)):
-            V[f"K{k} xor p={p}"] = (lambda p=p: L.membw_rows_launch(k, m, 1, b, b + k * p, n * p, p, n * p, S, nb, 2048, sh), enc)
+            g = (nb * ((S + 1023) // 1024) + 3) // 4  # full grid (one tile per wave), as the encode launches
+            V[f"K{k} xor p={p}"] = (lambda p=p, g=g: L.membw_rows_launch(k, m, 1, b, b + k * p, n * p, p, n * p, S, nb, g, sh), enc)
         V[f"K{k} enc p={p}"] = (lambda p=p: c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh), enc)
     times = {x: [] for x in V}
     for f, _ in V.values():
@@ -53,9 +54,9 @@ def main():
                                     ctypes.c_int, ctypes.c_void_p]
     sh = torch.cuda.current_stream().cuda_stream
     K = 1024
-    run(10, 4, 104858, 1024, [106496, 110592, 114688, 122880, 126976, 131072, 135168, 139264, 147456, 163840, 196608], L, sh)
-    run(16, 4, 262144, 256, [262144, 266240, 270336, 278528, 294912, 327680, 393216, 524288], L, sh)
-    run(10, 4, 26215, 4096, [26624, 28672, 32768, 36864, 49152, 65536], L, sh)
+    run(10, 4, 104858, 1024, [104864, 105472, 106496, 110592, 114688, 122880, 131072, 147456], L, sh)
+    run(16, 4, 262144, 256, [262144, 262400, 266240, 270336, 294912], L, sh)
+    run(10, 4, 26215, 4096, [26224, 26368, 26624, 27648, 28672, 32768, 36864], L, sh)
 
 
 if __name__ == "__main__":
