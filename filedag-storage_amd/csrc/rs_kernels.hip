@@ -64,6 +64,9 @@ constexpr int default_prefetch() {
 // (v_lshrrev_b64; the bits that cross from the high dword land in masked-off positions).
 // SP >= 0 (aligned layouts, A/B): whole output chunks leave by buffer stores with these cache
 // bits (aux: 1 = sc0, 2 = nt, 16 = sc1, 17 = sc0 sc1, 18 = nt sc1); -1 = the NT policy.
+// xcd_order (argument): XCD-grouped tile order.  The dispatcher sends workgroup b to XCD
+// b mod 8; with xcd_order set, workgroups are renumbered so that each XCD takes one
+// contiguous eighth of the tiles.
 template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
           bool UA = false, bool CRC = false, bool SH64 = false, int SP = -1>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                        uint32_t ntiles, const uint32_t* __restrict__ crc_tbl,
                                                        uint16_t* __restrict__ crc_out, uint32_t crc_slots,
-                                                       uint32_t crc_out_slot0) {
+                                                       uint32_t crc_out_slot0, uint32_t xcd_order) {
     static_assert(!CRC || (UA && D == 1), "fused chunk CRCs: unaligned-window kernels only");
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
     __shared__ uint32_t s_crc[CRC ? kCrcNWords : 1];
@@ -89,7 +92,12 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t nw = gridDim.x * kWavesPerWG;
-    uint32_t t = blockIdx.x * kWavesPerWG + wid;
+    uint32_t bid = blockIdx.x;
+    if (xcd_order) {  // bijection on [0, gridDim.x): XCD x gets the x-th contiguous share
+        const uint32_t g = gridDim.x, x = bid % 8u, q = g / 8u, r = g % 8u;
+        bid = x * q + (x < r ? x : r) + bid / 8u;
+    }
+    uint32_t t = bid * kWavesPerWG + wid;
     if (t >= ntiles) return;
 
     constexpr int P = PF == 0 ? default_prefetch<K, MT, D>() : (PF < K ? PF : K);  // rows in flight per lane

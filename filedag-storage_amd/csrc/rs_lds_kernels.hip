@@ -108,14 +108,16 @@ __device__ __forceinline__ void gf_mac_col(int c, const u32x4& x4, const u32x4 (
 
 // K inputs, MT (<= 4) outputs, NT cache policy as rs_fast_kernel (loads always nontemporal;
 // 1 = nontemporal stores, 2 = default stores), WPG waves per workgroup.  Same argument list
-// as rs_fast_kernel (the CRC arguments are unused), so the launcher treats both alike.
+// as rs_fast_kernel (the CRC and tile-order arguments are unused), so the launcher treats
+// both alike.
 template <int K, int MT, int NT, int WPG>
 __global__ __launch_bounds__(WPG * kWave) void rs_lds_kernel(const RsPlanDev* __restrict__ plan,
                                                              const uint8_t* __restrict__ in,
                                                              uint8_t* __restrict__ out, uint64_t in_bs,
                                                              uint64_t in_rs, uint64_t out_bs, uint64_t out_rs,
                                                              uint32_t S, uint32_t cpb, uint32_t tpb, uint32_t ntiles,
-                                                             const uint32_t*, uint16_t*, uint32_t, uint32_t) {
+                                                             const uint32_t*, uint16_t*, uint32_t, uint32_t,
+                                                             uint32_t) {
     static_assert(K >= 2 && K - 1 + MT < 64, "vmcnt immediates");
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
     __shared__ u32x4 s_ring[WPG][K][kWave];  // per wave: one 1 KiB slot per input row

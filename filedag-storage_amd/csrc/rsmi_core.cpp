@@ -232,8 +232,9 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 const uint32_t* ctbl = fuse ? fuse->tbl : nullptr;
                 uint16_t* cout = fuse ? fuse->out + b0 * fuse->slots * tpb * kWave : nullptr;
                 uint32_t cslots = fuse ? fuse->slots : 0, cslot0 = fuse ? fuse->out_slot0 : 0;
+                uint32_t xo = uint32_t(c->opt_xcd_order);
                 void* args[] = {&pd,    &inb,    &outb,  &in_bs, &in_rs, &out_bs, &out_rs, &S32,
-                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0};
+                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0, &xo};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
             }
@@ -244,6 +245,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             if (ts_label) c->last_kernel += ts_label == 1 ? ",TS=1" : ",SH64";
             if (lds_label) c->last_kernel += ",LDS,WPG=" + std::to_string(lds_label);
             if (sp_label >= 0) c->last_kernel += ",SP=" + std::to_string(sp_label);
+            if (c->opt_xcd_order && !lds_label) c->last_kernel += ",XO";
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -457,6 +459,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "tables")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_tables = int(value);
+    } else if (!std::strcmp(key, "xcd_order")) {
+        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_xcd_order = int(value);
     } else if (!std::strcmp(key, "buffer_stores")) {
         if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
         c->opt_buffer_stores = int(value);

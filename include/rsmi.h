@@ -250,7 +250,9 @@ same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 chunk fold: 1 = n
 (default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
 table fields into SGPRs by scalar loads instead of LDS (A/B)), "lds_dma" (1|2 = RS(10,4)
 aligned encode and 1-row reconstruct run the LDS-DMA staged kernel with 4|2 waves per
-workgroup (A/B)), "coalesce_us" / "coalesce_max"
+workgroup (A/B)), "nontemporal" 3|4 (sc1 / nt buffer stores), "store_aux" (buffer-store cache
+bits), "buffer_stores" (1: policy-1 launches use buffer stores) and "xcd_order" (1: XCD-grouped
+tile order) -- all A/B, measured in DESIGN.md section 4, "coalesce_us" / "coalesce_max"
 (rsmi_encode_block_coalesced), "small_call_bytes" (host calls moving at most this many shard
 bytes, default 2 MiB, run as one kernel that reads and writes page-locked host memory in
 place over PCIe -- pageable buffers are staged through a page-locked one by CPU copies --

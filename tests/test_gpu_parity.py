@@ -136,7 +136,7 @@ def _dev_layout(k, m, S, nblocks, pad):
                                   {"nontemporal": 2, "chunks_per_lane": 2}, {"tables": 1}, {"lds_dma": 1},
                                   {"lds_dma": 2}, {"nontemporal": 3}, {"nontemporal": 3, "chunks_per_lane": 2},
                                   {"store_aux": 18}, {"nontemporal": 4}, {"buffer_stores": 1},
-                                  {"buffer_stores": 1, "chunks_per_lane": 2}])
+                                  {"buffer_stores": 1, "chunks_per_lane": 2}, {"xcd_order": 1}])
 def test_encode_batch_dev_vs_oracle(k, m, S, nblocks, opts):
     rs, dbs, pbs = _dev_layout(k, m, S, nblocks, 256)
     host = np.zeros((nblocks, k, rs), dtype=np.uint8)
@@ -228,7 +228,7 @@ def test_unaligned_window_kernel_guards_and_reconstruct(S, offset, lost, data_on
                           (2, 1, 131072, 4, [1], False)])
 @pytest.mark.parametrize("opts", [{}, {"prefetch": 10}, {"nontemporal": 0}, {"nontemporal": 1}, {"nontemporal": 2},
                                   {"tables": 1}, {"lds_dma": 1}, {"lds_dma": 2}, {"nontemporal": 3},
-                                  {"store_aux": 17}, {"nontemporal": 4}, {"buffer_stores": 1}])
+                                  {"store_aux": 17}, {"nontemporal": 4}, {"buffer_stores": 1}, {"xcd_order": 1}])
 def test_reconstruct_batch_dev_vs_oracle(k, m, S, nblocks, lost, data_only, opts):
     n = k + m
     rs = (S + 255) // 256 * 256
