@@ -64,8 +64,9 @@ size_t rsmi_shard_size(size_t block_size, int k);
 
 /* Device row pitch for shards of S bytes that the fast kernels stream best on MI355X:
  * the next power of two for shards up to 64 KiB (when it wastes at most half a shard) and
- * for exact powers of two, otherwise S rounded up to 4 KiB (measured, DESIGN.md "Layout").
- * The host-staged entry points use it internally. */
+ * for exact powers of two, 11/8 S in 4 KiB granules for 96 KiB < S < 128 KiB (1 MiB RS(10,4)
+ * blocks), otherwise S rounded up to 4 KiB (measured, DESIGN.md "Layout").  The
+ * host-staged entry points use it internally. */
 size_t rsmi_recommended_pitch(size_t S);
 
 /* The cached (k+m) x k encode matrix, row-major. */
