@@ -219,6 +219,14 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             // shape (tools/bench_ab.sh, profiles/r01/grid_ab.txt).  waves_per_cu > 0 caps the
             // grid (A/B; the loop in the kernels strides over the remaining tiles).
             long wg_cap = std::numeric_limits<long>::max();
+            if (lds_label) {  // the LDS-DMA variant refills its ring across a wave's tiles: persistent
+                int& occ = c->occupancy[fn];
+                if (occ <= 0) {
+                    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpg * kWave, 0));
+                    if (occ <= 0) occ = 1;
+                }
+                wg_cap = long(c->num_cu) * occ;
+            }
             if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / wpg);
             // split into launches whose tile count fits 32 bits
             const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / tpb);

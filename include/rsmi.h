@@ -243,7 +243,8 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* ctx, const uint8_t* data, size_t data_
 
 /* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache
  * policy: -1 auto per output width (default), 0 default loads and stores, 1 nontemporal loads
- * and stores, 2 nontemporal loads only), "waves_per_cu" (grid cap, 0 = occupancy),
+ * and stores, 2 nontemporal loads only), "waves_per_cu" (grid cap; 0 = one tile per wave for the coding kernels, occupancy x CUs for the
+ * CRC rows kernels),
  * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: host batch calls whose buffers are page-locked
 (rsmi_host_alloc) run as one kernel that reads and writes them in place over PCIe, at any
 size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
