@@ -38,12 +38,10 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
     uint64_t nitems = nblocks * nrows * nseg;
-    int& occ = c->occupancy[fn];
-    if (occ <= 0) {
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
-        if (occ <= 0) occ = 1;
-    }
-    uint64_t cap = uint64_t(c->num_cu) * uint64_t(occ);  // persistent: the LDS tables load once per workgroup
+    // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
+    // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
+    // +3 % over occupancy x CUs, -25 % at one item per wave)
+    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
@@ -79,12 +77,10 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
     uint64_t nitems = nblocks * nrows * nseg;
-    int& occ = c->occupancy[fn];
-    if (occ <= 0) {
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kWG, 0));
-        if (occ <= 0) occ = 1;
-    }
-    uint64_t cap = uint64_t(c->num_cu) * uint64_t(occ);  // persistent: the LDS tables load once per workgroup
+    // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
+    // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
+    // +3 % over occupancy x CUs, -25 % at one item per wave)
+    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;

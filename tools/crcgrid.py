@@ -21,7 +21,7 @@ def main():
     out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
     V = {}
     ref = {}
-    for wpc in (0, 32, 64, 128, 1000000):
+    for wpc in (0, 96, 128, 192, 256, 384):
         c = rsmi.Codec(k, m)
         c.set_option("waves_per_cu", wpc)
         for kind in ("crc16", "crc32"):
