@@ -25,6 +25,9 @@ def main():
     L.membw_half_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.c_void_p]
+    L.membw_pol_launch.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
     st = torch.cuda.current_stream()
     sh = st.cuda_stream
     k, m, n, nb, S, p = 10, 4, 14, 4096, 26215, 32768
@@ -46,6 +49,12 @@ def main():
                                           nb * k * S)
         V[f"writes alone 4w grid={g}"] = (lambda g=g: L.membw_half_launch(1, 0, 4, b, b + k * p, n * p, p, n * p, S, nb,
                                                                           g, sh), nb * m * S)
+    g = (tiles + 3) // 4
+    # the reconstruct's pattern: 10 rows read (nt), 1 row written (plain stores, the bench's policy)
+    V[f"rows 10r->1w ntl plain-st grid={g}"] = (lambda: L.membw_pol_launch(10, 1, 1, 0, b + p, b, n * p, p, n * p, S, nb, g,
+                                                                          sh), nb * (k + 1) * S)
+    V["rows 10r->1w ntl plain-st grid=1024"] = (lambda: L.membw_pol_launch(10, 1, 1, 0, b + p, b, n * p, p, n * p, S, nb,
+                                                                           1024, sh), nb * (k + 1) * S)
     for f, _ in V.values():
         f()
     torch.cuda.synchronize()
