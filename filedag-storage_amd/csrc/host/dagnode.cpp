@@ -699,14 +699,30 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         for (size_t j = 0; j < nb; j++)
             for (int i = 0; i < n; i++)
                 if (present[i]) std::memcpy(flat + (j * n + i) * S, pend[j].shards[i].data(), S);
-        rc = rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), required.data());
+        // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
+        DataNodeClient& target = *nodes_[to].client;
+        const bool want32 = gpu_checksums_ && target.WantsValueChecksum();
+        std::vector<uint32_t> r16(gpu_checksums_ ? nb * size_t(n) : 0), r32(want32 ? nb * size_t(n) : 0);
+        rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, nb, present.data(),
+                                                                    required.data(), r16.data(),
+                                                                    want32 ? r32.data() : nullptr)
+                            : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(),
+                                                               required.data());
         if (rc) return rsmi_status(rc);
         const Bytes meta = encode_meta(size);
         // the rebuilt rows go to the target concurrently; outcomes are taken in key order
         std::vector<Status> ps(nb);
         fan_keys(int(nb), [&](int j) {
             const uint8_t* row = flat + (size_t(j) * n + size_t(to)) * S;
-            ps[j] = nodes_[to].client->Put(pend[j].key, meta, Bytes(row, row + S));
+            const Bytes shard(row, row + S);
+            if (!gpu_checksums_) {
+                ps[j] = target.Put(pend[j].key, meta, shard);
+                return;
+            }
+            const uint16_t c16 = entry_checksum(meta, S, r16[size_t(j) * n + size_t(to)]);
+            ps[j] = want32 ? target.PutWithChecksums(pend[j].key, meta, shard, c16,
+                                                     value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
+                           : target.PutWithChecksum(pend[j].key, meta, shard, c16);
         });
         for (size_t j = 0; j < nb; j++) {
             if (!ps[j].ok()) return ps[j];

@@ -89,6 +89,22 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     return RSMI_OK;
 }
 
+int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint64_t S,
+                        uint64_t nblocks, const uint8_t* present, const uint8_t* want, uint32_t* d16, uint32_t* d32,
+                        hipStream_t stream) {
+    const uint64_t n = uint64_t(c->n);
+    if (d16) HIP_TRY(hipMemsetAsync(d16, 0, nblocks * n * 4, stream));
+    if (d32) HIP_TRY(hipMemsetAsync(d32, 0, nblocks * n * 4, stream));
+    int rc;
+    for (uint64_t r = 0; r < n; r++) {
+        if (present[r] || !want[r]) continue;
+        const uint8_t* row = base + r * rpitch;
+        if (d16 && (rc = launch_crc(c, row, rpitch, bstride, 1, S, nblocks, d16 + r, n, stream, false))) return rc;
+        if (d32 && (rc = launch_crc32(c, row, rpitch, bstride, 1, S, nblocks, d32 + r, n, stream))) return rc;
+    }
+    return RSMI_OK;
+}
+
 // Encode with fused per-chunk CRCs, then R(row) of all k+m rows of every block into
 // raw[b * (k+m) + row] (device or page-locked host memory).  Needs S >= 16 and k <= 16.
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,

@@ -264,7 +264,7 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
 // read and rebuilt where they lie; pageable ones are staged (survivor rows in, rebuilt rows
 // back).  Caller holds ctx->mu.
 int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
-                             const uint8_t* present, const uint8_t* want) {
+                             const uint8_t* present, const uint8_t* want, uint32_t* raw16, uint32_t* raw32) {
     const size_t n = size_t(c->n);
     hipStream_t st = c->staging[0].stream;
     uint8_t* dev = host_alias(shards, (nblocks - 1) * bs + n * S);
@@ -282,7 +282,16 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
     }
     int rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
     if (rc) return rc;
+    const size_t raw_sz = nblocks * n * 4;
+    if (raw16 && (rc = reserve(c->d_crc, c->crc_cap, raw_sz))) return rc;
+    if (raw32 && (rc = reserve(c->d_crc32, c->crc32_cap, raw_sz))) return rc;
+    uint32_t* d16 = raw16 ? reinterpret_cast<uint32_t*>(c->d_crc) : nullptr;
+    uint32_t* d32 = raw32 ? reinterpret_cast<uint32_t*>(c->d_crc32) : nullptr;
+    if ((raw16 || raw32) && (rc = launch_rebuilt_crcs(c, dev, S, dbs, S, nblocks, present, want, d16, d32, st)))
+        return rc;
     HIP_TRY(hipStreamSynchronize(st));
+    if (raw16) HIP_TRY(hipMemcpy(raw16, d16, raw_sz, hipMemcpyDeviceToHost));
+    if (raw32) HIP_TRY(hipMemcpy(raw32, d32, raw_sz, hipMemcpyDeviceToHost));
     if (hs)
         for (size_t b = 0; b < nblocks; b++)
             for (size_t i = 0; i < n; i++)
@@ -291,7 +300,7 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
 }
 
 int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                 const uint8_t* present, const uint8_t* want) {
+                                 const uint8_t* present, const uint8_t* want, uint32_t* raw16, uint32_t* raw32) {
     if (!c || !shards || !present || !want) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (block_stride < size_t(c->n) * S) return RSMI_ERR_INVALID_ARG;
@@ -309,7 +318,7 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
     // pipeline) or the call is small (see encode_host_impl)
     if ((c->opt_zero_copy && host_alias(shards, (nblocks - 1) * block_stride + size_t(c->n) * S)) ||
         nblocks * size_t(c->n) * S <= size_t(c->opt_small_bytes))
-        return reconstruct_small(c, *plan, shards, block_stride, S, nblocks, present, want);
+        return reconstruct_small(c, *plan, shards, block_stride, S, nblocks, present, want, raw16, raw32);
     // rows to ship: the k survivors in; the missing rows the plan writes, out
     std::vector<int> in_rows, out_rows;
     for (int i = 0; i < c->n && int(in_rows.size()) < c->k; i++)
@@ -340,6 +349,8 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
             c->h_stage_cap = need;
         }
     }
+    if (raw16 && (rc = reserve(c->d_crc, c->crc_cap, nblocks * n * 4))) return rc;
+    if (raw32 && (rc = reserve(c->d_crc32, c->crc32_cap, nblocks * n * 4))) return rc;
     for (size_t b0 = 0, i = 0; b0 < nblocks; b0 += chunk, i++) {
         Staging& st = c->staging[i % ns];
         const size_t nb = std::min(chunk, nblocks - b0);
@@ -366,6 +377,11 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
             if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * n, st.stream))) return rc;
         }
         if ((rc = launch_plan(c, *plan, st.d_in, Sp, bs, st.d_in, Sp, bs, S, nb, st.stream))) return rc;
+        if ((raw16 || raw32) &&
+            (rc = launch_rebuilt_crcs(c, st.d_in, Sp, bs, S, nb, present, want,
+                                      raw16 ? reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n : nullptr,
+                                      raw32 ? reinterpret_cast<uint32_t*>(c->d_crc32) + b0 * n : nullptr, st.stream)))
+            return rc;
         if (zc) {
             for (int r : out_rows)
                 if ((rc = repitch(zc + b0 * block_stride + size_t(r) * S, block_stride, st.d_in + size_t(r) * Sp, bs, S,
@@ -386,6 +402,8 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
         }
     }
     for (int s = 0; s < ns; s++) HIP_TRY(hipStreamSynchronize(c->staging[s].stream));
+    if (raw16) HIP_TRY(hipMemcpy(raw16, c->d_crc, nblocks * n * 4, hipMemcpyDeviceToHost));
+    if (raw32) HIP_TRY(hipMemcpy(raw32, c->d_crc32, nblocks * n * 4, hipMemcpyDeviceToHost));
     if (!d2 && !zc) {
         for (size_t b0 = 0; b0 < nblocks; b0 += chunk) {
             const size_t nb = std::min(chunk, nblocks - b0);
@@ -465,6 +483,15 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_strid
 int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                      const uint8_t* present, const uint8_t* required) {
     return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required);
+}
+
+int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S,
+                                          size_t nblocks, const uint8_t* present, const uint8_t* required,
+                                          uint32_t* raw16_out, uint32_t* raw32_out) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (raw16_out) std::memset(raw16_out, 0, nblocks * size_t(c->n) * 4);
+    if (raw32_out) std::memset(raw32_out, 0, nblocks * size_t(c->n) * 4);
+    return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required, raw16_out, raw32_out);
 }
 
 }  // extern "C"

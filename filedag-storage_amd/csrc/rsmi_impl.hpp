@@ -167,11 +167,19 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
 int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                             size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out = nullptr);
 int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
-                             const uint8_t* present, const uint8_t* want);
+                             const uint8_t* present, const uint8_t* want, uint32_t* raw16 = nullptr,
+                      uint32_t* raw32 = nullptr);
 int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                 const uint8_t* present, const uint8_t* want);
+                                 const uint8_t* present, const uint8_t* want, uint32_t* raw16 = nullptr,
+                          uint32_t* raw32 = nullptr);
 int ensure_crc_tables(rsmi_ctx* c);
 int ensure_crc32_tables(rsmi_ctx* c);
+// R(row) / R32(row) of the rows the plan rebuilt (want && !present), one row per block at
+// base + b*bstride + r*rpitch, into the device buffers d16 / d32 at [b*n + r] (either may be
+// null; zeroed here), stream-ordered
+int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint64_t S,
+                        uint64_t nblocks, const uint8_t* present, const uint8_t* want, uint32_t* d16, uint32_t* d32,
+                        hipStream_t stream);
 int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
                  uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream);
 int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,

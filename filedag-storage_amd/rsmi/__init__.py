@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
                                                ctypes.c_void_p, c_size, ctypes.c_void_p]),
         "rsmi_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
                                                        ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_reconstruct_rows_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+                                                                 u8p, ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
@@ -264,6 +266,15 @@ class Codec:
         """R32(row) of the mutcask value checksum (CRC-32 IEEE, raw) for every row, on the device."""
         _check(lib().rsmi_crc32_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
                                          stream or None))
+
+    def reconstruct_rows_batch_host_crcs_ptr(self, shards_ptr: int, block_stride: int, S: int, nblocks: int,
+                                             present: Sequence[bool], required: Sequence[bool],
+                                             raw16_ptr: Optional[int], raw32_ptr: Optional[int]) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        q = bytearray(1 if x else 0 for x in required)
+        _check(lib().rsmi_reconstruct_rows_batch_host_crcs(self._h, shards_ptr, block_stride, S, nblocks,
+                                                           ctypes.addressof(_buf(p)), ctypes.addressof(_buf(q)),
+                                                           raw16_ptr or None, raw32_ptr or None))
 
     def encode_batch_host_crcs_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
                                    nblocks: int, raw16_ptr: Optional[int], raw32_ptr: Optional[int]) -> None:

@@ -239,6 +239,15 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* ctx, const uint8_t* data, size_t data_
                                 size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
                                 uint32_t* raw32_out);
 
+/* rsmi_reconstruct_rows_batch_host plus the raw checksums of every row it rebuilt, from the
+ * GPU where the rows land: raw16_out / raw32_out[b*(k+m) + r] = R(row) / R32(row) for rows r
+ * that are required and missing, 0 for the others; either may be NULL.  RepairDataNode's
+ * Puts of the rebuilt rows (data_recovery.go:102-106) then carry sender checksums like
+ * DagNode.Put's. */
+int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S,
+                                          size_t nblocks, const uint8_t* present, const uint8_t* required,
+                                          uint32_t* raw16_out, uint32_t* raw32_out);
+
 /* ------------------------------------------------------------------ tuning / introspection */
 
 /* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache

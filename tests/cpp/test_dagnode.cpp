@@ -586,6 +586,19 @@ static void test_gpu_value_checksums() {
             CHECK_OK(gpu.node->Get(keys[j], &got));
             CHECK(got == blocks[j]);
         }
+        // RepairDataNodeBatched onto a wiped mutcask node: the rebuilt rows carry both
+        // checksums from the GPU (rsmi_reconstruct_rows_batch_host_crcs); every stored value
+        // is byte-identical to the one written by the original Put
+        std::vector<Bytes> before(keys.size());
+        for (size_t j = 0; j < keys.size(); j++) CHECK(gpu.dn[1]->server().RawValue(keys[j], &before[j]));
+        gpu.dn[1]->server().Wipe();
+        size_t repaired = 0;
+        CHECK_OK(gpu.node->RepairDataNodeBatched(0, 1, 8, &repaired));
+        CHECK(repaired == keys.size());
+        for (size_t j = 0; j < keys.size(); j++) {
+            Bytes v;
+            CHECK(gpu.dn[1]->server().RawValue(keys[j], &v) && v == before[j]);
+        }
         // a rotted value on one datanode: the read treats that shard as missing and
         // reconstructs from the others (node.go:254-258), then read-repair rewrites it
         gpu.dn[0]->server().CorruptByte(keys.back(), kHeaderSize + 4 + 1);
