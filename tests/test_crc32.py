@@ -164,3 +164,35 @@ def test_encode_batch_host_crcs_entries(k, m, B, small, want16, pinned):
             assert rsmi.crc32_entry(h32, int(raw32v[b, i]), S) == orc.mutcask_entry_crc(c16, meta, row), (b, i)
     for p in ptrs:
         rsmi.lib().rsmi_host_free(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,S,nb,lost,required", [(10, 4, 26215, 24, [3], [3]), (10, 4, 26215, 9, [0, 12], [12]),
+                                                    (4, 2, 65536, 33, [1, 5], [1, 5]), (16, 4, 4097, 5, [9], [9])])
+@pytest.mark.parametrize("small", [0, 1 << 30])
+def test_reconstruct_rows_crcs(k, m, S, nb, lost, required, small):
+    """rsmi_reconstruct_rows_batch_host_crcs: the rebuilt rows equal the oracle's, and their raw
+    CRC-16 / CRC-32 equal the checksums of those rows; rows not rebuilt report 0."""
+    n = k + m
+    r = np.random.default_rng(S + nb)
+    data = r.integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+    full = np.concatenate([data, orc.encode_fast(k, m, data)], axis=1)
+    shards = full.copy()
+    shards[:, lost, :] = 0
+    present = [i not in lost for i in range(n)]
+    req = [i in required for i in range(n)]
+    r16 = np.full((nb, n), 0xDEAD, dtype=np.uint32)
+    r32 = np.full((nb, n), 0xDEAD, dtype=np.uint32)
+    with rsmi.Codec(k, m) as c:
+        c.set_option("small_call_bytes", small)
+        c.reconstruct_rows_batch_host_crcs_ptr(shards.ctypes.data, n * S, S, nb, present, req, r16.ctypes.data,
+                                               r32.ctypes.data)
+    for b in range(nb):
+        for i in range(n):
+            if i in required:
+                row = full[b, i].tobytes()
+                assert np.array_equal(shards[b, i], full[b, i]), (b, i)
+                assert rsmi.crc16_entry(b"", int(r16[b, i]), S) == orc.crc16_ibm(row), (b, i)
+                assert int(r32[b, i]) == raw32(row), (b, i)
+            else:
+                assert r16[b, i] == 0 and r32[b, i] == 0, (b, i)
