@@ -384,8 +384,9 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
     // it.  Fetches run concurrently in waves: when node i is reached unfetched, the next
     // (successes still needed) online nodes are fetched at once.  A fetch the replay never
     // reaches (the quorum was decided first) is a cancelled goroutine: dropped, no repair.
-    std::vector<Bytes> data(static_cast<size_t>(n));
+    std::vector<Bytes> data(static_cast<size_t>(n)), metas(static_cast<size_t>(n));
     std::vector<Status> got(static_cast<size_t>(n));
+    std::vector<DataNodeClient::Stored> stored(static_cast<size_t>(n));
     std::vector<char> fetched(static_cast<size_t>(n), 0);
     int succ = 0;
     for (int i = 0; i < n; i++) {
@@ -401,9 +402,11 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
             for (int j = i; j < n && int(wave.size()) < std::max(1, rq - succ); j++)
                 if (online[j] && !fetched[j]) wave.push_back(j);
             fan(int(wave.size()), [&](int t) {
-                Bytes m;
-                got[wave[t]] = online[wave[t]]->client->Get(key, &m, &data[wave[t]]);
+                const int j = wave[t];
+                got[j] = gpu_verified_reads_ ? online[j]->client->GetForVerify(key, &metas[j], &data[j], &stored[j])
+                                             : online[j]->client->Get(key, &metas[j], &data[j]);
             }, size_t(ceil_frac(f->meta.block_size, config_.data_blocks)));
+            if (gpu_verified_reads_) verify_wave(wave, metas, data, stored, got);
             for (int j : wave) fetched[j] = 1;
         }
         if (!got[i].ok()) {
@@ -416,6 +419,43 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
     }
     std::sort(f->repair.begin(), f->repair.end());
     return w.result(kErrReadQuorum);
+}
+
+void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas,
+                          const std::vector<Bytes>& data, const std::vector<DataNodeClient::Stored>& stored,
+                          std::vector<Status>& got) {
+    // shards to check, grouped by size (one GPU call per size; a block's shards share one)
+    std::map<size_t, std::vector<int>> by_size;
+    for (int j : wave)
+        if (got[j].ok() && !stored[j].verified) by_size[data[j].size()].push_back(j);
+    for (auto& g : by_size) {
+        const size_t S = g.first, w = g.second.size();
+        bool want32 = false;
+        for (int j : g.second) want32 |= stored[j].has_value_crc;
+        std::vector<uint32_t> r16(w, 0), r32(w, 0);
+        int rc = RSMI_OK;
+        if (S > 0) {
+            rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+            uint8_t* flat = ctx ? thread_staging().reserve(w * S) : nullptr;
+            if (ctx && !flat) rc = RSMI_ERR_DEVICE;
+            if (flat) {
+                for (size_t i = 0; i < w; i++) std::memcpy(flat + i * S, data[g.second[i]].data(), S);
+                rc = rsmi_crc_rows_host(ctx, flat, S, w, S, r16.data(), want32 ? r32.data() : nullptr);
+            }
+        }
+        for (size_t i = 0; i < w; i++) {
+            const int j = g.second[i];
+            if (rc) {  // no device: the read fails loudly (there is no CPU path)
+                got[j] = rsmi_status(rc);
+                continue;
+            }
+            // the mutcask engine checks its value first (cask.go:250), then the datanode its entry
+            if (stored[j].has_value_crc && value_checksum(metas[j], S, stored[j].crc, r32[i]) != stored[j].value_crc)
+                got[j] = Status::Error("mutcask: data may be rotted");
+            else if (entry_checksum(metas[j], S, r16[i]) != stored[j].crc)
+                got[j] = Status::Error("checking crc failed");
+        }
+    }
 }
 
 Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  // node.go:277-326
@@ -614,8 +654,9 @@ Status DagNode::fetch_for_repair(const std::string& key, int repair_index, std::
     shards->assign(size_t(n), Bytes());
     QuorumWait w(rq, n - rq + 1);
     // waves of concurrent fetches replayed in node order, as in fetch_for_get
-    std::vector<Bytes> data(static_cast<size_t>(n));
+    std::vector<Bytes> data(static_cast<size_t>(n)), metas(static_cast<size_t>(n));
     std::vector<Status> got(static_cast<size_t>(n));
+    std::vector<DataNodeClient::Stored> stored(static_cast<size_t>(n));
     std::vector<char> fetched(static_cast<size_t>(n), 0);
     int succ = 0;
     for (int i = 0; i < n && !w.decided(); i++) {

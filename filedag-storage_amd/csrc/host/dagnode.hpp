@@ -107,6 +107,12 @@ public:
     // instead of leaving the byte-serial CRC to the datanode.  On by
     // default; the stored entries are byte-identical either way.
     void SetGpuChecksums(bool v) { gpu_checksums_ = v; }
+    // Get / GetMany read shards with DataNodeClient::GetForVerify and check the stored entry
+    // (and mutcask value) checksums on the GPU, one call per fetch wave, instead of each
+    // datanode checking its own (server.go:93-97, cask.go:250).  A shard that fails is
+    // treated exactly like a failed fetch: missing, on the repair list, the next node
+    // fetched.  Off by default (it needs the datanode RPC that skips the check).
+    void SetGpuVerifiedReads(bool v) { gpu_verified_reads_ = v; }
     // The k+m datanode calls of one block run concurrently, like node.go's goroutine per
     // datanode (fanout.hpp); results are replayed in node order, so every quorum outcome,
     // repair list and error equals the sequential one.  On by default.
@@ -143,6 +149,10 @@ private:
     int num_slots_ = 0;
     int device_ = 0;
     bool gpu_checksums_ = true;
+    bool gpu_verified_reads_ = false;
+    // GPU check of the unverified shards of one fetch wave; failures become errors in got[]
+    void verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas, const std::vector<Bytes>& data,
+                     const std::vector<DataNodeClient::Stored>& stored, std::vector<Status>& got);
     bool parallel_ = true;
     size_t fanout_min_ = size_t(128) << 10;
     std::atomic<int> active_{0};          // caller threads inside the public calls

@@ -151,6 +151,27 @@ Status DataNodeServer::Get(const std::string& key, Bytes* meta, Bytes* data) {
     return unpack(v->data() + prefix(), v->size() - prefix(), meta, data);
 }
 
+Status DataNodeServer::GetUnverified(const std::string& key, Bytes* meta, Bytes* data, DataNodeClient::Stored* st) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = kv_.find(key);
+    if (it == kv_.end()) return not_found();
+    const Bytes& v = it->second;
+    const size_t pre = prefix();
+    if (v.size() < pre + size_t(kHeaderSize)) return Status::Error("unexpected EOF");
+    const uint8_t* e = v.data() + pre;
+    const size_t n = v.size() - pre;
+    const uint32_t msz = get_le32(e + 4), dsz = get_le32(e + 8);
+    if (size_t(kHeaderSize) + msz + dsz > n) return Status::Error("unexpected EOF");
+    *st = DataNodeClient::Stored{};
+    st->crc = uint16_t(get_le32(e));
+    st->has_value_crc = pre != 0;
+    st->value_crc = pre ? get_le32(v.data()) : 0;
+    st->verified = false;
+    if (meta) meta->assign(e + kHeaderSize, e + kHeaderSize + msz);
+    if (data) data->assign(e + kHeaderSize + msz, e + kHeaderSize + msz + dsz);
+    return Status::Ok();
+}
+
 Status DataNodeServer::GetMeta(const std::string& key, Bytes* meta) {
     std::lock_guard<std::mutex> g(mu_);
     const Bytes* v = nullptr;
@@ -222,6 +243,9 @@ Status InProcDataNode::PutWithChecksums(const std::string& key, const Bytes& met
 }
 Status InProcDataNode::Get(const std::string& key, Bytes* meta, Bytes* data) {
     return offline_ ? down() : server_.Get(key, meta, data);
+}
+Status InProcDataNode::GetForVerify(const std::string& key, Bytes* meta, Bytes* data, Stored* st) {
+    return offline_ ? down() : server_.GetUnverified(key, meta, data, st);
 }
 Status InProcDataNode::GetMeta(const std::string& key, Bytes* meta) {
     return offline_ ? down() : server_.GetMeta(key, meta);

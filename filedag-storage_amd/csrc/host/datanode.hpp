@@ -63,6 +63,20 @@ public:
         return PutWithChecksum(key, meta, data, crc);
     }
     virtual bool WantsValueChecksum() const { return false; }
+    // A Get whose checksum check the caller makes (GPU-verified reads): the shard plus the
+    // checksums stored with it, unchecked (*verified = false); value_crc is the mutcask value
+    // checksum when *has_value_crc.  A datanode without this RPC runs its verified Get
+    // (*verified = true), which is what this default does.
+    struct Stored {
+        uint16_t crc = 0;
+        uint32_t value_crc = 0;
+        bool has_value_crc = false;
+        bool verified = true;
+    };
+    virtual Status GetForVerify(const std::string& key, Bytes* meta, Bytes* data, Stored* st) {
+        *st = Stored{};
+        return Get(key, meta, data);
+    }
     virtual Status Get(const std::string& key, Bytes* meta, Bytes* data) = 0;
     virtual Status GetMeta(const std::string& key, Bytes* meta) = 0;
     virtual Status Delete(const std::string& key) = 0;
@@ -85,6 +99,8 @@ public:
     Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
                             uint32_t value_crc);
     Status Get(const std::string& key, Bytes* meta, Bytes* data);
+    // the entry's parts and stored checksums without checking either (the reader verifies)
+    Status GetUnverified(const std::string& key, Bytes* meta, Bytes* data, DataNodeClient::Stored* st);
     Status GetMeta(const std::string& key, Bytes* meta);
     Status Delete(const std::string& key);
     Status Size(const std::string& key, int64_t* size);
@@ -117,6 +133,7 @@ public:
                             uint32_t value_crc) override;
     bool WantsValueChecksum() const override { return server_.engine() == KvEngine::Mutcask; }
     Status Get(const std::string& key, Bytes* meta, Bytes* data) override;
+    Status GetForVerify(const std::string& key, Bytes* meta, Bytes* data, Stored* st) override;
     Status GetMeta(const std::string& key, Bytes* meta) override;
     Status Delete(const std::string& key) override;
     Status Size(const std::string& key, int64_t* size) override;

@@ -198,6 +198,43 @@ int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     return hip_status(hipGetLastError());
 }
 
+int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size_t nrows, size_t S,
+                       uint32_t* raw16_out, uint32_t* raw32_out) {
+    if (!c || !rows || (!raw16_out && !raw32_out) || (nrows > 1 && row_stride < S)) return RSMI_ERR_INVALID_ARG;
+    if (nrows == 0) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_device(c);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = c->staging[0].stream;
+    // page-locked rows are read in place over PCIe; pageable ones through the small-call staging
+    const uint8_t* dev = host_alias(const_cast<uint8_t*>(rows), (nrows - 1) * row_stride + S);
+    size_t stride = row_stride;
+    if (!dev) {
+        uint8_t* hs = small_stage(c, nrows * S);
+        if (!hs) return RSMI_ERR_DEVICE;
+        for (size_t r = 0; r < nrows; r++) std::memcpy(hs + r * S, rows + r * row_stride, S);
+        dev = host_alias(hs, nrows * S);
+        stride = S;
+        if (!dev) return RSMI_ERR_DEVICE;
+    }
+    const size_t sz = nrows * 4;
+    if (raw16_out) {
+        if ((rc = reserve(c->d_crc, c->crc_cap, sz))) return rc;
+        if ((rc = launch_crc(c, dev, stride, stride, 1, S, nrows, reinterpret_cast<uint32_t*>(c->d_crc), 1, st))) return rc;
+    }
+    if (raw32_out) {
+        if ((rc = reserve(c->d_crc32, c->crc32_cap, sz))) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_crc32, 0, sz, st));
+        if ((rc = launch_crc32(c, dev, stride, stride, 1, S, nrows, reinterpret_cast<uint32_t*>(c->d_crc32), 1, st)))
+            return rc;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (raw16_out) HIP_TRY(hipMemcpy(raw16_out, c->d_crc, sz, hipMemcpyDeviceToHost));
+    if (raw32_out) HIP_TRY(hipMemcpy(raw32_out, c->d_crc32, sz, hipMemcpyDeviceToHost));
+    return RSMI_OK;
+}
+
 uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
 
 uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n) { return crc32_checksum(p, n); }

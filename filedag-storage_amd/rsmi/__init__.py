@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_encode_block_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
         "rsmi_encode_batch_dev_crc": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size,
                                                      c_size, ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_crc_rows_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
         "rsmi_crc32_ieee": (ctypes.c_uint32, [u8p, c_size]),
         "rsmi_crc32_entry": (ctypes.c_uint32, [u8p, c_size, ctypes.c_uint32, c_size]),
         "rsmi_crc32_rows_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, ctypes.c_int, c_size, c_size,
@@ -260,6 +262,11 @@ class Codec:
                        out_bs: int, stream: int = 0) -> None:
         _check(lib().rsmi_crc16_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
                                          stream or None))
+
+    def crc_rows_host_ptr(self, rows_ptr: int, row_stride: int, nrows: int, S: int, raw16_ptr: Optional[int],
+                          raw32_ptr: Optional[int]) -> None:
+        _check(lib().rsmi_crc_rows_host(self._h, rows_ptr, row_stride, nrows, S, raw16_ptr or None,
+                                        raw32_ptr or None))
 
     def crc32_rows_dev(self, d_rows: int, rs: int, bs: int, nrows: int, S: int, nblocks: int, d_out: int,
                        out_bs: int, stream: int = 0) -> None:

@@ -208,6 +208,13 @@ int rsmi_encode_batch_dev_crc(rsmi_ctx* ctx, const uint8_t* d_data, size_t data_
 /* rsmi_encode_block plus raw_out[r] = R(shard r), r < k+m. */
 int rsmi_encode_block_crc(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out);
 
+/* R(row) (raw16_out) and/or R32(row) (raw32_out, mutcask CRC-32) of nrows host rows of S bytes,
+ * row r at rows + r*row_stride; page-locked rows (rsmi_host_alloc) are read in place over
+ * PCIe.  The Dag Node's GPU-verified reads check fetched shards against the checksums the
+ * datanodes stored (server.go:93-97 moved to the reader); either output may be NULL. */
+int rsmi_crc_rows_host(rsmi_ctx* ctx, const uint8_t* rows, size_t row_stride, size_t nrows, size_t S,
+                       uint32_t* raw16_out, uint32_t* raw32_out);
+
 /* ------------------------------------------------------------------ mutcask CRC-32 */
 
 /* The mutcask KV engine under a datanode (kv/mutcask/cask.go:73-97, selected by

@@ -608,6 +608,72 @@ static void test_gpu_value_checksums() {
     }
 }
 
+// GPU-verified reads (SetGpuVerifiedReads): datanodes return shards with their stored
+// checksums unchecked and the DagNode checks every fetch wave on the GPU.  A node that delivers
+// a flipped byte (corrupted in transit: its GetMeta still passes) is caught there, treated as a
+// failed fetch, and the block still comes back intact from the other shards, with the node on
+// the read-repair list -- over badger and mutcask datanodes, for Get and GetMany.
+struct FlippingNode : InProcDataNode {
+    using InProcDataNode::InProcDataNode;
+    bool flip = false;
+    Status GetForVerify(const std::string& key, Bytes* meta, Bytes* data, Stored* st) override {
+        Status s = InProcDataNode::GetForVerify(key, meta, data, st);
+        if (s.ok() && flip && !data->empty()) (*data)[data->size() / 2] ^= 0x01;
+        return s;
+    }
+};
+
+static void test_gpu_verified_reads() {
+    for (KvEngine engine : {KvEngine::Badger, KvEngine::Mutcask}) {
+        const int k = 10, m = 4;
+        DagNodeConfig cfg;
+        cfg.name = "verify";
+        cfg.data_blocks = k;
+        cfg.parity_blocks = m;
+        std::vector<std::shared_ptr<FlippingNode>> dn;
+        std::vector<std::shared_ptr<DataNodeClient>> clients;
+        for (int i = 0; i < k + m; i++) {
+            cfg.nodes.push_back("127.0.0.1:" + std::to_string(9111 + i));
+            dn.push_back(std::make_shared<FlippingNode>(cfg.nodes.back(), engine));
+            clients.push_back(dn.back());
+        }
+        std::unique_ptr<DagNode> node;
+        CHECK_OK(DagNode::New(cfg, clients, &node));
+        node->HealthCheckAll();
+        node->SetGpuVerifiedReads(true);
+        std::mt19937_64 r(21);
+        std::vector<std::string> keys;
+        std::vector<Bytes> blocks;
+        for (size_t sz : {size_t(6), size_t(4099), size_t(262144), size_t(1048590)}) {
+            keys.push_back("v-" + std::to_string(sz));
+            blocks.push_back(rand_bytes(r, sz));
+            CHECK_OK(node->Put(keys.back(), blocks.back()));
+        }
+        for (size_t j = 0; j < keys.size(); j++) {
+            Bytes got;
+            CHECK_OK(node->Get(keys[j], &got));
+            CHECK(got == blocks[j]);
+        }
+        CHECK(node->RepairQueueLen() == 0);
+        dn[1]->flip = true;  // data shard 1 arrives corrupted
+        for (size_t j = 0; j < keys.size(); j++) {
+            Bytes got;
+            CHECK_OK(node->Get(keys[j], &got));
+            CHECK(got == blocks[j]);
+        }
+        CHECK(node->RepairQueueLen() == keys.size());
+        std::vector<Bytes> gm;
+        std::vector<Status> st;
+        node->GetMany(keys, &gm, &st, 8);
+        for (size_t j = 0; j < keys.size(); j++) {
+            CHECK_OK(st[j]);
+            CHECK(gm[j] == blocks[j]);
+        }
+        dn[1]->flip = false;
+        node->Close();
+    }
+}
+
 // Concurrent DagNode.Put from many threads (the reference's goroutine-per-request Dag Pool):
 // the per-block encodes coalesce into GPU batches (rsmi_encode_block_coalesced), and every
 // stored shard and entry checksum still equals the oracle's.
@@ -696,6 +762,7 @@ int main(int argc, char** argv) {
         test_migrate();
         test_gpu_entry_checksums();
         test_gpu_value_checksums();
+        test_gpu_verified_reads();
         test_concurrent_puts();
     }
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);

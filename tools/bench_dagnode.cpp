@@ -119,6 +119,15 @@ int main(int argc, char** argv) {
     const double getT = secs(t0);
     const long gcalls = ctx ? rsmi_get_stat(ctx, "coalesced_calls") - gc0 : 0;
     const long gbatches = ctx ? rsmi_get_stat(ctx, "coalesced_batches") - gb0 : 0;
+    // the same degraded reads with the checksums checked on the GPU instead of by each datanode
+    d->SetGpuVerifiedReads(true);
+    t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Get(keys[i], &got);
+    const double get1v = secs(t0);
+    t0 = clk::now();
+    d->GetMany(keys, &gm, &st, best_batch);
+    const double getbv = secs(t0);
+    d->SetGpuVerifiedReads(false);
     dn[0]->SetOffline(false);
     d->RunRepairTasks();
     dn[3]->server().Wipe();
@@ -169,6 +178,7 @@ int main(int argc, char** argv) {
                 batches);
     std::printf("Get, 1 lost shard  %8.2f GiB/s\nGetMany (batched)  %8.2f GiB/s (batch %zu)\n", gib / get1, gib / getb,
                 best_batch);
+    std::printf("Get / GetMany, GPU-verified reads %6.2f / %.2f GiB/s\n", gib / get1v, gib / getbv);
     std::printf("Get, %d threads    %8.2f GiB/s (%ld reconstructs in %ld coalesced GPU batches)\n", T, gib / getT,
                 gcalls, gbatches);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
