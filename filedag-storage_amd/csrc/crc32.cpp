@@ -79,12 +79,14 @@ Crc32Tables::Crc32Tables() {
     for (int i = 1; i < kCrc32Powers; i++) square(P[i - 1], P[i]);
     slice(inv, Q[0]);
     for (int i = 1; i < kCrc32InvPowers; i++) square(Q[i - 1], Q[i]);
-    for (int i = 0; i < kCrc32Powers; i++)
+    for (int t = 0; t < kCrc32SegTiles; t++)
+        for (int q = 0; q < 32; q++)
+            for (int v = 0; v < 16; v++) NT[t][q][v] = shift(N[q][v], uint64_t(1024) * (kCrc32SegTiles - 1 - t));
+    for (int j = 0; j < kCrc32ScanPowers; j++)
         for (int h = 0; h < 8; h++)
-            for (int v = 0; v < 16; v++) PN[i][h][v] = apply(P[i], uint32_t(v) << (4 * h));
-    for (int i = 0; i < kCrc32InvPowers; i++)
-        for (int h = 0; h < 8; h++)
-            for (int v = 0; v < 16; v++) QN[i][h][v] = apply(Q[i], uint32_t(v) << (4 * h));
+            for (int v = 0; v < 16; v++) SN[j][h][v] = apply(P[4 + j], uint32_t(v) << (4 * h));
+    for (int i = 0; i < kCrc32SegPowers; i++) shift_columns(uint64_t(8192) << i, SC[i]);
+    unshift_columns(8192, SC[kCrc32SegPowers]);
     // A^-1 really inverts A, on a basis
     for (int bit = 0; bit < 32; bit++)
         if (apply(Q[0], apply(P[0], 1u << bit)) != (1u << bit)) std::abort();
@@ -96,10 +98,18 @@ uint32_t Crc32Tables::shift(uint32_t s, uint64_t n) const {
     return s;
 }
 
-uint32_t Crc32Tables::unshift(uint32_t s, uint32_t n) const {
+uint32_t Crc32Tables::unshift(uint32_t s, uint32_t n) const {  // n <= 8192
     for (int i = 0; n && i < kCrc32InvPowers; i++, n >>= 1)
         if (n & 1) s = apply(Q[i], s);
     return s;
+}
+
+void Crc32Tables::shift_columns(uint64_t n, uint32_t (&col)[32]) const {
+    for (int b = 0; b < 32; b++) col[b] = shift(1u << b, n);
+}
+
+void Crc32Tables::unshift_columns(uint32_t n, uint32_t (&col)[32]) const {
+    for (int b = 0; b < 32; b++) col[b] = unshift(1u << b, n);
 }
 
 uint32_t Crc32Tables::fold(uint32_t s, const uint8_t* p, size_t n) const {

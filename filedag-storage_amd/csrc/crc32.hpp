@@ -7,9 +7,11 @@
 //   raw CRC        R(D) = fold of the byte update over D from s = 0
 //   Checksum(D)    = ~(A^|D|(0xFFFFFFFF) ^ R(D)),   R(D1 || D2) = A^|D2|(R(D1)) ^ R(D2)
 // No group order is used: forward shifts come from tables of A^(2^i), i < 32 (any 32-bit
-// byte count), and the one backward shift the device needs -- a row's last 1 KiB tile ends
-// up to 1023 bytes past the row's end -- from tables of A^-(2^i), i < 10.  The host applies
-// them byte-sliced (4 lookups); the device nibble-sliced (8 lookups, 512 B per power).
+// byte count), backward ones (below 8 KiB: a row's last device segment ends up to 8191 bytes
+// past the row's end) from tables of A^-(2^i), i < 14.  The host applies them byte-sliced
+// (4 lookups).  The device folds with nibble tables (8 lookups per word, 16-entry tables that
+// never bank-conflict), and applies its few per-segment shifts in column form (a 32 x 32
+// matrix over GF(2) as the images of the 32 basis vectors: 2 VALU per bit, no lookups).
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -17,23 +19,32 @@
 namespace rsmi {
 
 constexpr int kCrc32Powers = 32;    // A^(2^i)
-constexpr int kCrc32InvPowers = 10;  // A^-(2^i): backward shifts below 1024 bytes
+constexpr int kCrc32InvPowers = 14;  // A^-(2^i): backward shifts up to 8192 bytes
+constexpr int kCrc32SegTiles = 8;    // device segment: 8 tiles of 1 KiB (rs_crc32_rows_kernel)
+constexpr int kCrc32ScanPowers = 6;  // A^(16 * 2^j), j < 6: the 64-lane scan of a tile
+constexpr int kCrc32SegPowers = 19;  // A^(8192 * 2^i), i < 19: whole-segment shifts
 
 struct Crc32Tables {
     uint32_t T[256];                          // reflected 0xEDB88320
     uint32_t N[32][16];                       // nibble tables: N[2p][v] = A^(15-p)(T[v]), N[2p+1][v] = A^(15-p)(T[v << 4])
     uint32_t P[kCrc32Powers][4][256];         // P[i][h][x] = A^(2^i)(x << 8h)
     uint32_t Q[kCrc32InvPowers][4][256];      // Q[i][h][x] = A^-(2^i)(x << 8h)
-    // nibble-sliced copies for the device (512 B per power, so all of them fit in LDS):
-    // PN[i][h][v] = A^(2^i)(v << 4h), QN likewise
-    uint32_t PN[kCrc32Powers][8][16];
-    uint32_t QN[kCrc32InvPowers][8][16];
+    // device tables.  NT[t][q][v]: the nibble table N[q] moved 1024 * (7 - t) bytes further
+    // from the end, for a chunk in tile t of an 8-tile segment (value relative to the
+    // segment's end); SN[j][h][v] = A^(16 * 2^j)(v << 4h), nibble-sliced scan powers;
+    // SC[i][b] = A^(8192 * 2^i)(1 << b), column-form segment powers, and SC[19] = A^-8192
+    uint32_t NT[kCrc32SegTiles][32][16];
+    uint32_t SN[kCrc32ScanPowers][8][16];
+    uint32_t SC[kCrc32SegPowers + 1][32];
     Crc32Tables();
     static uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {
         return t[0][s & 0xFF] ^ t[1][(s >> 8) & 0xFF] ^ t[2][(s >> 16) & 0xFF] ^ t[3][s >> 24];
     }
     uint32_t shift(uint32_t s, uint64_t n) const;    // A^n(s), n < 2^32
-    uint32_t unshift(uint32_t s, uint32_t n) const;  // A^-n(s), n < 1024
+    uint32_t unshift(uint32_t s, uint32_t n) const;  // A^-n(s), n < 8192
+    // A^n / A^-n in column form (col[b] = image of 1 << b)
+    void shift_columns(uint64_t n, uint32_t (&col)[32]) const;
+    void unshift_columns(uint32_t n, uint32_t (&col)[32]) const;
     uint32_t fold(uint32_t s, const uint8_t* p, size_t n) const;
 };
 

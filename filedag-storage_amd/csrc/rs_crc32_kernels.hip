@@ -2,19 +2,21 @@
 // kv/mutcask/cask.go:73-97; algebra in crc32.hpp), the CRC-32 sibling of
 // rs_crc16_rows_kernel (rs_kernels.hip).
 //
-// Work item = (row, segment of kCrcSegTiles consecutive 1 KiB tiles).  Each lane loads its
-// 16-byte chunk of every tile of the segment (all loads in flight first), folds each chunk
-// with 32 nibble lookups into 16-entry u32 tables (N: chunk value relative to the chunk's
-// end; a wave-wide lookup into one table touches at most 16 dwords in 16 distinct banks, so
-// it never conflicts) and carries a running register across the tiles (A^1024 between
-// them).  A Hillis-Steele scan over the 64 lanes (A^(16 * 2^j) per level) leaves the
-// segment's value, relative to the segment's end, in lane 63.  Lane 63 then moves it to the
-// row's end -- forward by S - end for inner segments (A^(2^i) tables, i < 32), backward by
-// end - S < 1024 for the last one (A^-(2^i), i < 10) -- and XORs it into the row's word.
-// Every power is applied nibble-sliced (8 lookups into 16-entry tables, 512 B per power),
-// so all 42 of them sit in LDS next to the fold tables (23 KiB): the end shift is a
-// dependent chain of up to 32 applications, and chained L2 reads made it the kernel's
-// bottleneck (2.7 TB/s at 26 KB rows with byte-sliced tables in global memory).
+// Work item = (row, segment of kCrc32SegTiles = 8 consecutive 1 KiB tiles).  Each lane loads
+// its 16-byte chunk of every tile of the segment (all loads in flight first) and folds each
+// chunk with 32 nibble lookups into 16-entry u32 tables (a wave-wide lookup into one table
+// touches at most 16 dwords in 16 distinct banks, so it never conflicts).  Tile t of the
+// segment has its own tables (NT[t] = A^(1024 * (7 - t)) o N), so every chunk's value comes
+// out relative to the end of the segment's 8-tile span with no per-tile shift.  A
+// Hillis-Steele scan over the 64 lanes (A^(16 * 2^j) per level) leaves the segment's value in
+// lane 63, which moves it to the row's end and XORs it into the row's word.  With
+// S = 8192 q + r, inner segment j moves by 8192 (q - j - 1) + r; the last segment's span ends
+// at 8192 q (r = 0: the row's end) or 8192 (q + 1) = the row's end + 8192 - r, so it moves by
+// r - 8192.  A^r arrives by value (per launch), A^(8192 * 2^i) and A^-8192 from global
+// memory, all in column form, one column per lane, applied with a DPP XOR reduction (~10
+// instructions, no LDS -- the kernel's binding resource).  Per 8 KiB item: 256 fold lookups +
+// 48 scan lookups; the earlier form (a per-tile A^1024 and a chained end shift through
+// nibble tables) took ~430.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,8 +29,8 @@ namespace rsmi {
 
 namespace {
 
-// A^(2^i) or A^-(2^i) of s from a nibble-sliced table t[8][16] (512 B): the nibble offsets
-// come out of two masked words, as in the chunk fold
+// A^(16 * 2^j) of s from a nibble-sliced table t[8][16] (512 B): the nibble offsets come out
+// of two masked words, as in the chunk fold
 __device__ __forceinline__ uint32_t pow_nib(const uint32_t* t, uint32_t s) {
     uint32_t lo = (s << 2) & 0x3C3C3C3Cu, hi = (s >> 2) & 0x3C3C3C3Cu;
     asm volatile("" : "+v"(lo), "+v"(hi));
@@ -42,23 +44,48 @@ __device__ __forceinline__ uint32_t pow_nib(const uint32_t* t, uint32_t s) {
     return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), l[6] ^ l[7]);
 }
 
+// M(s) for a matrix M held lane-distributed (lane l < 32 of col holds M's image of 1 << l;
+// lanes 32-63 repeat them) and a wave-uniform s: each lane keeps its column if bit l of s is
+// set, an XOR scan over each 16-lane row (DPP row_shr 1, 2, 4, 8) leaves the rows' sums in
+// lanes 15 and 31.  No SGPR copies of the matrix, no LDS.
+__device__ __forceinline__ uint32_t dpp_xor_shr(uint32_t x, int n) {
+    switch (n) {  // DPP control must be a constant: row_shr:n = 0x110 + n
+        case 1: return x ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, false));
+        case 2: return x ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, false));
+        case 4: return x ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, false));
+        default: return x ^ uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, false));
+    }
+}
+
+__device__ __forceinline__ uint32_t apply_lanes(uint32_t col, uint32_t s, uint32_t l32) {
+    uint32_t x = ((s >> l32) & 1u) ? col : 0u;
+    x = dpp_xor_shr(x, 1);
+    x = dpp_xor_shr(x, 2);
+    x = dpp_xor_shr(x, 4);
+    x = dpp_xor_shr(x, 8);
+    return uint32_t(__builtin_amdgcn_readlane(int(x), 15)) ^ uint32_t(__builtin_amdgcn_readlane(int(x), 31));
+}
+
 }  // namespace
 
-// tbl: N[32][16] | PN[32][8][16] | QN[10][8][16] (u32 words, rs_plan.hpp), all staged in LDS
+// tbl: NT[8][32][16] | SN[6][8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp)
 template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
-                                                            uint64_t out_bs) {
-    __shared__ uint32_t s_tbl[kCrc32TableWords];
-    for (int i = threadIdx.x; i < kCrc32TableWords; i += kWG) s_tbl[i] = tbl[i];
+                                                            uint64_t out_bs, Crc32Shift sh) {
+    __shared__ uint32_t s_tbl[kCrc32LdsWords];
+    for (int i = threadIdx.x; i < kCrc32LdsWords; i += kWG) s_tbl[i] = tbl[i];
     __syncthreads();
-    const uint32_t* s_n = s_tbl;
-    const uint32_t* sP = s_tbl + kCrc32NWords;
-    const uint32_t* sQ = sP + kCrc32Powers * kCrc32PowWords;
-    auto lpow = [&](int i, uint32_t s) { return pow_nib(sP + i * kCrc32PowWords, s); };
-
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl);
+    const uint32_t* sS = s_tbl + kCrc32FoldWords;
+    const uint32_t* sC = tbl + kCrc32LdsWords;
+    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024)), r8 = uint32_t(S % (kCrc32SegTiles * 1024));
+    const uint32_t l32 = threadIdx.x & 31;
+    uint32_t col_r = 0;  // A^r, lane-distributed
+#pragma unroll
+    for (int b = 0; b < 32; b++) col_r = l32 == uint32_t(b) ? sh.col[b] : col_r;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
@@ -68,11 +95,11 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
         const uint64_t b = rid / nrows;
         const uint32_t r = uint32_t(rid - b * nrows);
         const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-        const uint32_t t0 = seg * kCrcSegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
-        u32x4 v[kCrcSegTiles];
+        const uint32_t t0 = seg * kCrc32SegTiles;
+        const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
+        u32x4 v[kCrc32SegTiles];
 #pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++)
+        for (int i = 0; i < kCrc32SegTiles; i++)
             if (uint32_t(i) < nt) {
                 const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
                 // wave-uniform: only a row's last tile needs the per-lane bounds and masks
@@ -82,11 +109,9 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
                     v[i] = crc_chunk_load<ALIGNED>(row, off, S);
             }
         uint32_t acc = 0;
-        const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_n);
 #pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++) {
+        for (int i = 0; i < kCrc32SegTiles; i++) {
             if (uint32_t(i) < nt) {
-                uint32_t c = 0;
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     // byte offsets 4 x nibble into the 16-entry u32 tables (64 B each)
@@ -96,33 +121,32 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const int p = 4 * w + q;
-                        l[2 * q] = *reinterpret_cast<const uint32_t*>(nb + 128 * p + ((lo >> (8 * q)) & 0xFF));
-                        l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(nb + 128 * p + 64 + ((hi >> (8 * q)) & 0xFF));
+                        const int o = 2048 * i + 128 * p;
+                        l[2 * q] = *reinterpret_cast<const uint32_t*>(nb + o + ((lo >> (8 * q)) & 0xFF));
+                        l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(nb + o + 64 + ((hi >> (8 * q)) & 0xFF));
                     }
-                    c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+                    acc = xor3(acc, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
                 }
-                acc = lpow(10, acc) ^ c;  // previous tiles move 1 KiB further from the end
             }
         }
 #pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const uint32_t w = lpow(4 + j, acc);  // 16 * 2^j bytes
+        for (int j = 0; j < kCrc32ScanPowers; j++) {
+            const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
             const uint32_t t = __shfl_up(w, 1u << j);
             if (lane >= (1u << j)) acc ^= t;
         }
-        if (lane == kWave - 1) {
-            const uint64_t seg_end = uint64_t(t0 + nt) * (kWave * 16);
-            if (seg_end <= S) {
-                uint64_t e = S - seg_end;
-                for (int i = 0; e; i++, e >>= 1)
-                    if (e & 1) acc = lpow(i, acc);
-            } else {
-                uint32_t e = uint32_t(seg_end - S);  // < 1024: only the last tile passes S
-                for (int i = 0; e; i++, e >>= 1)
-                    if (e & 1) acc = pow_nib(sQ + i * kCrc32PowWords, acc);
-            }
-            atomicXor(out + b * out_bs + r, acc);
+        // lane 63's value, wave-uniform from here on
+        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));
+        if (seg + 1 < nseg) {
+            // whole segments, then the remainder r
+            uint32_t a = q8 - seg - 1;
+            for (int i = 0; a; i++, a >>= 1)
+                if (a & 1) val = apply_lanes(sC[32 * i + l32], val, l32);
+            val = apply_lanes(col_r, val, l32);
+        } else if (r8) {
+            val = apply_lanes(col_r, apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32), l32);
         }
+        if (lane == 0) atomicXor(out + b * out_bs + r, val);
     }
 }
 

@@ -60,10 +60,17 @@ constexpr int kCrcPWords = 15 * 2 * 256 / 2;
 constexpr int kCrcUWords = 16 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
 constexpr int kCrcTableWords = kCrcPWords + kCrcUWords + kCrcNWords;
-// CRC-32 (crc32.hpp) device tables: N[32][16] | PN[32][8][16] | QN[10][8][16], u32 words
-constexpr int kCrc32NWords = 32 * 16;
+// CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
+// LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
+constexpr int kCrc32FoldWords = 8 * 32 * 16;
 constexpr int kCrc32PowWords = 8 * 16;  // one nibble-sliced power
-constexpr int kCrc32TableWords = kCrc32NWords + (32 + 10) * kCrc32PowWords;
+constexpr int kCrc32LdsWords = kCrc32FoldWords + 6 * kCrc32PowWords;
+constexpr int kCrc32TableWords = kCrc32LdsWords + 20 * 32;
+// per-launch shift to the row's end, column form (crc32.hpp), passed by value: A^(S mod 8192),
+// the end of an inner segment moved over whatever of the row follows whole segments
+struct Crc32Shift {
+    uint32_t col[32];
+};
 void* crc16_rows_kernel(bool aligned, int fold);
 void* crc16_combine_kernel();
 void* crc32_rows_kernel(bool aligned);

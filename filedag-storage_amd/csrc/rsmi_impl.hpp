@@ -88,6 +88,8 @@ struct rsmi_ctx {
     uint32_t* d_crc32_tbl = nullptr;  // CRC-32 device tables (crc32.hpp), uploaded on first use
     uint8_t* d_crc32 = nullptr;       // raw row CRC-32s of host batch calls
     size_t crc32_cap = 0;
+    rsmi::Crc32Shift crc32_shift{};  // launch_crc32's per-S shift matrix, for crc32_shift_S
+    uint64_t crc32_shift_S = ~uint64_t(0);
     uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
     size_t chunks_cap = 0;
     // options
