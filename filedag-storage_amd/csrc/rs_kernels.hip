@@ -533,6 +533,200 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
     }
 }
 
+// FOLD 2 of the CRC-16 rows pass: the item shape of rs_crc16_rows_kernel, but every lookup
+// goes to a 64-entry u16 table (32 dwords: the 32 lanes of a ds_read_b32 half-wave hit at most
+// one dword per bank, so no lookup conflicts).  A chunk folds with 22 H lookups (21 six-bit
+// fields and a two-bit one, across its 128 bits) instead of 32 nibble lookups; the tile step
+// (A^1024) and the lane scan apply their powers six bits at a time (3 conflict-free lookups
+// where the byte tables took 2 with random banks); and lane 63's value is made wave-uniform
+// before the end shift, so those lookups are broadcasts.  Measured level with FOLD 1: the
+// kernel is bound by VALU issue and latency, not LDS.
+__device__ __forceinline__ uint32_t crc_pow6(const uint8_t* ph, int i, uint32_t s) {
+    const uint8_t* t = ph + i * 384;
+    return uint32_t(*reinterpret_cast<const uint16_t*>(t + ((s << 1) & 0x7E))) ^
+           uint32_t(*reinterpret_cast<const uint16_t*>(t + 128 + ((s >> 5) & 0x7E))) ^
+           uint32_t(*reinterpret_cast<const uint16_t*>(t + 256 + ((s >> 11) & 0x7E)));
+}
+
+// byte offset 2 * (bits 6f..6f+5 of the chunk) into the 64-entry u16 table of field f
+template <int F>
+__device__ __forceinline__ uint32_t six_off(const u32x4& v) {
+    constexpr int o = 6 * F, d = o / 32, sh = o % 32;
+    if constexpr (F == kCrcSixFields - 1) {
+        return (v[3] >> 29) & 0x6u;  // bits 126, 127
+    } else if constexpr (sh == 0) {
+        return (v[d] << 1) & 0x7Eu;
+    } else if constexpr (sh + 6 <= 32) {
+        return (v[d] >> (sh - 1)) & 0x7Eu;
+    } else {
+        return __builtin_amdgcn_alignbit(v[d + 1], v[d], sh - 1) & 0x7Eu;
+    }
+}
+
+template <int F>
+__device__ __forceinline__ uint32_t six_fold(const uint8_t* h, const u32x4& v) {
+    const uint32_t x = *reinterpret_cast<const uint16_t*>(h + 128 * F + six_off<F>(v));
+    if constexpr (F + 1 < kCrcSixFields) return x ^ six_fold<F + 1>(h, v);
+    else return x;
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(kWG) void rs_crc16_rows6_kernel(const uint32_t* __restrict__ tbl,
+                                                             const uint8_t* __restrict__ base, uint64_t bstride,
+                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
+                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
+                                                             uint64_t out_bs) {
+    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcHWords + kCrcPHWords];
+    for (int i = threadIdx.x; i < kCrcHWords + kCrcPHWords; i += kWG) s_tbl[i] = tbl[kCrcHOff + i];
+    __syncthreads();
+    const uint8_t* sH = reinterpret_cast<const uint8_t*>(s_tbl);
+    const uint8_t* sPH = sH + kCrcHWords * 4;
+
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
+        const uint32_t seg = uint32_t(it % nseg);
+        const uint64_t rid = it / nseg;
+        const uint64_t b = rid / nrows;
+        const uint32_t r = uint32_t(rid - b * nrows);
+        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+        const uint32_t t0 = seg * kCrcSegTiles;
+        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
+        u32x4 v[kCrcSegTiles];
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++)
+            if (uint32_t(i) < nt) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
+                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+                else
+                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
+            }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++)
+            if (uint32_t(i) < nt) acc = crc_pow6(sPH, 10, acc) ^ six_fold<0>(sH, v[i]);  // earlier tiles move 1 KiB
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t w = crc_pow6(sPH, 4 + j, acc);  // 16 * 2^j bytes
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (lane >= (1u << j)) acc ^= t;
+        }
+        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));
+        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
+        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
+        if (e < 0) e += kCrcOrder;
+        for (int i = 0; e; i++, e >>= 1)
+            if (e & 1) val = crc_pow6(sPH, i, val);
+        if (lane == 0) atomicXor(out + b * out_bs + r, val);
+    }
+}
+
+// FOLD 3: the FOLD 1 (nibble) rows pass, software-pipelined, for 16-byte-aligned rows.  A wave
+// issues the 8 tile loads of its next item before it folds the current one (two register sets,
+// the loop unrolled by two), so its own fold covers the next item's memory latency instead of
+// only the other waves on the SIMD.  Loads are unconditional -- chunks past the row's end read
+// the row's last chunk and are masked to zero in the fold, and the prefetch past the last item
+// re-reads that item -- so no load sits behind a branch and the compiler's vmcnt waits count
+// only the older set.
+__device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4& v) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint32_t lo = (v[w] << 1) & 0x1E1E1E1Eu, hi = (v[w] >> 3) & 0x1E1E1E1Eu;
+        asm volatile("" : "+v"(lo), "+v"(hi));
+        uint32_t l[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int p = 4 * w + q;
+            l[2 * q] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + ((lo >> (8 * q)) & 0xFF));
+            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
+        }
+        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t* __restrict__ tbl,
+                                                                 const uint8_t* __restrict__ base, uint64_t bstride,
+                                                                 uint64_t rpitch, uint32_t nrows, uint64_t S,
+                                                                 uint32_t tpb, uint32_t nseg, uint64_t nitems,
+                                                                 uint32_t* __restrict__ out, uint64_t out_bs) {
+    __shared__ uint32_t s_tbl[kCrcPWords + kCrcNWords];
+    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
+    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + kCrcUWords + i];
+    __syncthreads();
+    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sP + kCrcPWords * 2);
+
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
+    auto issue = [&](uint64_t it, u32x4(&v)[kCrcSegTiles]) {
+        const uint32_t seg = uint32_t(it % nseg);
+        const uint64_t rid = it / nseg;
+        const uint64_t b = rid / nrows;
+        const uint32_t r = uint32_t(rid - b * nrows);
+        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++) {
+            const uint64_t off = (uint64_t(seg * kCrcSegTiles + i) * kWave + lane) * 16;
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
+        }
+    };
+    auto finish = [&](uint64_t it, u32x4(&v)[kCrcSegTiles]) {
+        const uint32_t seg = uint32_t(it % nseg);
+        const uint64_t rid = it / nseg;
+        const uint64_t b = rid / nrows;
+        const uint32_t r = uint32_t(rid - b * nrows);
+        const uint32_t t0 = seg * kCrcSegTiles;
+        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < kCrcSegTiles; i++) {
+            if (uint32_t(i) < nt) {
+                if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
+                    const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const int64_t n = valid - 4 * w;
+                        v[i][w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                    }
+                }
+                acc = crc_pow(sP, 10, acc) ^ crc_nib_chunk(nb, v[i]);  // earlier tiles move 1 KiB
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const uint32_t w = crc_pow(sP, 4 + j, acc);  // 16 * 2^j bytes
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (lane >= (1u << j)) acc ^= t;
+        }
+        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
+        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
+        if (e < 0) e += kCrcOrder;
+#pragma unroll
+        for (int i = 0; i < kCrcPowers; i++)
+            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
+        if (lane == kWave - 1) atomicXor(out + b * out_bs + r, acc);
+    };
+    const uint64_t it0 = uint64_t(blockIdx.x) * (kWG / kWave) + wid;
+    if (it0 >= nitems) return;
+    const uint64_t itmax = nitems - 1;
+    u32x4 va[kCrcSegTiles], vb[kCrcSegTiles];
+    issue(it0, va);
+    for (uint64_t it = it0;; it += 2 * nw) {
+        issue(it + nw < itmax ? it + nw : itmax, vb);
+        finish(it, va);
+        if (it + nw > itmax) break;
+        issue(it + 2 * nw < itmax ? it + 2 * nw : itmax, va);
+        finish(it + nw, vb);
+        if (it + 2 * nw > itmax) break;
+    }
+}
+
 // R(row) from the fused kernels' per-chunk values (rs_fast_kernel CRC): one wave per row.
 // Lane l folds chunks l, l + 64, ... (A^1024 between them), a lane scan combines the lanes
 // (A^(16*2^j)), and lane 63 shifts the total from the 1 KiB grid end to the row end.  The
@@ -582,6 +776,11 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
 void* crc16_combine_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_kernel); }
 
 void* crc16_rows_kernel(bool aligned, int fold) {
+    if (fold == 3 && aligned) return reinterpret_cast<void*>(&rs_crc16_rows_pipe_kernel);
+    if (fold == 3) fold = 1;  // the pipelined pass needs aligned rows
+    if (fold == 2)
+        return aligned ? reinterpret_cast<void*>(&rs_crc16_rows6_kernel<true>)
+                       : reinterpret_cast<void*>(&rs_crc16_rows6_kernel<false>);
     if (fold == 0)
         return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 0>)
                        : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false, 0>);

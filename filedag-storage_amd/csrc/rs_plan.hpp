@@ -52,14 +52,20 @@ void* generic_kernel();
 void* repitch_kernel();
 
 // CRC-16 of shard rows (crc16.hpp): the device table buffer holds P[15][2][256], then
-// U[16][256], then N[32][16] (u16); a wave folds kCrcSegTiles 1 KiB tiles of one row.
-// Chunk fold: 0 = one U lookup per byte (256-entry tables, bank conflicts), 1 = one N
-// lookup per nibble (16-entry tables: each lookup touches 8 distinct banks, conflict-free).
+// U[16][256], N[32][16], H[22][64] and PH[15][3][64] (u16); a wave folds kCrcSegTiles 1 KiB
+// tiles of one row.  Chunk fold: 0 = one U lookup per byte (256-entry tables, bank
+// conflicts), 1 = one N lookup per nibble (16-entry tables: each lookup touches 8 distinct
+// banks, conflict-free), 2 = one H lookup per six bits (64 u16 = 32 dwords, one per bank of a
+// ds_read_b32 half-wave: conflict-free) with powers from PH, also conflict-free (A/B: level
+// with 1).
 constexpr int kCrcSegTiles = 8;
 constexpr int kCrcPWords = 15 * 2 * 256 / 2;
 constexpr int kCrcUWords = 16 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
-constexpr int kCrcTableWords = kCrcPWords + kCrcUWords + kCrcNWords;
+constexpr int kCrcHWords = 22 * 64 / 2;
+constexpr int kCrcPHWords = 15 * 3 * 64 / 2;
+constexpr int kCrcHOff = kCrcPWords + kCrcUWords + kCrcNWords;
+constexpr int kCrcTableWords = kCrcHOff + kCrcHWords + kCrcPHWords;
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;

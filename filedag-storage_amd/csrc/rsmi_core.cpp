@@ -494,7 +494,7 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         if (value < 1 || value > 65536) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_max = value;
     } else if (!std::strcmp(key, "crc_fold")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
+        if (value < 0 || value > 3) return RSMI_ERR_INVALID_ARG;
         c->opt_crc_fold = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;

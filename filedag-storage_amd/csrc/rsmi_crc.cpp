@@ -14,11 +14,14 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.U) + sizeof(t.N) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.U) + sizeof(t.N) + sizeof(t.H) + sizeof(t.PH) == size_t(kCrcTableWords) * 4,
+                  "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
     std::memcpy(h.data(), t.P, sizeof(t.P));
     std::memcpy(h.data() + kCrcPWords * 2, t.U, sizeof(t.U));
     std::memcpy(h.data() + (kCrcPWords + kCrcUWords) * 2, t.N, sizeof(t.N));
+    std::memcpy(h.data() + kCrcHOff * 2, t.H, sizeof(t.H));
+    std::memcpy(h.data() + (kCrcHOff + kCrcHWords) * 2, t.PH, sizeof(t.PH));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -40,8 +43,10 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     uint64_t nitems = nblocks * nrows * nseg;
     // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
     // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
-    // +3 % over occupancy x CUs, -25 % at one item per wave)
-    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
+    // +3 % over occupancy x CUs, -25 % at one item per wave).  The pipelined pass (fold 3)
+    // keeps its next item's loads in flight itself and does best at 48 (tools/crc_wpc_sweep.sh)
+    const bool pipe = c->opt_crc_fold == 3 && aligned;
+    uint64_t cap = uint64_t(c->num_cu) * (pipe ? 48 : 96) / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
@@ -86,8 +91,10 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     uint64_t nitems = nblocks * nrows * nseg;
     // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
     // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
-    // +3 % over occupancy x CUs, -25 % at one item per wave)
-    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
+    // +3 % over occupancy x CUs, -25 % at one item per wave).  The pipelined pass (fold 3)
+    // keeps its next item's loads in flight itself and does best at 48 (tools/crc_wpc_sweep.sh)
+    const bool pipe = c->opt_crc_fold == 3 && aligned;
+    uint64_t cap = uint64_t(c->num_cu) * (pipe ? 48 : 96) / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;

@@ -264,8 +264,9 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t
  * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: host batch calls whose buffers are page-locked
 (rsmi_host_alloc) run as one kernel that reads and writes them in place over PCIe, at any
 size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
-same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 chunk fold: 1 = nibble tables
-(default), 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
+same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 rows pass: 3 = nibble tables,
+software-pipelined, for aligned rows (default; unaligned rows take 1), 1 = nibble tables, 2 =
+six-bit tables, 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
 table fields into SGPRs by scalar loads instead of LDS (A/B)), "lds_dma" (1|2 = RS(10,4)
 aligned encode and 1-row reconstruct run the LDS-DMA staged kernel with 4|2 waves per
 workgroup (A/B)), "nontemporal" 3|4 (sc1 / nt buffer stores), "store_aux" (buffer-store cache

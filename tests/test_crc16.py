@@ -91,7 +91,7 @@ def _device_rows(nb, nrows, S, pitch, offset, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1024, 1025, 8191, 8192, 8193, 26215, 104858, 262144])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
-@pytest.mark.parametrize("fold", [1, 0])
+@pytest.mark.parametrize("fold", [3, 2, 1, 0])
 def test_rows_dev_matches_oracle(S, layout, fold):
     import torch
 

@@ -14,6 +14,11 @@ sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
 import rsmi  # noqa: E402
 
 
+# env CRC_FOLDS (e.g. "2,1") and CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
+FOLDS = [f if f == "crc32" else int(f) for f in os.environ.get("CRC_FOLDS", "3,2,1,0,crc32").split(",")]
+WPC = int(os.environ.get("CRC_WPC", "0"))
+
+
 def main():
     st = torch.cuda.current_stream()
     for k, m, B, nb in ((10, 4, 262144, 4096), (10, 4, 1 << 20, 1024), (16, 4, 4 << 20, 256)):
@@ -22,8 +27,10 @@ def main():
         p = rsmi.recommended_pitch(S)
         buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
         out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
-        for fold in (1, 0, "crc32"):
+        for fold in FOLDS:
             c = rsmi.Codec(k, m)
+            if WPC:
+                c.set_option("waves_per_cu", WPC)
             if fold == "crc32":
                 f = lambda: c.crc32_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             else:
@@ -42,7 +49,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
-            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 fold=' + ('nibble' if fold else 'byte')}: "
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 fold=' + ('nibble-pipelined', 'six-bit', 'nibble', 'byte')[3 - fold]}: "
                   f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
             c.close()
 
