@@ -79,6 +79,6 @@ struct Crc32Shift {
 };
 void* crc16_rows_kernel(bool aligned, int fold);
 void* crc16_combine_kernel();
-void* crc32_rows_kernel(bool aligned);
+void* crc32_rows_kernel(bool aligned, bool pipe);
 
 }  // namespace rsmi

@@ -71,13 +71,17 @@ int ensure_crc32_tables(rsmi_ctx* c) {
 
 // CRC-32 R(row) of nrows rows per block, XORed into out[b*out_bs + r] (the caller zeroes
 // it), stream-ordered.  Rows may lie in device or page-locked host memory.
+// grid of the pipelined CRC-32 pass, waves per CU (crc_wpc_sweep.sh)
+constexpr int kCrc32PipeWaves = 48;
+
 int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
                  uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream) {
     if (!nblocks || !nrows || S == 0) return RSMI_OK;  // R(empty) = 0
     int rc = ensure_crc32_tables(c);
     if (rc) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = crc32_rows_kernel(aligned);
+    const bool pipe = c->opt_crc32_pipe && aligned;
+    void* fn = crc32_rows_kernel(aligned, pipe);
     const uint64_t tile = uint64_t(kWave) * 16, span = tile * kCrc32SegTiles;
     if (S / span >= (uint64_t(1) << kCrc32SegPowers)) return RSMI_ERR_INVALID_ARG;  // rows below 4 GiB
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
@@ -89,12 +93,9 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     }
     Crc32Shift sh = c->crc32_shift;
     uint64_t nitems = nblocks * nrows * nseg;
-    // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
-    // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
-    // +3 % over occupancy x CUs, -25 % at one item per wave).  The pipelined pass (fold 3)
-    // keeps its next item's loads in flight itself and does best at 48 (tools/crc_wpc_sweep.sh)
-    const bool pipe = c->opt_crc_fold == 3 && aligned;
-    uint64_t cap = uint64_t(c->num_cu) * (pipe ? 48 : 96) / 4;
+    // 96 waves per CU as for the CRC-16 pass; the pipelined pass (option crc32_pipe) at
+    // kCrc32PipeWaves (tools/crc_wpc_sweep.sh)
+    uint64_t cap = uint64_t(c->num_cu) * (pipe ? kCrc32PipeWaves : 96) / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;

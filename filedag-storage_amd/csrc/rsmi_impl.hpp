@@ -99,6 +99,7 @@ struct rsmi_ctx {
     int opt_prefetch = 0;
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
     int opt_crc_fold = 3;   // CRC-16 rows pass: 3 = nibble tables, pipelined; 1 = nibble; 2 = six-bit; 0 = byte (A/B)
+    int opt_crc32_pipe = 0;  // CRC-32 rows pass: 0 = plain, 1 = software-pipelined for aligned rows (A/B, level)
     int opt_xcd_order = 0;      // 1: RS(10,4) bench shapes with XCD-grouped tile order (A/B)
     int opt_buffer_stores = 0;  // 1: aligned launches of policy 1 use policy 4 (buffer stores)
     int opt_store_aux = -1;  // >= 0: RS(10,4) kernels store with these buffer cache bits (A/B)

@@ -266,7 +266,8 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t
 size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
 same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 rows pass: 3 = nibble tables,
 software-pipelined, for aligned rows (default; unaligned rows take 1), 1 = nibble tables, 2 =
-six-bit tables, 0 = byte tables (A/B)), "tables" (1 = RS(10,4) kernels read three of the five
+six-bit tables, 0 = byte tables (A/B)), "crc32_pipe" (CRC-32 rows pass: 0 = plain (default), 1 =
+software-pipelined for aligned rows (A/B: level with 0)), "tables" (1 = RS(10,4) kernels read three of the five
 table fields into SGPRs by scalar loads instead of LDS (A/B)), "lds_dma" (1|2 = RS(10,4)
 aligned encode and 1-row reconstruct run the LDS-DMA staged kernel with 4|2 waves per
 workgroup (A/B)), "nontemporal" 3|4 (sc1 / nt buffer stores), "store_aux" (buffer-store cache

@@ -163,7 +163,7 @@ def test_null_arguments():
 def test_new_options_and_stats_validate():
     L = rsmi.lib()
     with rsmi.Codec(10, 4) as c:
-        for key, good, bad in [(b"tables", 2, 3), (b"lds_dma", 2, 3), (b"store_aux", 16, 3), (b"buffer_stores", 1, 2), (b"xcd_order", 1, 2), (b"crc_fold", 3, 4), (b"coalesce_us", 50, -1),
+        for key, good, bad in [(b"tables", 2, 3), (b"lds_dma", 2, 3), (b"store_aux", 16, 3), (b"buffer_stores", 1, 2), (b"xcd_order", 1, 2), (b"crc_fold", 3, 4), (b"crc32_pipe", 0, 2), (b"coalesce_us", 50, -1),
                                (b"coalesce_max", 16, 0)]:
             assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
             assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key

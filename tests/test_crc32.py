@@ -67,7 +67,8 @@ def test_oracle_mutcask_entry_crc_is_checksum_of_framed_entry():
 @pytest.mark.gpu
 @pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1023, 1024, 1025, 8191, 8192, 8193, 16384, 24577, 26215, 73729, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
-def test_rows_dev_matches_zlib(S, layout):
+@pytest.mark.parametrize("pipe", [1, 0])
+def test_rows_dev_matches_zlib(S, layout, pipe):
     import torch
 
     nrows, nb = 3, 5
@@ -80,6 +81,7 @@ def test_rows_dev_matches_zlib(S, layout):
     dev = host.to("cuda")
     out = torch.full((nb, nrows + 1), 0xDEAD, dtype=torch.int32, device="cuda")
     with rsmi.Codec(4, 2) as c:
+        c.set_option("crc32_pipe", pipe)
         c.crc32_rows_dev(dev.data_ptr() + off, pitch, nrows * pitch, nrows, S, nb, out.data_ptr(), nrows + 1)
         torch.cuda.synchronize()
         assert c.last_kernel() == "rs_crc32_rows_kernel"

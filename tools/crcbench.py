@@ -15,7 +15,7 @@ import rsmi  # noqa: E402
 
 
 # env CRC_FOLDS (e.g. "2,1") and CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
-FOLDS = [f if f == "crc32" else int(f) for f in os.environ.get("CRC_FOLDS", "3,2,1,0,crc32").split(",")]
+FOLDS = [f if f.startswith("crc32") else int(f) for f in os.environ.get("CRC_FOLDS", "3,2,1,0,crc32").split(",")]
 WPC = int(os.environ.get("CRC_WPC", "0"))
 
 
@@ -31,7 +31,8 @@ def main():
             c = rsmi.Codec(k, m)
             if WPC:
                 c.set_option("waves_per_cu", WPC)
-            if fold == "crc32":
+            if fold in ("crc32", "crc32pipe"):
+                c.set_option("crc32_pipe", int(fold == "crc32pipe"))
                 f = lambda: c.crc32_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             else:
                 c.set_option("crc_fold", fold)
@@ -49,7 +50,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
-            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 fold=' + ('nibble-pipelined', 'six-bit', 'nibble', 'byte')[3 - fold]}: "
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {('crc32 pipelined' if fold == 'crc32pipe' else 'crc32 (mutcask)') if fold in ('crc32', 'crc32pipe') else 'crc16 fold=' + ('nibble-pipelined', 'six-bit', 'nibble', 'byte')[3 - fold]}: "
                   f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
             c.close()
 
