@@ -75,6 +75,24 @@ def fused_vs_separate():
         "encode with fused CRC": lambda: c.encode_batch_dev_crc(b, p, n * p, b + k * p, p, n * p, S, nb,
                                                                 raw.data_ptr(), sh),
     }
+    s2 = torch.cuda.Stream()
+
+    def staged(parts):
+        # encode part i on the main stream while the CRC pass of part i - 1 runs on s2
+        q = nb // parts
+        for i in range(parts):
+            off = i * q * n * p
+            c.encode_batch_dev(b + off, p, n * p, b + off + k * p, p, n * p, S, q, sh)
+            e = torch.cuda.Event()
+            e.record(st)
+            s2.wait_event(e)
+            c.crc16_rows_dev(b + off, p, n * p, n, S, q, raw.data_ptr() + i * q * n * 4, n, s2.cuda_stream)
+        e = torch.cuda.Event()
+        e.record(s2)
+        st.wait_event(e)
+
+    for parts in (2, 4, 8):
+        V[f"encode || CRC pass, {parts} parts"] = lambda parts=parts: staged(parts)
     t_end = time.perf_counter() + 0.2
     while time.perf_counter() < t_end:
         for f in V.values():
@@ -91,7 +109,7 @@ def fused_vs_separate():
             ts[name].append(e0.elapsed_time(e1))
     for name in V:
         med = statistics.median(ts[name])
-        print(f"RS(10,4) 256 KiB x {nb}: {name:28s} {med * 1e3:8.1f} us  "
+        print(f"RS(10,4) 256 KiB x {nb}: {name:32s} {med * 1e3:8.1f} us  "
               f"{nb * n * S / med / 1e6:8.1f} GB/s of shard bytes", flush=True)
     c.close()
 
