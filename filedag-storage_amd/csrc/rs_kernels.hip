@@ -736,10 +736,12 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
                                                                const uint16_t* __restrict__ chunks, uint32_t cpb,
                                                                uint32_t pitch, uint64_t S, uint64_t nrows,
                                                                uint32_t* __restrict__ out) {
-    __shared__ uint32_t s_tbl[kCrcPWords];
-    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
+    // six-bit power tables PH (5.6 KiB, conflict-free: crc_pow6); the chunk values are loaded
+    // 8 steps at a time ahead of the dependent A^1024 chain
+    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcPHWords];
+    for (int i = threadIdx.x; i < kCrcPHWords; i += kWG) s_tbl[i] = tbl[kCrcHOff + kCrcHWords + i];
     __syncthreads();
-    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
+    const uint8_t* sPH = reinterpret_cast<const uint8_t*>(s_tbl);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
@@ -748,28 +750,36 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
     for (uint64_t r = uint64_t(blockIdx.x) * (kWG / kWave) + wid; r < nrows; r += nw) {
         const uint16_t* rc = chunks + r * pitch;
         uint32_t acc = 0;
-        for (uint32_t t = 0; t < T; t++) {
-            const uint32_t ch = t * kWave + lane;
-            uint32_t c = ch < cpb ? rc[ch] : 0u;
-            if (ch == cpb - 1) {  // onto the grid: as if followed by 16*cpb - S zero bytes
+        for (uint32_t t0 = 0; t0 < T; t0 += 8) {
+            uint32_t c[8];
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if ((lead >> i) & 1) c = crc_pow(sP, i, c);
+            for (int i = 0; i < 8; i++) {
+                const uint32_t ch = (t0 + i) * kWave + lane;
+                c[i] = ch < cpb ? rc[ch] : 0u;
             }
-            acc = crc_pow(sP, 10, acc) ^ c;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if (t0 + i >= T) break;
+                if ((t0 + i) * kWave + lane == cpb - 1) {  // onto the grid: as if followed by 16*cpb - S zero bytes
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if ((lead >> q) & 1) c[i] = crc_pow6(sPH, q, c[i]);
+                }
+                acc = crc_pow6(sPH, 10, acc) ^ c[i];
+            }
         }
 #pragma unroll
         for (int j = 0; j < 6; j++) {
-            const uint32_t w = crc_pow(sP, 4 + j, acc);
+            const uint32_t w = crc_pow6(sPH, 4 + j, acc);
             const uint32_t t = __shfl_up(w, 1u << j);
             if (lane >= (1u << j)) acc ^= t;
         }
+        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // uniform: broadcast lookups
         int64_t e = (int64_t(S) - int64_t(T) * (kWave * 16)) % int64_t(kCrcOrder);
         if (e < 0) e += kCrcOrder;
-#pragma unroll
-        for (int i = 0; i < kCrcPowers; i++)
-            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
-        if (lane == kWave - 1) out[r] = acc;
+        for (int i = 0; e; i++, e >>= 1)
+            if (e & 1) val = crc_pow6(sPH, i, val);
+        if (lane == 0) out[r] = val;
     }
 }
 

@@ -140,7 +140,9 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
     uint64_t S64 = S, rows = nblocks * n;
     const uint32_t* tb = c->d_crc_tbl;
     void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &raw};
-    const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 4));
+    // one wave per row up to 64 waves per CU: the combine is a dependent chain per lane, so
+    // it wants many waves in flight
+    const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 16));
     HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
     return RSMI_OK;
 }
