@@ -728,62 +728,95 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 }
 
 // R(row) from the fused kernels' per-chunk values (rs_fast_kernel CRC): one wave per row.
-// Lane l folds chunks l, l + 64, ... (A^1024 between them), a lane scan combines the lanes
-// (A^(16*2^j)), and lane 63 shifts the total from the 1 KiB grid end to the row end.  The
+// Lane l folds chunks 8l..8l+7, 512 + 8l.., ... (A^8192 between wave steps), a lane scan
+// combines the lanes (A^(128*2^j)), and lane 63 shifts the total from the 8 KiB grid end to
+// the row end.  The
 // row's last chunk is relative to S (its window ends at S), so it first moves onto the
 // 16-byte grid by A^(16*cpb - S).  out[row] is written once (host memory allowed).
+template <bool SIX>
 __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* __restrict__ tbl,
                                                                const uint16_t* __restrict__ chunks, uint32_t cpb,
                                                                uint32_t pitch, uint64_t S, uint64_t nrows,
                                                                uint32_t* __restrict__ out) {
-    // six-bit power tables PH (5.6 KiB, conflict-free: crc_pow6); the chunk values are loaded
-    // 8 steps at a time ahead of the dependent A^1024 chain
-    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcPHWords];
-    for (int i = threadIdx.x; i < kCrcPHWords; i += kWG) s_tbl[i] = tbl[kCrcHOff + kCrcHWords + i];
+    // six-bit power tables PH (5.6 KiB, conflict-free: crc_pow6).  A wave step covers 512
+    // chunks: lane l loads chunks 8l..8l+7 as one 16-byte load (the chunk values are u16),
+    // combines them with a depth-3 tree (A^16, A^32, A^64), and its running register steps by
+    // A^8192 between wave steps; the lane scan then uses A^(128 * 2^j).  Loads for 4 wave
+    // steps are issued ahead of the dependent chain.
+    // SIX = false (default): the byte-sliced powers P (2 lookups and ~3 VALU per power, random
+    // banks) -- the kernel is VALU-bound, so fewer VALU beat conflict-free lookups
+    constexpr int kWords = SIX ? kCrcPHWords : kCrcPWords;
+    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kWords];
+    for (int i = threadIdx.x; i < kWords; i += kWG) s_tbl[i] = tbl[(SIX ? kCrcHOff + kCrcHWords : 0) + i];
     __syncthreads();
     const uint8_t* sPH = reinterpret_cast<const uint8_t*>(s_tbl);
+    auto pw = [&](int i, uint32_t x) {
+        if constexpr (SIX) return crc_pow6(sPH, i, x);
+        else return crc_pow(reinterpret_cast<const uint16_t*>(s_tbl), i, x);
+    };
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    const uint32_t T = (cpb + kWave - 1) / kWave;
+    constexpr uint32_t kStep = kWave * 8;  // chunks per wave step
+    const uint32_t T = (cpb + kStep - 1) / kStep;
     const uint32_t lead = uint32_t((uint64_t(cpb) * 16 - S) % kCrcOrder);  // 16*cpb - S < 16
     for (uint64_t r = uint64_t(blockIdx.x) * (kWG / kWave) + wid; r < nrows; r += nw) {
         const uint16_t* rc = chunks + r * pitch;
         uint32_t acc = 0;
-        for (uint32_t t0 = 0; t0 < T; t0 += 8) {
-            uint32_t c[8];
+        for (uint32_t t0 = 0; t0 < T; t0 += 4) {
+            u32x4 v[4];
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t ch = (t0 + i) * kWave + lane;
-                c[i] = ch < cpb ? rc[ch] : 0u;
+            for (int i = 0; i < 4; i++) {
+                const uint32_t g = (t0 + i) * kStep + 8 * lane;
+                v[i] = u32x4{0, 0, 0, 0};
+                if (t0 + i < T && g < pitch) v[i] = *reinterpret_cast<const u32x4*>(rc + g);  // pitch % 64 == 0
             }
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
+            for (int i = 0; i < 4; i++) {
                 if (t0 + i >= T) break;
-                if ((t0 + i) * kWave + lane == cpb - 1) {  // onto the grid: as if followed by 16*cpb - S zero bytes
+                const uint32_t g = (t0 + i) * kStep + 8 * lane;
+                uint32_t c[8];
 #pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if ((lead >> q) & 1) c[i] = crc_pow6(sPH, q, c[i]);
+                for (int q = 0; q < 8; q++) {
+                    c[q] = (v[i][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+                    if (g + q >= cpb) c[q] = 0;
                 }
-                acc = crc_pow6(sPH, 10, acc) ^ c[i];
+                if (g <= cpb - 1 && cpb - 1 < g + 8) {  // onto the grid: as if followed by 16*cpb - S zero bytes
+                    const uint32_t q = cpb - 1 - g;
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int e = 0; e < 8; e++) x = uint32_t(e) == q ? c[e] : x;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        if ((lead >> b) & 1) x = pw(b, x);
+#pragma unroll
+                    for (int e = 0; e < 8; e++) c[e] = uint32_t(e) == q ? x : c[e];
+                }
+                const uint32_t p0 = pw(4, c[0]) ^ c[1], p1 = pw(4, c[2]) ^ c[3];
+                const uint32_t p2 = pw(4, c[4]) ^ c[5], p3 = pw(4, c[6]) ^ c[7];
+                const uint32_t x = pw(6, pw(5, p0) ^ p1) ^ (pw(5, p2) ^ p3);
+                acc = pw(13, acc) ^ x;  // earlier wave steps move 8 KiB
             }
         }
 #pragma unroll
         for (int j = 0; j < 6; j++) {
-            const uint32_t w = crc_pow6(sPH, 4 + j, acc);
+            const uint32_t w = pw(7 + j, acc);  // 128 * 2^j bytes
             const uint32_t t = __shfl_up(w, 1u << j);
             if (lane >= (1u << j)) acc ^= t;
         }
         uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // uniform: broadcast lookups
-        int64_t e = (int64_t(S) - int64_t(T) * (kWave * 16)) % int64_t(kCrcOrder);
+        int64_t e = (int64_t(S) - int64_t(T) * (kStep * 16)) % int64_t(kCrcOrder);
         if (e < 0) e += kCrcOrder;
         for (int i = 0; e; i++, e >>= 1)
-            if (e & 1) val = crc_pow6(sPH, i, val);
+            if (e & 1) val = pw(i, val);
         if (lane == 0) out[r] = val;
     }
 }
 
-void* crc16_combine_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_kernel); }
+void* crc16_combine_kernel(bool six) {
+    return six ? reinterpret_cast<void*>(&rs_crc16_combine_kernel<true>)
+               : reinterpret_cast<void*>(&rs_crc16_combine_kernel<false>);
+}
 
 void* crc16_rows_kernel(bool aligned, int fold) {
     if (fold == 3 && aligned) return reinterpret_cast<void*>(&rs_crc16_rows_pipe_kernel);

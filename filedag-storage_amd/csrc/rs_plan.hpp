@@ -78,7 +78,7 @@ struct Crc32Shift {
     uint32_t col[32];
 };
 void* crc16_rows_kernel(bool aligned, int fold);
-void* crc16_combine_kernel();
+void* crc16_combine_kernel(bool six);
 void* crc32_rows_kernel(bool aligned, bool pipe);
 
 }  // namespace rsmi

@@ -142,8 +142,9 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
     void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &raw};
     // one wave per row up to 64 waves per CU: the combine is a dependent chain per lane, so
     // it wants many waves in flight
-    const uint32_t grid = uint32_t(std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * 16));
-    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+    const uint64_t wpc = c->opt_waves_per_cu > 0 ? uint64_t(c->opt_waves_per_cu) : 64;
+    const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * wpc / 4)));
+    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(c->opt_crc_fold == 2), dim3(grid), dim3(kWG), args, 0, st));
     return RSMI_OK;
 }
 

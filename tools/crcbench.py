@@ -67,6 +67,10 @@ def fused_vs_separate():
     raw = torch.empty((nb, n), dtype=torch.int32, device="cuda")
     b = buf.data_ptr()
     c = rsmi.Codec(k, m)
+    if WPC:
+        c.set_option("waves_per_cu", WPC)
+    if os.environ.get("CRC_COMBINE_FOLD"):  # 2: the combine kernel's six-bit powers
+        c.set_option("crc_fold", int(os.environ["CRC_COMBINE_FOLD"]))
     sh = st.cuda_stream
     V = {
         "encode only": lambda: c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh),
