@@ -35,18 +35,6 @@ Crc16Tables::Crc16Tables() {
                 const uint16_t v = P[i - 1][h][x];
                 P[i][h][x] = uint16_t(P[i - 1][0][v & 0xFF] ^ P[i - 1][1][v >> 8]);
             }
-    for (int f = 0; f < kCrcSixFields; f++)
-        for (int x = 0; x < 64; x++) {
-            uint16_t h = 0;
-            for (int k = 0; k < 6; k++) {
-                const int j = 6 * f + k;  // chunk bit j lies in byte j / 8, which is 15 - j / 8 bytes from the end
-                if ((x >> k & 1) && j < 128) h ^= U[15 - j / 8][1 << (j % 8)];
-            }
-            H[f][x] = (6 * f + 6 > 128 && x >= 4) ? 0 : h;
-        }
-    for (int i = 0; i < kCrcPowers; i++)
-        for (int k = 0; k < 3; k++)
-            for (int x = 0; x < 64; x++) PH[i][k][x] = (x << (6 * k)) < 65536 ? pow2(i, uint16_t(x << (6 * k))) : 0;
     // the group order the negative shifts rely on: A^32767 = I on a basis
     for (int bit = 0; bit < 16; bit++)
         if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();

@@ -25,18 +25,12 @@ namespace rsmi {
 
 constexpr int kCrcPowers = 15;  // A^(2^i), i < 15: any exponent mod 32767
 constexpr uint32_t kCrcOrder = 32767;
-constexpr int kCrcSixFields = 22;  // a 16-byte chunk as 21 six-bit fields and one two-bit field
 
 struct Crc16Tables {
     uint16_t T[256];                  // howeyc makeTable(IBM)
     uint16_t U[16][256];              // U[p][b] = A^p(T[b])
     uint16_t N[32][16];               // nibble tables: N[2p][v] = U[15-p][v], N[2p+1][v] = U[15-p][v << 4]
     uint16_t P[kCrcPowers][2][256];   // P[i][0][x] = A^(2^i)(x), P[i][1][x] = A^(2^i)(x << 8)
-    // six-bit tables (64 u16 = 32 dwords each, so a wave-wide lookup never bank-conflicts):
-    // H[f][x] = R of a chunk whose bits 6f..6f+5 (little-endian over the 16 bytes) are x and
-    // all others zero; PH[i][k][x] = A^(2^i)(x << 6k)
-    uint16_t H[kCrcSixFields][64];
-    uint16_t PH[kCrcPowers][3][64];
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
     // A^n(s) for any n >= 0 (reduced mod 32767)

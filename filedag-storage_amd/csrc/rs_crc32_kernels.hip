@@ -68,19 +68,14 @@ __device__ __forceinline__ uint32_t apply_lanes(uint32_t col, uint32_t s, uint32
 
 }  // namespace
 
-// tbl: NT[8][32][16] | SN[6][8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).
-// PIPE (aligned rows only; option crc32_pipe, A/B): the loop of rs_crc16_rows_pipe_kernel --
-// each wave issues its next item's 8 tile loads before it folds the current item, loads are
-// unconditional (chunks past the row's end re-read its last chunk, masked to zero in the fold).
-// Measured level with the plain loop (-3% to +5% over three row sizes and four grids), so
-// the plain loop stays the default.
-template <bool ALIGNED, bool PIPE>
+// tbl: NT[8][32][16] | SN[6][8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).  (A software-
+// pipelined loop like rs_crc16_rows_pipe_kernel's measured level with this one, -3% to +5%.)
+template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
                                                             uint64_t out_bs, Crc32Shift sh) {
-    static_assert(ALIGNED || !PIPE, "the pipelined pass needs aligned rows");
     __shared__ uint32_t s_tbl[kCrc32LdsWords];
     for (int i = threadIdx.x; i < kCrc32LdsWords; i += kWG) s_tbl[i] = tbl[i];
     __syncthreads();
@@ -95,24 +90,11 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
     auto row_of = [&](uint64_t it, uint32_t& seg, uint64_t& b, uint32_t& r) {
         seg = uint32_t(it % nseg);
         const uint64_t rid = it / nseg;
         b = rid / nrows;
         r = uint32_t(rid - b * nrows);
-    };
-    // all 8 tile loads, unconditional (PIPE)
-    auto issue = [&](uint64_t it, u32x4(&v)[kCrc32SegTiles]) {
-        uint32_t seg, r;
-        uint64_t b;
-        row_of(it, seg, b, r);
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-#pragma unroll
-        for (int i = 0; i < kCrc32SegTiles; i++) {
-            const uint64_t off = (uint64_t(seg * kCrc32SegTiles + i) * kWave + lane) * 16;
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
-        }
     };
     // fold, scan, shift to the row's end, atomic XOR
     auto finish = [&](uint64_t it, u32x4(&v)[kCrc32SegTiles]) {
@@ -125,14 +107,6 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
 #pragma unroll
         for (int i = 0; i < kCrc32SegTiles; i++) {
             if (uint32_t(i) < nt) {
-                if (PIPE && (uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
-                    const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        const int64_t n = valid - 4 * w;
-                        v[i][w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
-                    }
-                }
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     // byte offsets 4 x nibble into the 16-entry u32 tables (64 B each)
@@ -170,47 +144,31 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
         if (lane == 0) atomicXor(out + b * out_bs + r, val);
     };
     const uint64_t it0 = uint64_t(blockIdx.x) * (kWG / kWave) + wid;
-    if constexpr (PIPE) {
-        if (it0 >= nitems) return;
-        const uint64_t itmax = nitems - 1;
-        u32x4 va[kCrc32SegTiles], vb[kCrc32SegTiles];
-        issue(it0, va);
-        for (uint64_t it = it0;; it += 2 * nw) {
-            issue(it + nw < itmax ? it + nw : itmax, vb);
-            finish(it, va);
-            if (it + nw > itmax) break;
-            issue(it + 2 * nw < itmax ? it + 2 * nw : itmax, va);
-            finish(it + nw, vb);
-            if (it + 2 * nw > itmax) break;
-        }
-    } else {
-        for (uint64_t it = it0; it < nitems; it += nw) {
-            uint32_t seg, r;
-            uint64_t b;
-            row_of(it, seg, b, r);
-            const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-            const uint32_t t0 = seg * kCrc32SegTiles;
-            const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
-            u32x4 v[kCrc32SegTiles];
+    for (uint64_t it = it0; it < nitems; it += nw) {
+        uint32_t seg, r;
+        uint64_t b;
+        row_of(it, seg, b, r);
+        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+        const uint32_t t0 = seg * kCrc32SegTiles;
+        const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
+        u32x4 v[kCrc32SegTiles];
 #pragma unroll
-            for (int i = 0; i < kCrc32SegTiles; i++)
-                if (uint32_t(i) < nt) {
-                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
-                    // wave-uniform: only a row's last tile needs the per-lane bounds and masks
-                    if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
-                        v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-                    else
-                        v[i] = crc_chunk_load<ALIGNED>(row, off, S);
-                }
-            finish(it, v);
-        }
+        for (int i = 0; i < kCrc32SegTiles; i++)
+            if (uint32_t(i) < nt) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
+                // wave-uniform: only a row's last tile needs the per-lane bounds and masks
+                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+                else
+                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
+            }
+        finish(it, v);
     }
 }
 
-void* crc32_rows_kernel(bool aligned, bool pipe) {
-    if (!aligned) return reinterpret_cast<void*>(&rs_crc32_rows_kernel<false, false>);
-    return pipe ? reinterpret_cast<void*>(&rs_crc32_rows_kernel<true, true>)
-                : reinterpret_cast<void*>(&rs_crc32_rows_kernel<true, false>);
+void* crc32_rows_kernel(bool aligned) {
+    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_kernel<true>)
+                   : reinterpret_cast<void*>(&rs_crc32_rows_kernel<false>);
 }
 
 }  // namespace rsmi

@@ -30,27 +30,21 @@
 
 namespace rsmi {
 
-// Default rows in flight per lane for the software pipeline.
-// Narrow outputs (MT <= 2) keep every input row in flight (registers are cheap there,
-// measured +2.6% on RS(10,4) 1-row reconstruct); wide outputs keep a ring of 6 (D=1) or 3.
-template <int K, int MT, int D>
-constexpr int default_prefetch() {
-    constexpr int cap = MT <= 2 ? 16 : (D == 1 ? 6 : 3);
+// Rows in flight per lane for the software pipeline: narrow outputs (MT <= 2) keep every
+// input row in flight (registers are cheap there, measured +2.6% on RS(10,4) 1-row
+// reconstruct); wide outputs keep a ring of 6.
+template <int K, int MT>
+constexpr int rows_in_flight() {
+    constexpr int cap = MT <= 2 ? 16 : 6;
     return K < cap ? K : cap;
 }
 
-// K inputs, MT (<=4) outputs, D chunks of 16 B per lane per row, NT cache policy (0 = default
-// loads and stores, 1 = nontemporal loads and stores, 2 = nontemporal loads, default stores,
-// 3 = nontemporal loads, write-through sc1 buffer stores that drop the line from the L2,
-// 4 = policy 1 with the stores as nontemporal buffer stores: 32-bit lane offsets against a
-// wave-uniform descriptor instead of 64-bit lane addresses),
-// PF rows in flight per lane (0 = default_prefetch), WPS waves per SIMD the register
-// allocation must allow.
-// TS: table source.  0 = all five field words per output from LDS (broadcast
-// ds_read_b128); 1 = fields 0 and 2 from LDS, fields 1, 3 and 4 by scalar loads into SGPRs
-// (each v_perm takes one SGPR operand), cutting the LDS return traffic by 3/5.
-// UA: rows at any byte alignment and pitch (S >= 16; D = 1).  A lane's 16-byte window starts
-// at min(16*ch, S - 16): the row's last window overlaps the one before it instead of running
+// K inputs, MT (<= 4) outputs, one 16-byte chunk per lane per row.
+// NT: cache policy, 1 = nontemporal loads and stores (write-heavy tiles), 2 = nontemporal
+// loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.
+// WPS: waves per SIMD the register allocation must allow.
+// UA: rows at any byte alignment and pitch (S >= 16).  A lane's 16-byte window starts at
+// min(16*ch, S - 16): the row's last window overlaps the one before it instead of running
 // past S, so loads never leave [0, S) and every store is a whole 16-byte window (the
 // overlapped bytes get the same value from both lanes).  This serves the Split layout itself
 // (rows back to back at pitch S, odd for RS(10,4)) and page-locked host memory read and
@@ -59,24 +53,19 @@ constexpr int default_prefetch() {
 // values (crc16.hpp: R of the chunk's bytes relative to the chunk's end, nibble tables) and
 // store them as u16 at crc_out[(block * crc_slots + shard) * tpb * 64 + chunk]; input row c is
 // shard in_row[c], output row j is shard crc_out_slot0 + out_row[j].  rs_crc16_combine_kernel
-// turns them into R(row).  The small host path uses this so the shard bytes cross PCIe once.
-// SH64: build the shifted selector words of two dwords with one 64-bit shift each
-// (v_lshrrev_b64; the bits that cross from the high dword land in masked-off positions).
-// SP >= 0 (aligned layouts, A/B): whole output chunks leave by buffer stores with these cache
-// bits (aux: 1 = sc0, 2 = nt, 16 = sc1, 17 = sc0 sc1, 18 = nt sc1); -1 = the NT policy.
-// xcd_order (argument): XCD-grouped tile order.  The dispatcher sends workgroup b to XCD
-// b mod 8; with xcd_order set, workgroups are renumbered so that each XCD takes one
-// contiguous eighth of the tiles.
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false, bool SH64 = false, int SP = -1>
+// turns them into R(row).
+// Launch geometry: one tile per wave; the loop strides over further tiles only
+// when the caller caps the grid (option waves_per_cu).
+template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                        uint32_t ntiles, const uint32_t* __restrict__ crc_tbl,
                                                        uint16_t* __restrict__ crc_out, uint32_t crc_slots,
-                                                       uint32_t crc_out_slot0, uint32_t xcd_order) {
-    static_assert(!CRC || (UA && D == 1), "fused chunk CRCs: unaligned-window kernels only");
+                                                       uint32_t crc_out_slot0) {
+    static_assert(!CRC || UA, "fused chunk CRCs: unaligned-window kernels only");
+    static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
     __shared__ uint32_t s_crc[CRC ? kCrcNWords : 1];
     {
@@ -84,7 +73,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
         for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
         if constexpr (CRC)
-            for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_crc[i] = crc_tbl[kCrcPWords + kCrcUWords + i];
+            for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_crc[i] = crc_tbl[kCrcPWords + i];
     }
     __syncthreads();
 
@@ -92,15 +81,10 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t nw = gridDim.x * kWavesPerWG;
-    uint32_t bid = blockIdx.x;
-    if (xcd_order) {  // bijection on [0, gridDim.x): XCD x gets the x-th contiguous share
-        const uint32_t g = gridDim.x, x = bid % 8u, q = g / 8u, r = g % 8u;
-        bid = x * q + (x < r ? x : r) + bid / 8u;
-    }
-    uint32_t t = bid * kWavesPerWG + wid;
+    uint32_t t = blockIdx.x * kWavesPerWG + wid;
     if (t >= ntiles) return;
 
-    constexpr int P = PF == 0 ? default_prefetch<K, MT, D>() : (PF < K ? PF : K);  // rows in flight per lane
+    constexpr int P = rows_in_flight<K, MT>();
     uint64_t in_off[K], out_off[MT];
 #pragma unroll
     for (int c = 0; c < K; c++) in_off[c] = uint64_t(plan->in_row[c]) * in_rs;
@@ -116,30 +100,22 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #ifndef RSMI_DIAG_CACHED
         const uint8_t* ib = in + uint64_t(blk) * in_bs;
         uint8_t* ob = out + uint64_t(blk) * out_bs;
-        const uint32_t ch0 = tib * (kWave * D) + lane;
 #else  // diagnostic build (tools/Makefile diag-cached): tiles wrap onto the first 16
        // blocks (~7 MB, cache-resident), so the kernel's own issue rate (VALU, LDS, waits)
        // is what the launch time shows
         const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
         uint8_t* ob = out + uint64_t(blk & 15) * out_bs;
-        const uint32_t ch0 = tib * (kWave * D) + lane;
 #endif
-        uint32_t chl[D];  // load chunk, clamped: every lane's loads stay unconditional
-#pragma unroll
-        for (int d = 0; d < D; d++) {
-            const uint32_t ch = ch0 + kWave * d;
-            chl[d] = ch < cpb ? ch : cpb - 1;
-        }
-        uint32_t win[D];  // UA: byte offset of the lane's 16-byte window
-#pragma unroll
-        for (int d = 0; d < D; d++) win[d] = UA ? (chl[d] * 16u < S - 16u ? chl[d] * 16u : S - 16u) : 0u;
-        // CRC: the lane's chunk of one row -> u16 chunk value (bytes of the window before the
-        // chunk's start -- only in the row's overlapping last window -- count as zero)
-        // leading bytes of the lane's window that belong to the previous chunk (the last
-        // window only), as per-dword keep masks; branch-free so the folds stay in straight code
+        const uint32_t ch = tib * kWave + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;  // load chunk, clamped: loads stay unconditional
+        // UA: byte offset of the lane's 16-byte window
+        const uint32_t win = UA ? (chl * 16u < S - 16u ? chl * 16u : S - 16u) : 0u;
+        // CRC: leading bytes of the lane's window that belong to the previous chunk (the last
+        // window only) count as zero, as per-dword keep masks; branch-free so the folds stay in
+        // straight code
         u32x4 keep = {~0u, ~0u, ~0u, ~0u};
         if constexpr (CRC) {
-            const int lead = int(chl[0] * 16u - win[0]);
+            const int lead = int(chl * 16u - win);
 #pragma unroll
             for (int w = 0; w < 4; w++) {
                 const int nb = lead - 4 * w;
@@ -148,55 +124,50 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         }
         uint16_t* crc_tile = nullptr;  // this lane's chunk slot in shard 0 of the tile's block
         if constexpr (CRC) {
-            crc_tile = crc_out + uint64_t(blk) * crc_slots * (uint64_t(tpb) * kWave) + ch0;
+            crc_tile = crc_out + uint64_t(blk) * crc_slots * (uint64_t(tpb) * kWave) + ch;
             asm volatile("" : "+v"(crc_tile));
         }
         auto crc_store = [&](u32x4 x, uint32_t shard) {
             if constexpr (CRC) {
-                {
-                    x &= keep;
-                    const uint8_t* nbt = reinterpret_cast<const uint8_t*>(s_crc);
-                    uint32_t cr = 0;
+                x &= keep;
+                const uint8_t* nbt = reinterpret_cast<const uint8_t*>(s_crc);
+                uint32_t cr = 0;
 #pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        uint32_t lo = (x[w] << 1) & 0x1E1E1E1Eu, hi = (x[w] >> 3) & 0x1E1E1E1Eu;
-                        asm volatile("" : "+v"(lo), "+v"(hi));
-                        uint32_t l[8];
+                for (int w = 0; w < 4; w++) {
+                    uint32_t lo = (x[w] << 1) & 0x1E1E1E1Eu, hi = (x[w] >> 3) & 0x1E1E1E1Eu;
+                    asm volatile("" : "+v"(lo), "+v"(hi));
+                    uint32_t l[8];
 #pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const int p = 4 * w + q;
-                            l[2 * q] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + ((lo >> (8 * q)) & 0xFF));
-                            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
-                        }
-                        cr = xor3(cr, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+                    for (int q = 0; q < 4; q++) {
+                        const int p = 4 * w + q;
+                        l[2 * q] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + ((lo >> (8 * q)) & 0xFF));
+                        l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
                     }
-                    // unconditional: lanes past the row's end own padding slots (chunk pitch
-                    // tpb * 64), so no branch splits the column loop (a branch there lets the
-                    // compiler sink every column's GF math past it)
-                    crc_tile[uint64_t(shard) * (uint64_t(tpb) * kWave)] = uint16_t(cr);
+                    cr = xor3(cr, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
                 }
+                // unconditional: lanes past the row's end own padding slots (chunk pitch
+                // tpb * 64), so no branch splits the column loop (a branch there lets the
+                // compiler sink every column's GF math past it)
+                crc_tile[uint64_t(shard) * (uint64_t(tpb) * kWave)] = uint16_t(cr);
             }
         };
-        auto load_col = [&](int c, u32x4 (&dst)[D]) {
-#pragma unroll
-            for (int d = 0; d < D; d++) {
-                if constexpr (UA)
-                    dst[d] = ld16u<NT != 0>(ib + in_off[c] + win[d]);
-                else
-                    dst[d] = ld16<NT != 0>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl[d]);
-            }
+        auto load_col = [&](int c) {
+            if constexpr (UA)
+                return ld16u<true>(ib + in_off[c] + win);
+            else
+                return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl);
         };
 
         // Software pipeline over the K input rows: a ring of P rows in flight, one
         // scheduling region per row (sched_barrier) so the compiler cannot hoist every
         // load and table read to the top and blow the 128-VGPR budget.
-        u32x4 v[P][D];
+        u32x4 v[P];
 #pragma unroll
-        for (int c = 0; c < P; c++) load_col(c, v[c]);
+        for (int c = 0; c < P; c++) v[c] = load_col(c);
 
         // acc ^= p1^p2^p3 per column, folded two columns at a time with 3-input XORs:
         // even columns leave p3 pending, odd columns retire it (1.5 VALU per column).
-        uint32_t acc[MT][4 * D], pend[MT][4 * D];
+        uint32_t acc[MT][4], pend[MT][4];
 
         // Opaque per-tile table base: stops LICM from hoisting all K*20 table words out
         // of the tile loop (which would pin ~200 VGPRs and drop occupancy to 1 wave).
@@ -204,23 +175,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         asm volatile("" : "+v"(tb));
         const u32x4* tbl = s_tbl + tb;
         u32x4 Tn[5];
-        auto load_tables = [&](int c, u32x4 (&dst)[5]) {
-            if constexpr (TS == 0) {
 #pragma unroll
-                for (int f = 0; f < 5; f++) dst[f] = tbl[c * 5 + f];
-            } else {
-                dst[0] = tbl[c * 5 + 0];
-                dst[2] = tbl[c * 5 + 2];
-                const u32x4* g = reinterpret_cast<const u32x4*>(plan->tbl) + c * 5;
-#pragma unroll
-                for (int f : {1, 3, 4}) {
-                    const u32x4 w = g[f];  // uniform address: s_load_dwordx4
-#pragma unroll
-                    for (int j = 0; j < 4; j++) dst[f][j] = __builtin_amdgcn_readfirstlane(w[j]);
-                }
-            }
-        };
-        load_tables(0, Tn);
+        for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
 
 #pragma unroll
         for (int c = 0; c < K; c++) {
@@ -229,62 +185,41 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
             for (int f = 0; f < 5; f++) T[f] = Tn[f];
 #pragma unroll
-            for (int d = 0; d < D; d++) {
-                uint32_t sh3[4], sh6[4];
-                if constexpr (SH64) {
+            for (int w = 0; w < 4; w++) {
+                const uint32_t x = u4get(v[slot], w);
+                const uint32_t s1 = x & 0x07070707u;
+                const uint32_t s2 = (x >> 3) & 0x07070707u;
+                const uint32_t s3 = (x >> 6) & 0x03030303u;
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint64_t xx = (uint64_t(u4get(v[slot][d], 2 * h + 1)) << 32) | u4get(v[slot][d], 2 * h);
-                        uint64_t a = xx >> 3, b = xx >> 6;
-                        asm volatile("" : "+v"(a), "+v"(b));  // keep them 64-bit shifts
-                        sh3[2 * h] = uint32_t(a);
-                        sh3[2 * h + 1] = uint32_t(a >> 32);
-                        sh6[2 * h] = uint32_t(b);
-                        sh6[2 * h + 1] = uint32_t(b >> 32);
-                    }
-                }
-#pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    const uint32_t x = u4get(v[slot][d], w);
-                    const uint32_t s1 = x & 0x07070707u;
-                    const uint32_t s2 = (SH64 ? sh3[w] : x >> 3) & 0x07070707u;
-                    const uint32_t s3 = (SH64 ? sh6[w] : x >> 6) & 0x03030303u;
-#pragma unroll
-                    for (int j = 0; j < MT; j++) {
-#ifndef RSMI_DIAG_NOMATH
-                        const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
-                        const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
-                        const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
-#else  // diagnostic build (tools/Makefile, never the product): same loads, ring, table reads
-       // and stores, GF products replaced by one XOR per (output, input) dword
-                        const uint32_t p1 = x ^ u4get(T[0], j), p2 = u4get(T[1], j) ^ u4get(T[2], j) ^ s1,
-                                       p3 = u4get(T[3], j) ^ u4get(T[4], j) ^ s2 ^ s3;
-#endif
-                        uint32_t& a = acc[j][d * 4 + w];
-                        uint32_t& q = pend[j][d * 4 + w];
-                        if constexpr (!PAIR) {
-                            a = c == 0 ? p1 ^ p2 ^ p3 : xor3(a, p1, p2) ^ p3;
-                        } else if (c == 0 && K == 1) {
-                            a = xor3(p1, p2, p3);
-                        } else if (c == 0) {
-                            a = p1 ^ p2;
-                            q = p3;
-                        } else if (c & 1) {
-                            a = xor3(a, p1, p2);
-                            a = xor3(a, p3, q);
-                        } else if (c == K - 1) {
-                            a = xor3(a, p1, p2);
-                            a ^= p3;
-                        } else {
-                            a = xor3(a, p1, p2);
-                            q = p3;
-                        }
+                for (int j = 0; j < MT; j++) {
+                    const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
+                    const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
+                    const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
+                    uint32_t& a = acc[j][w];
+                    uint32_t& q = pend[j][w];
+                    if (c == 0 && K == 1) {
+                        a = xor3(p1, p2, p3);
+                    } else if (c == 0) {
+                        a = p1 ^ p2;
+                        q = p3;
+                    } else if (c & 1) {
+                        a = xor3(a, p1, p2);
+                        a = xor3(a, p3, q);
+                    } else if (c == K - 1) {
+                        a = xor3(a, p1, p2);
+                        a ^= p3;
+                    } else {
+                        a = xor3(a, p1, p2);
+                        q = p3;
                     }
                 }
             }
-            if constexpr (CRC) crc_store(v[slot][0], plan->in_row[c]);
-            if (c + P < K) load_col(c + P, v[slot]);
-            if (c + 1 < K) load_tables(c + 1, Tn);
+            if constexpr (CRC) crc_store(v[slot], plan->in_row[c]);
+            if (c + P < K) v[slot] = load_col(c + P);
+            if (c + 1 < K) {
+#pragma unroll
+                for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         // Anchor the results outside the store predicate; otherwise the compiler sinks the
@@ -292,52 +227,44 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
         for (int j = 0; j < MT; j++)
 #pragma unroll
-            for (int w = 0; w < 4 * D; w++) asm volatile("" : "+v"(acc[j][w]));
+            for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
 
+        if (UA && ch < cpb) {
 #pragma unroll
-        for (int d = 0; d < D; d++) {
-            const uint32_t ch = ch0 + kWave * d;
-            if (UA && ch < cpb) {
+            for (int j = 0; j < MT; j++) {
+                const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                st16u<NT == 1>(ob + out_off[j] + win, o);
+                if constexpr (CRC) {
+                    crc_store(o, crc_out_slot0 + plan->out_row[j]);
+                    __builtin_amdgcn_sched_barrier(0);  // one row's 32 table reads in flight at a time
+                }
+            }
+        } else if (!UA && ch < cpb) {
+            const uint32_t boff = ch * 16u;
+            if (boff + 16u <= S) {
 #pragma unroll
                 for (int j = 0; j < MT; j++) {
-                    const u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
-                    st16u<NT == 1>(ob + out_off[j] + win[d], o);
-                    if constexpr (CRC) {
-                        crc_store(o, crc_out_slot0 + plan->out_row[j]);
-                        __builtin_amdgcn_sched_barrier(0);  // one row's 32 table reads in flight at a time
-                    }
+                    const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                    if constexpr (NT == 1)
+                        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                    else
+                        *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
                 }
-            } else if (!UA && ch < cpb) {
-                const uint32_t boff = ch * 16u;
-                if (boff + 16u <= S) {
+            } else {
+                // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
 #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        u32x4 o = u32x4{acc[j][d * 4 + 0], acc[j][d * 4 + 1], acc[j][d * 4 + 2], acc[j][d * 4 + 3]};
-                        constexpr int kSP = SP >= 0 ? SP : (NT == 3 ? 16 : NT == 4 ? 2 : -1);
-                        if constexpr (kSP >= 0) {
-                            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ob + out_off[j], 0, 0x7FFFFFFF, 0x00020000);
-                            __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, int(boff), 0, kSP);
-                        } else if constexpr (NT == 1)
-                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
-                        else
-                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
-                    }
-                } else {
-                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+                for (int j = 0; j < MT; j++) {
+                    uint8_t* p = ob + out_off[j] + boff;
 #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        uint8_t* p = ob + out_off[j] + boff;
-#pragma unroll
-                        for (int w = 0; w < 4; w++) {
-                            const uint32_t val = acc[j][d * 4 + w];
-                            const uint32_t o = boff + 4u * w;
-                            if (o + 4u <= S) {
-                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
-                            } else if (o < S) {
-                                p[4 * w] = uint8_t(val);
-                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
-                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
-                            }
+                    for (int w = 0; w < 4; w++) {
+                        const uint32_t val = acc[j][w];
+                        const uint32_t o = boff + 4u * w;
+                        if (o + 4u <= S) {
+                            *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                        } else if (o < S) {
+                            p[4 * w] = uint8_t(val);
+                            if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                            if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
                         }
                     }
                 }
@@ -436,10 +363,9 @@ void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 // R(row) of the datanode entry checksum (crc16.hpp has the algebra).  A wave owns one
 // segment of kCrcSegTiles consecutive 1 KiB tiles of one row: each lane loads its 16-byte
 // chunk of every tile (all loads in flight first), folds each chunk with positional LDS
-// lookups -- 32 nibble lookups in 16-entry tables (FOLD 1: every wave-wide lookup reads 8
-// distinct dwords in 8 distinct banks, so it never conflicts) or 16 byte lookups in
-// 256-entry tables (FOLD 0: random banks) -- and carries a running register across the
-// tiles (A^1024 between tiles).  A
+// lookups -- 32 nibble lookups in 16-entry tables (every wave-wide lookup reads 8 distinct
+// dwords in 8 distinct banks, so it never conflicts) -- and carries a running register
+// across the tiles (A^1024 between tiles).  A
 // Hillis-Steele scan over the 64 lanes (A^(16*2^j) per level) leaves the segment's value,
 // relative to the segment's end, in lane 63; shifting it by (S - segment end) mod 32767
 // bytes places it relative to the row's end, and one atomic XOR adds it into the row's
@@ -449,20 +375,36 @@ __device__ __forceinline__ uint32_t crc_pow(const uint16_t* sP, int i, uint32_t 
     return uint32_t(sP[i * 512 + (s & 0xFF)]) ^ uint32_t(sP[i * 512 + 256 + (s >> 8)]);
 }
 
-template <bool ALIGNED, int FOLD>
+__device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4& v) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint32_t lo = (v[w] << 1) & 0x1E1E1E1Eu, hi = (v[w] >> 3) & 0x1E1E1E1Eu;
+        asm volatile("" : "+v"(lo), "+v"(hi));
+        uint32_t l[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int p = 4 * w + q;
+            l[2 * q] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + ((lo >> (8 * q)) & 0xFF));
+            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
+        }
+        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+    }
+    return c;
+}
+
+template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
                                                             uint64_t out_bs) {
-    constexpr int kFoldWords = FOLD == 0 ? kCrcUWords : kCrcNWords;
-    constexpr int kFoldOff = FOLD == 0 ? kCrcPWords : kCrcPWords + kCrcUWords;
-    __shared__ uint32_t s_tbl[kCrcPWords + kFoldWords];
+    __shared__ uint32_t s_tbl[kCrcPWords + kCrcNWords];
     for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
-    for (int i = threadIdx.x; i < kFoldWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kFoldOff + i];
+    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + i];
     __syncthreads();
     const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
-    const uint16_t* sF = sP + kCrcPWords * 2;  // U[16][256] or N[32][16]
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sP + kCrcPWords * 2);  // N[32][16]
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -490,30 +432,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
 #pragma unroll
         for (int i = 0; i < kCrcSegTiles; i++) {
             if (uint32_t(i) < nt) {
-                uint32_t c = 0;
-                if constexpr (FOLD == 0) {
-#pragma unroll
-                    for (int p = 0; p < 16; p++) c ^= sF[(15 - p) * 256 + ((v[i][p >> 2] >> (8 * (p & 3))) & 0xFF)];
-                } else {
-                    // nibble byte offsets into the u16 tables (2 x nibble), one dword at a time
-                    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sF);
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        uint32_t lo = (v[i][w] << 1) & 0x1E1E1E1Eu, hi = (v[i][w] >> 3) & 0x1E1E1E1Eu;
-                        // opaque: keeps the two masks (else the compiler re-derives a shift
-                        // and an AND per nibble), so each offset is one byte extract
-                        asm volatile("" : "+v"(lo), "+v"(hi));
-                        uint32_t l[8];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const int p = 4 * w + q;
-                            l[2 * q] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + ((lo >> (8 * q)) & 0xFF));
-                            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
-                        }
-                        // 8 lookups into the register with four 3-input XORs
-                        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
-                    }
-                }
+                const uint32_t c = crc_nib_chunk(nb, v[i]);
                 acc = crc_pow(sP, 10, acc) ^ c;  // previous tiles move 1 KiB further from the end
             }
         }
@@ -533,121 +452,13 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
     }
 }
 
-// FOLD 2 of the CRC-16 rows pass: the item shape of rs_crc16_rows_kernel, but every lookup
-// goes to a 64-entry u16 table (32 dwords: the 32 lanes of a ds_read_b32 half-wave hit at most
-// one dword per bank, so no lookup conflicts).  A chunk folds with 22 H lookups (21 six-bit
-// fields and a two-bit one, across its 128 bits) instead of 32 nibble lookups; the tile step
-// (A^1024) and the lane scan apply their powers six bits at a time (3 conflict-free lookups
-// where the byte tables took 2 with random banks); and lane 63's value is made wave-uniform
-// before the end shift, so those lookups are broadcasts.  Measured level with FOLD 1: the
-// kernel is bound by VALU issue and latency, not LDS.
-__device__ __forceinline__ uint32_t crc_pow6(const uint8_t* ph, int i, uint32_t s) {
-    const uint8_t* t = ph + i * 384;
-    return uint32_t(*reinterpret_cast<const uint16_t*>(t + ((s << 1) & 0x7E))) ^
-           uint32_t(*reinterpret_cast<const uint16_t*>(t + 128 + ((s >> 5) & 0x7E))) ^
-           uint32_t(*reinterpret_cast<const uint16_t*>(t + 256 + ((s >> 11) & 0x7E)));
-}
-
-// byte offset 2 * (bits 6f..6f+5 of the chunk) into the 64-entry u16 table of field f
-template <int F>
-__device__ __forceinline__ uint32_t six_off(const u32x4& v) {
-    constexpr int o = 6 * F, d = o / 32, sh = o % 32;
-    if constexpr (F == kCrcSixFields - 1) {
-        return (v[3] >> 29) & 0x6u;  // bits 126, 127
-    } else if constexpr (sh == 0) {
-        return (v[d] << 1) & 0x7Eu;
-    } else if constexpr (sh + 6 <= 32) {
-        return (v[d] >> (sh - 1)) & 0x7Eu;
-    } else {
-        return __builtin_amdgcn_alignbit(v[d + 1], v[d], sh - 1) & 0x7Eu;
-    }
-}
-
-template <int F>
-__device__ __forceinline__ uint32_t six_fold(const uint8_t* h, const u32x4& v) {
-    const uint32_t x = *reinterpret_cast<const uint16_t*>(h + 128 * F + six_off<F>(v));
-    if constexpr (F + 1 < kCrcSixFields) return x ^ six_fold<F + 1>(h, v);
-    else return x;
-}
-
-template <bool ALIGNED>
-__global__ __launch_bounds__(kWG) void rs_crc16_rows6_kernel(const uint32_t* __restrict__ tbl,
-                                                             const uint8_t* __restrict__ base, uint64_t bstride,
-                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
-                                                             uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
-                                                             uint64_t out_bs) {
-    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcHWords + kCrcPHWords];
-    for (int i = threadIdx.x; i < kCrcHWords + kCrcPHWords; i += kWG) s_tbl[i] = tbl[kCrcHOff + i];
-    __syncthreads();
-    const uint8_t* sH = reinterpret_cast<const uint8_t*>(s_tbl);
-    const uint8_t* sPH = sH + kCrcHWords * 4;
-
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
-        const uint32_t seg = uint32_t(it % nseg);
-        const uint64_t rid = it / nseg;
-        const uint64_t b = rid / nrows;
-        const uint32_t r = uint32_t(rid - b * nrows);
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-        const uint32_t t0 = seg * kCrcSegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
-        u32x4 v[kCrcSegTiles];
-#pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++)
-            if (uint32_t(i) < nt) {
-                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
-                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-                else
-                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
-            }
-        uint32_t acc = 0;
-#pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++)
-            if (uint32_t(i) < nt) acc = crc_pow6(sPH, 10, acc) ^ six_fold<0>(sH, v[i]);  // earlier tiles move 1 KiB
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const uint32_t w = crc_pow6(sPH, 4 + j, acc);  // 16 * 2^j bytes
-            const uint32_t t = __shfl_up(w, 1u << j);
-            if (lane >= (1u << j)) acc ^= t;
-        }
-        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));
-        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
-        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
-        if (e < 0) e += kCrcOrder;
-        for (int i = 0; e; i++, e >>= 1)
-            if (e & 1) val = crc_pow6(sPH, i, val);
-        if (lane == 0) atomicXor(out + b * out_bs + r, val);
-    }
-}
-
-// FOLD 3: the FOLD 1 (nibble) rows pass, software-pipelined, for 16-byte-aligned rows.  A wave
+// The nibble rows pass, software-pipelined, for 16-byte-aligned rows (the default).  A wave
 // issues the 8 tile loads of its next item before it folds the current one (two register sets,
 // the loop unrolled by two), so its own fold covers the next item's memory latency instead of
 // only the other waves on the SIMD.  Loads are unconditional -- chunks past the row's end read
 // the row's last chunk and are masked to zero in the fold, and the prefetch past the last item
 // re-reads that item -- so no load sits behind a branch and the compiler's vmcnt waits count
 // only the older set.
-__device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4& v) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        uint32_t lo = (v[w] << 1) & 0x1E1E1E1Eu, hi = (v[w] >> 3) & 0x1E1E1E1Eu;
-        asm volatile("" : "+v"(lo), "+v"(hi));
-        uint32_t l[8];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int p = 4 * w + q;
-            l[2 * q] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + ((lo >> (8 * q)) & 0xFF));
-            l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nb + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
-        }
-        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
-    }
-    return c;
-}
-
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
@@ -655,7 +466,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
                                                                  uint32_t* __restrict__ out, uint64_t out_bs) {
     __shared__ uint32_t s_tbl[kCrcPWords + kCrcNWords];
     for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
-    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + kCrcUWords + i];
+    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + i];
     __syncthreads();
     const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
     const uint8_t* nb = reinterpret_cast<const uint8_t*>(sP + kCrcPWords * 2);
@@ -728,32 +539,21 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 }
 
 // R(row) from the fused kernels' per-chunk values (rs_fast_kernel CRC): one wave per row.
-// Lane l folds chunks 8l..8l+7, 512 + 8l.., ... (A^8192 between wave steps), a lane scan
-// combines the lanes (A^(128*2^j)), and lane 63 shifts the total from the 8 KiB grid end to
-// the row end.  The
-// row's last chunk is relative to S (its window ends at S), so it first moves onto the
-// 16-byte grid by A^(16*cpb - S).  out[row] is written once (host memory allowed).
-template <bool SIX>
+// A wave step covers 512 chunks: lane l loads chunks 8l..8l+7 as one 16-byte load (the chunk
+// values are u16), combines them with a depth-3 tree (A^16, A^32, A^64), and its running
+// register steps by A^8192 between wave steps; a lane scan then combines the lanes
+// (A^(128*2^j)), and lane 63 shifts the total from the 8 KiB grid end to the row end.  Loads
+// for 4 wave steps are issued ahead of the dependent chain.  The row's last chunk is relative
+// to S (its window ends at S), so it first moves onto the 16-byte grid by A^(16*cpb - S).
+// out[row] is written once (host memory allowed).
 __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* __restrict__ tbl,
                                                                const uint16_t* __restrict__ chunks, uint32_t cpb,
                                                                uint32_t pitch, uint64_t S, uint64_t nrows,
                                                                uint32_t* __restrict__ out) {
-    // six-bit power tables PH (5.6 KiB, conflict-free: crc_pow6).  A wave step covers 512
-    // chunks: lane l loads chunks 8l..8l+7 as one 16-byte load (the chunk values are u16),
-    // combines them with a depth-3 tree (A^16, A^32, A^64), and its running register steps by
-    // A^8192 between wave steps; the lane scan then uses A^(128 * 2^j).  Loads for 4 wave
-    // steps are issued ahead of the dependent chain.
-    // SIX = false (default): the byte-sliced powers P (2 lookups and ~3 VALU per power, random
-    // banks) -- the kernel is VALU-bound, so fewer VALU beat conflict-free lookups
-    constexpr int kWords = SIX ? kCrcPHWords : kCrcPWords;
-    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kWords];
-    for (int i = threadIdx.x; i < kWords; i += kWG) s_tbl[i] = tbl[(SIX ? kCrcHOff + kCrcHWords : 0) + i];
+    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcPWords];
+    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
     __syncthreads();
-    const uint8_t* sPH = reinterpret_cast<const uint8_t*>(s_tbl);
-    auto pw = [&](int i, uint32_t x) {
-        if constexpr (SIX) return crc_pow6(sPH, i, x);
-        else return crc_pow(reinterpret_cast<const uint16_t*>(s_tbl), i, x);
-    };
+    auto pw = [&](int i, uint32_t x) { return crc_pow(reinterpret_cast<const uint16_t*>(s_tbl), i, x); };
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
@@ -813,134 +613,49 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
     }
 }
 
-void* crc16_combine_kernel(bool six) {
-    return six ? reinterpret_cast<void*>(&rs_crc16_combine_kernel<true>)
-               : reinterpret_cast<void*>(&rs_crc16_combine_kernel<false>);
-}
+void* crc16_combine_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_kernel); }
 
-void* crc16_rows_kernel(bool aligned, int fold) {
-    if (fold == 3 && aligned) return reinterpret_cast<void*>(&rs_crc16_rows_pipe_kernel);
-    if (fold == 3) fold = 1;  // the pipelined pass needs aligned rows
-    if (fold == 2)
-        return aligned ? reinterpret_cast<void*>(&rs_crc16_rows6_kernel<true>)
-                       : reinterpret_cast<void*>(&rs_crc16_rows6_kernel<false>);
-    if (fold == 0)
-        return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 0>)
-                       : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false, 0>);
-    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_kernel<true, 1>)
-                   : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false, 1>);
+// aligned rows: the pipelined pass; any other layout: the plain nibble pass
+void* crc16_rows_kernel(bool aligned) {
+    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_pipe_kernel)
+                   : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false>);
 }
 
 // ------------------------------------------------------------------ dispatch table
-template <int K, int MT, int D, int NT, int PF = 0, bool PAIR = true, int WPS = kMinWavesPerSimd, int TS = 0,
-          bool UA = false, bool CRC = false, bool SH64 = false, int SP = -1>
-static void* fast_ptr() {
-    return reinterpret_cast<void*>(&rs_fast_kernel<K, MT, D, NT, PF, PAIR, WPS, TS, UA, CRC, SH64, SP>);
-}
-
-// fused chunk-CRC variants: UA, D = 1, the auto cache policy of the shape
+// One kernel per (K, MT) and layout, with the cache policy of the shape (auto_cache_policy in
+// rsmi_core.cpp): nontemporal stores unless the tile reads at least 4 rows per row it writes.
 constexpr int auto_nt(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
+
 template <int K, int MT>
-static void* crc_ptr() {
-    // 2 waves/SIMD: the chunk folds need registers beyond the 128 the streaming kernels keep
-    // to, and these serve latency-bound small calls, not HBM streams
-    return fast_ptr<K, MT, 1, auto_nt(K, MT), 0, true, 2, 0, true, true>();
+static void fill_km(FastKernelTable& t) {
+    constexpr int NT = auto_nt(K, MT);
+    t.fn[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT>);
+    t.ua[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true>);
+    // 2 waves/SIMD: the chunk folds need registers beyond the 128 the streaming kernels keep to
+    t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, 2, true, true>);
 }
 
-template <int K, int D, int NT>
-static void fill_k(FastKernelTable& t) {
-    t.fn[K][1][D][NT] = fast_ptr<K, 1, D, NT>();
-    t.fn[K][2][D][NT] = fast_ptr<K, 2, D, NT>();
-    t.fn[K][3][D][NT] = fast_ptr<K, 3, D, NT>();
-    t.fn[K][4][D][NT] = fast_ptr<K, 4, D, NT>();
-}
-
-// unaligned-layout kernels: D = 1, cache policy 1 (write-heavy tiles) or 2 (read-heavy)
 template <int K>
-static void fill_ua(FastKernelTable& t) {
-    t.ua[K][1][1] = fast_ptr<K, 1, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][2][1] = fast_ptr<K, 2, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][3][1] = fast_ptr<K, 3, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][4][1] = fast_ptr<K, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][1][2] = fast_ptr<K, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][2][2] = fast_ptr<K, 2, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][3][2] = fast_ptr<K, 3, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua[K][4][2] = fast_ptr<K, 4, 1, 2, 0, true, kMinWavesPerSimd, 0, true>();
-    t.ua_crc[K][1] = crc_ptr<K, 1>();
-    t.ua_crc[K][2] = crc_ptr<K, 2>();
-    t.ua_crc[K][3] = crc_ptr<K, 3>();
-    t.ua_crc[K][4] = crc_ptr<K, 4>();
-}
-
-template <int D, int NT>
-static void fill_d(FastKernelTable& t) {
-    fill_k<1, D, NT>(t);
-    fill_k<2, D, NT>(t);
-    fill_k<3, D, NT>(t);
-    fill_k<4, D, NT>(t);
-    fill_k<5, D, NT>(t);
-    fill_k<6, D, NT>(t);
-    fill_k<8, D, NT>(t);
-    fill_k<10, D, NT>(t);
-    fill_k<12, D, NT>(t);
-    fill_k<16, D, NT>(t);
-}
-
-// A/B variants of the RS(10,4) encode / 1-row reconstruct shapes (rsmi_set_option "prefetch")
-const ExpKernelTable& exp_kernels() {
-    static const ExpKernelTable t = [] {
-        ExpKernelTable x{};
-        x.fn[0][0] = fast_ptr<10, 4, 1, 1, 4>();
-        x.fn[0][1] = fast_ptr<10, 4, 1, 1, 8>();
-        x.fn[0][2] = fast_ptr<10, 4, 1, 1, 10>();
-        x.fn[1][0] = fast_ptr<10, 1, 1, 1, 4>();
-        x.fn[1][1] = fast_ptr<10, 1, 1, 1, 8>();
-        x.fn[1][2] = fast_ptr<10, 1, 1, 1, 10>();
-        x.fn[0][3] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 1>();
-        x.fn[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 1>();
-        x.fn[0][4] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, true>();
-        x.fn[1][4] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, true>();
-        // store cache bits (option store_aux), in the order of kStoreAux
-        x.st[0][0] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 0>();
-        x.st[0][1] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 1>();
-        x.st[0][2] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 2>();
-        x.st[0][3] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 16>();
-        x.st[0][4] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 17>();
-        x.st[0][5] = fast_ptr<10, 4, 1, 1, 0, true, kMinWavesPerSimd, 0, false, false, false, 18>();
-        x.st[1][0] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 0>();
-        x.st[1][1] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 1>();
-        x.st[1][2] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 2>();
-        x.st[1][3] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 16>();
-        x.st[1][4] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 17>();
-        x.st[1][5] = fast_ptr<10, 1, 1, 2, 0, true, kMinWavesPerSimd, 0, false, false, false, 18>();
-        return x;
-    }();
-    return t;
+static void fill_k(FastKernelTable& t) {
+    fill_km<K, 1>(t);
+    fill_km<K, 2>(t);
+    fill_km<K, 3>(t);
+    fill_km<K, 4>(t);
 }
 
 const FastKernelTable& fast_kernels() {
     static const FastKernelTable t = [] {
         FastKernelTable x{};
-        fill_d<1, 0>(x);
-        fill_d<2, 0>(x);
-        fill_d<1, 1>(x);
-        fill_d<2, 1>(x);
-        fill_d<1, 2>(x);
-        fill_d<2, 2>(x);
-        fill_d<1, 3>(x);
-        fill_d<2, 3>(x);
-        fill_d<1, 4>(x);
-        fill_d<2, 4>(x);
-        fill_ua<1>(x);
-        fill_ua<2>(x);
-        fill_ua<3>(x);
-        fill_ua<4>(x);
-        fill_ua<5>(x);
-        fill_ua<6>(x);
-        fill_ua<8>(x);
-        fill_ua<10>(x);
-        fill_ua<12>(x);
-        fill_ua<16>(x);
+        fill_k<1>(x);
+        fill_k<2>(x);
+        fill_k<3>(x);
+        fill_k<4>(x);
+        fill_k<5>(x);
+        fill_k<6>(x);
+        fill_k<8>(x);
+        fill_k<10>(x);
+        fill_k<12>(x);
+        fill_k<16>(x);
         return x;
     }();
     return t;

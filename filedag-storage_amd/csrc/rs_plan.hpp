@@ -21,51 +21,27 @@ struct RsPlanDev {
     uint32_t tbl[kMaxK * kColDwords];
 };
 
-// Instantiated fast kernels: fn[K][MT][D][NT] (null when K has no instantiation); NT is
-// the cache policy (0 default, 1 nontemporal loads + stores, 2 nontemporal loads only).
+// Instantiated fast kernels, one per (K, MT) with the shape's cache policy (null when K has no
+// instantiation): aligned layouts, unaligned-window layouts, and the unaligned-window form
+// with fused per-chunk CRC-16 values.
 struct FastKernelTable {
-    void* fn[17][kMaxMT + 1][3][5];  // [K][MT][D][cache policy 0..4]
-    void* ua[17][kMaxMT + 1][3];  // unaligned-layout variants [K][MT][NT], D = 1
-    void* ua_crc[17][kMaxMT + 1];  // the same with fused per-chunk CRC-16 (auto cache policy)
-};
-
-// Experimental variants: fn[shape][v], shape 0 = K10/MT4, 1 = K10/MT1 (D=1);
-// v 0/1/2 = 4/8/10 rows in flight (NT=1); v 3 = split table source (TS=1; NT 1 for MT4,
-// 2 for MT1, the auto policy's choices).
-struct ExpKernelTable {
-    void* fn[2][5];  // v 4 = 64-bit selector shifts (SH64)
-    void* st[2][6];  // buffer stores with the cache bits kStoreAux[v] (option store_aux)
-};
-constexpr int kStoreAux[6] = {0, 1, 2, 16, 17, 18};
-
-// LDS-DMA staged variants (rs_lds_kernels.hip, option lds_dma): [0] RS(10,4) encode and
-// [1] 1-row reconstruct with 4 waves per workgroup, [2]/[3] the same with 2
-struct LdsKernelTable {
-    void* fn[4];
-    int wpg[4];
+    void* fn[17][kMaxMT + 1];
+    void* ua[17][kMaxMT + 1];
+    void* ua_crc[17][kMaxMT + 1];
 };
 
 const FastKernelTable& fast_kernels();
-const LdsKernelTable& lds_kernels();
-const ExpKernelTable& exp_kernels();
 void* generic_kernel();
 void* repitch_kernel();
 
-// CRC-16 of shard rows (crc16.hpp): the device table buffer holds P[15][2][256], then
-// U[16][256], N[32][16], H[22][64] and PH[15][3][64] (u16); a wave folds kCrcSegTiles 1 KiB
-// tiles of one row.  Chunk fold: 0 = one U lookup per byte (256-entry tables, bank
-// conflicts), 1 = one N lookup per nibble (16-entry tables: each lookup touches 8 distinct
-// banks, conflict-free), 2 = one H lookup per six bits (64 u16 = 32 dwords, one per bank of a
-// ds_read_b32 half-wave: conflict-free) with powers from PH, also conflict-free (A/B: level
-// with 1).
+// CRC-16 of shard rows (crc16.hpp): the device table buffer holds P[15][2][256] (the powers
+// A^(2^i), byte-sliced) and N[32][16] (u16); a wave folds kCrcSegTiles 1 KiB tiles of one row
+// with one N lookup per nibble (16-entry tables: each wave-wide lookup touches 8 distinct
+// banks, so it never conflicts).
 constexpr int kCrcSegTiles = 8;
 constexpr int kCrcPWords = 15 * 2 * 256 / 2;
-constexpr int kCrcUWords = 16 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
-constexpr int kCrcHWords = 22 * 64 / 2;
-constexpr int kCrcPHWords = 15 * 3 * 64 / 2;
-constexpr int kCrcHOff = kCrcPWords + kCrcUWords + kCrcNWords;
-constexpr int kCrcTableWords = kCrcHOff + kCrcHWords + kCrcPHWords;
+constexpr int kCrcTableWords = kCrcPWords + kCrcNWords;
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
@@ -77,8 +53,8 @@ constexpr int kCrc32TableWords = kCrc32LdsWords + 20 * 32;
 struct Crc32Shift {
     uint32_t col[32];
 };
-void* crc16_rows_kernel(bool aligned, int fold);
-void* crc16_combine_kernel(bool six);
-void* crc32_rows_kernel(bool aligned, bool pipe);
+void* crc16_rows_kernel(bool aligned);
+void* crc16_combine_kernel();
+void* crc32_rows_kernel(bool aligned);
 
 }  // namespace rsmi

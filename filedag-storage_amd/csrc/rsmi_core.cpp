@@ -147,10 +147,10 @@ std::vector<uint8_t> want_mask(const rsmi_ctx* c, const uint8_t* present, int da
     return w;
 }
 
-const char* kernel_label(int K, int MT, int D, int NT, bool fast) {
+const char* kernel_label(int K, int MT, int NT, bool fast) {
     static thread_local char buf[96];
     if (fast)
-        std::snprintf(buf, sizeof buf, "rs_fast_kernel<K=%d,MT=%d,D=%d,NT=%d>", K, MT, D, NT);
+        std::snprintf(buf, sizeof buf, "rs_fast_kernel<K=%d,MT=%d,NT=%d>", K, MT, NT);
     else
         std::snprintf(buf, sizeof buf, "rs_generic_kernel<K=%d,MT=%d>", K, MT);
     return buf;
@@ -174,59 +174,25 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
     const bool ua = (!aligned || fuse) && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
     if (fuse && !ua) return RSMI_ERR_INVALID_ARG;  // callers fall back to the separate CRC pass
     for (const DevTile& t : plan.tiles) {
-        const int D = ua ? 1 : c->opt_d;
-        int NT = c->opt_nt >= 0 ? c->opt_nt : auto_cache_policy(t.K, t.MT);
-        // UA variants exist for policies 1 and 2 (sc1 buffer stores need aligned chunks)
-        if (ua && (NT == 0 || NT >= 3)) NT = t.K >= 4 * t.MT ? 2 : 1;
-        if (!ua && NT == 1 && c->opt_buffer_stores) NT = 4;
+        const int NT = auto_cache_policy(t.K, t.MT);
         void* fn = nullptr;
-        if (aligned && t.K <= 16) fn = fast_kernels().fn[t.K][t.MT][D][NT];
-        if (ua && t.K <= 16) fn = fuse ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().ua[t.K][t.MT][NT];
+        if (t.K <= 16) {
+            if (fuse) fn = fast_kernels().ua_crc[t.K][t.MT];
+            else if (aligned) fn = fast_kernels().fn[t.K][t.MT];
+            else if (ua) fn = fast_kernels().ua[t.K][t.MT];
+        }
         if (fuse && !fn) return RSMI_ERR_INVALID_ARG;
-        if (fuse) NT = auto_cache_policy(t.K, t.MT);  // the one policy the fused variants have
-        int pf_label = 0, ts_label = 0;
-        if (fn && !ua && c->opt_prefetch && t.K == 10 && (t.MT == 4 || t.MT == 1) && D == 1 && NT == 1) {
-            const int pi = c->opt_prefetch == 4 ? 0 : c->opt_prefetch == 8 ? 1 : 2;
-            fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][pi];
-            pf_label = c->opt_prefetch;
-        } else if (fn && !ua && c->opt_tables >= 1 && t.K == 10 && D == 1 &&
-                   ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
-            fn = exp_kernels().fn[t.MT == 4 ? 0 : 1][c->opt_tables == 1 ? 3 : 4];
-            ts_label = c->opt_tables;
-        }
-        int sp_label = -1;
-        if (fn && !ua && c->opt_store_aux >= 0 && t.K == 10 && D == 1 && ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2)))
-            for (int i = 0; i < 6; i++)
-                if (kStoreAux[i] == c->opt_store_aux) {
-                    fn = exp_kernels().st[t.MT == 4 ? 0 : 1][i];
-                    sp_label = c->opt_store_aux;
-                }
-        int wpg = kWG / kWave, lds_label = 0;
-        if (fn && !ua && c->opt_lds >= 1 && c->opt_lds <= 2 && t.K == 10 && D == 1 &&
-            ((t.MT == 4 && NT == 1) || (t.MT == 1 && NT == 2))) {
-            const int i = (t.MT == 4 ? 0 : 1) + (c->opt_lds == 2 ? 2 : 0);
-            fn = lds_kernels().fn[i];
-            wpg = lds_kernels().wpg[i];
-            lds_label = wpg;
-        }
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
-            const uint64_t tpb = (cpb + uint64_t(kWave * D) - 1) / uint64_t(kWave * D);
+            const uint64_t tpb = (cpb + uint64_t(kWave) - 1) / uint64_t(kWave);
+            constexpr int wpg = kWG / kWave;
             // One tile per wave: the hardware dispatcher hands each free slot the next workgroup,
             // which balances the launch across CUs and XCDs of uneven effective bandwidth.  A
             // persistent grid (occupancy x CUs, each wave striding over ~26 tiles) gives every CU
             // the same share and waits for the slowest: measured 9-28 % slower on every BASELINE
-            // shape (tools/bench_ab.sh, profiles/r01/grid_ab.txt).  waves_per_cu > 0 caps the
-            // grid (A/B; the loop in the kernels strides over the remaining tiles).
+            // shape.  waves_per_cu > 0 caps the grid (the loop in the kernels
+            // strides over the remaining tiles).
             long wg_cap = std::numeric_limits<long>::max();
-            if (lds_label) {  // the LDS-DMA variant refills its ring across a wave's tiles: persistent
-                int& occ = c->occupancy[fn];
-                if (occ <= 0) {
-                    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpg * kWave, 0));
-                    if (occ <= 0) occ = 1;
-                }
-                wg_cap = long(c->num_cu) * occ;
-            }
             if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / wpg);
             // split into launches whose tile count fits 32 bits
             const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / tpb);
@@ -240,20 +206,14 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 const uint32_t* ctbl = fuse ? fuse->tbl : nullptr;
                 uint16_t* cout = fuse ? fuse->out + b0 * fuse->slots * tpb * kWave : nullptr;
                 uint32_t cslots = fuse ? fuse->slots : 0, cslot0 = fuse ? fuse->out_slot0 : 0;
-                uint32_t xo = uint32_t(c->opt_xcd_order);
-                void* args[] = {&pd,    &inb,    &outb,  &in_bs, &in_rs, &out_bs, &out_rs, &S32,
-                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0, &xo};
+                void* args[] = {&pd,    &inb,   &outb,   &in_bs, &in_rs, &out_bs, &out_rs, &S32,
+                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
             }
-            c->last_kernel = kernel_label(t.K, t.MT, D, NT, true);
-            if (ua) c->last_kernel += ",UA";
+            c->last_kernel = kernel_label(t.K, t.MT, NT, true);
+            if (ua || fuse) c->last_kernel += ",UA";
             if (fuse) c->last_kernel += ",CRC";
-            if (pf_label) c->last_kernel += ",PF=" + std::to_string(pf_label);
-            if (ts_label) c->last_kernel += ts_label == 1 ? ",TS=1" : ",SH64";
-            if (lds_label) c->last_kernel += ",LDS,WPG=" + std::to_string(lds_label);
-            if (sp_label >= 0) c->last_kernel += ",SP=" + std::to_string(sp_label);
-            if (c->opt_xcd_order && !lds_label) c->last_kernel += ",XO";
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -261,7 +221,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             const RsPlanDev* pd = t.dev;
             void* args[] = {&pd, &in, &out, &in_bs, &in_rs, &out_bs, &out_rs, &S, &nblocks};
             HIP_TRY(hipLaunchKernel(generic_kernel(), dim3(gx, gy), dim3(kWG), args, 0, stream));
-            c->last_kernel = kernel_label(t.K, t.MT, 0, 0, false);
+            c->last_kernel = kernel_label(t.K, t.MT, 0, false);
         }
     }
     return hip_status(hipGetLastError());
@@ -450,40 +410,9 @@ int rsmi_decode_matrix(const rsmi_ctx* c, const uint8_t* present, uint8_t* out, 
 int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     if (!c || !key) return RSMI_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (!std::strcmp(key, "chunks_per_lane")) {
-        if (value != 1 && value != 2) return RSMI_ERR_INVALID_ARG;
-        c->opt_d = int(value);
-    } else if (!std::strcmp(key, "nontemporal")) {
-        if (value < -1 || value > 4) return RSMI_ERR_INVALID_ARG;
-        c->opt_nt = int(value);
-    } else if (!std::strcmp(key, "prefetch")) {
-        // 4/8/10 = rows in flight (A/B only; RS(10,4) encode and 1-row reconstruct, NT=1)
-        if (value != 0 && value != 4 && value != 8 && value != 10)
-            return RSMI_ERR_INVALID_ARG;
-        c->opt_prefetch = int(value);
-    } else if (!std::strcmp(key, "zero_copy")) {
+    if (!std::strcmp(key, "zero_copy")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
-    } else if (!std::strcmp(key, "tables")) {
-        if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
-        c->opt_tables = int(value);
-    } else if (!std::strcmp(key, "xcd_order")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
-        c->opt_xcd_order = int(value);
-    } else if (!std::strcmp(key, "buffer_stores")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
-        c->opt_buffer_stores = int(value);
-    } else if (!std::strcmp(key, "store_aux")) {
-        // buffer-store cache bits for the RS(10,4) encode / 1-row reconstruct shapes (A/B)
-        bool ok = value == -1;
-        for (int a : kStoreAux) ok |= value == a;
-        if (!ok) return RSMI_ERR_INVALID_ARG;
-        c->opt_store_aux = int(value);
-    } else if (!std::strcmp(key, "lds_dma")) {
-        // 1/2 = LDS-DMA staged kernel with 4/2 waves per workgroup (rs_lds_kernels.hip; aligned
-        // RS(10,4) encode and 1-row reconstruct shapes)
-        if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
-        c->opt_lds = int(value);
     } else if (!std::strcmp(key, "small_call_bytes")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_small_bytes = value;
@@ -493,12 +422,6 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "coalesce_max")) {
         if (value < 1 || value > 65536) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_max = value;
-    } else if (!std::strcmp(key, "crc_fold")) {
-        if (value < 0 || value > 3) return RSMI_ERR_INVALID_ARG;
-        c->opt_crc_fold = int(value);
-    } else if (!std::strcmp(key, "crc32_pipe")) {
-        if (value != 0 && value != 1) return RSMI_ERR_INVALID_ARG;
-        c->opt_crc32_pipe = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;

@@ -14,14 +14,10 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.U) + sizeof(t.N) + sizeof(t.H) + sizeof(t.PH) == size_t(kCrcTableWords) * 4,
-                  "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.N) == size_t(kCrcTableWords) * 4, "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
     std::memcpy(h.data(), t.P, sizeof(t.P));
-    std::memcpy(h.data() + kCrcPWords * 2, t.U, sizeof(t.U));
-    std::memcpy(h.data() + (kCrcPWords + kCrcUWords) * 2, t.N, sizeof(t.N));
-    std::memcpy(h.data() + kCrcHOff * 2, t.H, sizeof(t.H));
-    std::memcpy(h.data() + (kCrcHOff + kCrcHWords) * 2, t.PH, sizeof(t.PH));
+    std::memcpy(h.data() + kCrcPWords * 2, t.N, sizeof(t.N));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -36,17 +32,16 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     if (zero) HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
     if (S == 0) return RSMI_OK;  // R(empty) = 0
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = crc16_rows_kernel(aligned, c->opt_crc_fold);
+    void* fn = crc16_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16;
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
     uint64_t nitems = nblocks * nrows * nseg;
     // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
-    // workgroup still amortizes its LDS table staging over ~6 items per wave (tools/crcgrid.py:
-    // +3 % over occupancy x CUs, -25 % at one item per wave).  The pipelined pass (fold 3)
-    // keeps its next item's loads in flight itself and does best at 48 (tools/crc_wpc_sweep.sh)
-    const bool pipe = c->opt_crc_fold == 3 && aligned;
-    uint64_t cap = uint64_t(c->num_cu) * (pipe ? 48 : 96) / 4;
+    // workgroup still amortizes its LDS table staging over ~6 items per wave (+3 % over
+    // occupancy x CUs, -25 % at one item per wave).  The pipelined pass (aligned rows) keeps
+    // its next item's loads in flight itself and does best at 48
+    uint64_t cap = uint64_t(c->num_cu) * (aligned ? 48 : 96) / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
@@ -71,8 +66,6 @@ int ensure_crc32_tables(rsmi_ctx* c) {
 
 // CRC-32 R(row) of nrows rows per block, XORed into out[b*out_bs + r] (the caller zeroes
 // it), stream-ordered.  Rows may lie in device or page-locked host memory.
-// grid of the pipelined CRC-32 pass, waves per CU (crc_wpc_sweep.sh)
-constexpr int kCrc32PipeWaves = 48;
 
 int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstride, uint32_t nrows, uint64_t S,
                  uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream) {
@@ -80,8 +73,7 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     int rc = ensure_crc32_tables(c);
     if (rc) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    const bool pipe = c->opt_crc32_pipe && aligned;
-    void* fn = crc32_rows_kernel(aligned, pipe);
+    void* fn = crc32_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16, span = tile * kCrc32SegTiles;
     if (S / span >= (uint64_t(1) << kCrc32SegPowers)) return RSMI_ERR_INVALID_ARG;  // rows below 4 GiB
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
@@ -93,9 +85,8 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     }
     Crc32Shift sh = c->crc32_shift;
     uint64_t nitems = nblocks * nrows * nseg;
-    // 96 waves per CU as for the CRC-16 pass; the pipelined pass (option crc32_pipe) at
-    // kCrc32PipeWaves (tools/crc_wpc_sweep.sh)
-    uint64_t cap = uint64_t(c->num_cu) * (pipe ? kCrc32PipeWaves : 96) / 4;
+    // 96 waves per CU as for the plain CRC-16 pass
+    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;
@@ -144,7 +135,7 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
     // it wants many waves in flight
     const uint64_t wpc = c->opt_waves_per_cu > 0 ? uint64_t(c->opt_waves_per_cu) : 64;
     const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * wpc / 4)));
-    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(c->opt_crc_fold == 2), dim3(grid), dim3(kWG), args, 0, st));
+    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
     return RSMI_OK;
 }
 

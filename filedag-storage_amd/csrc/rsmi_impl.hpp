@@ -78,7 +78,6 @@ struct rsmi_ctx {
     int dev_status = RSMI_OK;
     int num_cu = 256;
     std::map<std::string, std::shared_ptr<rsmi::impl::Plan>> plans;
-    std::map<void*, int> occupancy;
     std::vector<rsmi::impl::Staging> staging;  // [0] single-block calls, [0..2] batch pipeline
     uint8_t* h_stage = nullptr;    // pinned landing area for rebuilt rows (odd S)
     size_t h_stage_cap = 0;
@@ -93,18 +92,8 @@ struct rsmi_ctx {
     uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
     size_t chunks_cap = 0;
     // options
-    int opt_d = 1;
-    int opt_nt = -1;  // cache policy, -1 = auto_cache_policy(MT) (see there)
-    long opt_waves_per_cu = 0;
-    int opt_prefetch = 0;
+    long opt_waves_per_cu = 0;  // grid cap (0 = one tile per wave / the CRC passes' defaults)
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores
-    int opt_crc_fold = 3;   // CRC-16 rows pass: 3 = nibble tables, pipelined; 1 = nibble; 2 = six-bit; 0 = byte (A/B)
-    int opt_crc32_pipe = 0;  // CRC-32 rows pass: 0 = plain, 1 = software-pipelined for aligned rows (A/B, level)
-    int opt_xcd_order = 0;      // 1: RS(10,4) bench shapes with XCD-grouped tile order (A/B)
-    int opt_buffer_stores = 0;  // 1: aligned launches of policy 1 use policy 4 (buffer stores)
-    int opt_store_aux = -1;  // >= 0: RS(10,4) kernels store with these buffer cache bits (A/B)
-    int opt_lds = 0;        // 1/2 = LDS-DMA staged kernel, 4/2 waves per workgroup (A/B)
-    int opt_tables = 0;     // 1 = split LDS/SGPR table source (A/B, RS(10,4) shapes)
     long opt_small_bytes = 2L << 20;  // host calls up to this many shard bytes run zero-copy
     uint8_t* h_small = nullptr;       // page-locked staging of small calls (pageable callers)
     size_t h_small_cap = 0;
@@ -150,7 +139,7 @@ int encode_plan(rsmi_ctx* c, std::shared_ptr<Plan>& out);
 int decode_rows(const rsmi_ctx* c, const uint8_t* present, Matrix& dec, std::vector<int>& used);
 int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, const uint8_t* want, std::shared_ptr<Plan>& out);
 std::vector<uint8_t> want_mask(const rsmi_ctx* c, const uint8_t* present, int data_only);
-const char* kernel_label(int K, int MT, int D, int NT, bool fast);
+const char* kernel_label(int K, int MT, int NT, bool fast);
 int auto_cache_policy(int K, int MT);
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,

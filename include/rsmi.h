@@ -257,27 +257,16 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t
 
 /* ------------------------------------------------------------------ tuning / introspection */
 
-/* Kernel variant knobs (A/B in one process): "chunks_per_lane" (1|2), "nontemporal" (cache
- * policy: -1 auto per output width (default), 0 default loads and stores, 1 nontemporal loads
- * and stores, 2 nontemporal loads only), "waves_per_cu" (grid cap; 0 = one tile per wave for the coding kernels, occupancy x CUs for the
- * CRC rows kernels),
- * "prefetch" (experimental RS(10,4) variants 4|8|10), "zero_copy" (1 = default: host batch calls whose buffers are page-locked
-(rsmi_host_alloc) run as one kernel that reads and writes them in place over PCIe, at any
-size -- equal to the copy-engine pipeline for encode and 8-18% faster for reconstruct; 2 = the
-same; 0 = always the copy-engine pipeline), "crc_fold" (CRC-16 rows pass: 3 = nibble tables,
-software-pipelined, for aligned rows (default; unaligned rows take 1), 1 = nibble tables, 2 =
-six-bit tables, 0 = byte tables (A/B)), "crc32_pipe" (CRC-32 rows pass: 0 = plain (default), 1 =
-software-pipelined for aligned rows (A/B: level with 0)), "tables" (1 = RS(10,4) kernels read three of the five
-table fields into SGPRs by scalar loads instead of LDS (A/B)), "lds_dma" (1|2 = RS(10,4)
-aligned encode and 1-row reconstruct run the LDS-DMA staged kernel with 4|2 waves per
-workgroup (A/B)), "nontemporal" 3|4 (sc1 / nt buffer stores), "store_aux" (buffer-store cache
-bits), "buffer_stores" (1: policy-1 launches use buffer stores) and "xcd_order" (1: XCD-grouped
-tile order) -- all A/B, measured in DESIGN.md section 4, "coalesce_us" / "coalesce_max"
-(rsmi_encode_block_coalesced), "small_call_bytes" (host calls moving at most this many shard
-bytes, default 2 MiB, run as one kernel that reads and writes page-locked host memory in
-place over PCIe -- pageable buffers are staged through a page-locked one by CPU copies --
-instead of the copy-engine pipeline; 0 = never).  Returns
- * RSMI_ERR_INVALID_ARG for unknown keys or values. */
+/* Options: "waves_per_cu" (grid cap; 0 = the default geometry: one tile per wave for the
+ * coding kernels, 48/96 waves per CU for the CRC rows passes), "zero_copy" (1 = default: host
+ * batch calls whose buffers are page-locked (rsmi_host_alloc) run as one kernel that reads and
+ * writes them in place over PCIe, at any size; 2 = the same, also reading inputs in place on
+ * the pipeline path; 0 = always the copy-engine pipeline), "small_call_bytes" (host calls moving
+ * at most this many shard bytes, default 2 MiB, run as one such kernel -- pageable buffers are
+ * staged through a page-locked one by CPU copies; 0 = never), "coalesce_us" / "coalesce_max"
+ * (rsmi_encode_block_coalesced).  Kernel variants measured slower than the defaults are not
+ * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
+ * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none). */
 const char* rsmi_last_kernel(const rsmi_ctx* ctx);

@@ -149,12 +149,10 @@ def test_null_arguments():
     assert L.rsmi_encode_matrix(None, None) == rsmi.ErrInvalidArg
     with rsmi.Codec(2, 1) as c:
         assert L.rsmi_set_option(c._h, b"no_such_knob", 1) == rsmi.ErrInvalidArg
-        assert L.rsmi_set_option(c._h, b"chunks_per_lane", 3) == rsmi.ErrInvalidArg
-        assert L.rsmi_set_option(c._h, b"chunks_per_lane", 2) == rsmi.OK
-        assert L.rsmi_set_option(c._h, b"nontemporal", 5) == rsmi.ErrInvalidArg
-        for v in (-1, 0, 1, 2, 3, 4):
-            assert L.rsmi_set_option(c._h, b"nontemporal", v) == rsmi.OK
-        assert L.rsmi_set_option(c._h, b"prefetch", 505) == rsmi.ErrInvalidArg
+        # kernel variants measured slower than the defaults are not in the library
+        for gone in (b"chunks_per_lane", b"nontemporal", b"prefetch", b"tables", b"lds_dma", b"store_aux",
+                     b"buffer_stores", b"xcd_order", b"crc_fold", b"crc32_pipe"):
+            assert L.rsmi_set_option(c._h, gone, 1) == rsmi.ErrInvalidArg, gone
         assert L.rsmi_set_option(c._h, b"zero_copy", 0) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"zero_copy", 2) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"zero_copy", 3) == rsmi.ErrInvalidArg
@@ -163,8 +161,7 @@ def test_null_arguments():
 def test_new_options_and_stats_validate():
     L = rsmi.lib()
     with rsmi.Codec(10, 4) as c:
-        for key, good, bad in [(b"tables", 2, 3), (b"lds_dma", 2, 3), (b"store_aux", 16, 3), (b"buffer_stores", 1, 2), (b"xcd_order", 1, 2), (b"crc_fold", 3, 4), (b"crc32_pipe", 0, 2), (b"coalesce_us", 50, -1),
-                               (b"coalesce_max", 16, 0)]:
+        for key, good, bad in [(b"waves_per_cu", 8, -1), (b"coalesce_us", 50, -1), (b"coalesce_max", 16, 0)]:
             assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
             assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key
         assert c.stat("coalesced_calls") == 0 and c.stat("coalesced_batches") == 0

@@ -67,8 +67,8 @@ def test_oracle_mutcask_entry_crc_is_checksum_of_framed_entry():
 @pytest.mark.gpu
 @pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1023, 1024, 1025, 8191, 8192, 8193, 16384, 24577, 26215, 73729, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
-@pytest.mark.parametrize("pipe", [1, 0])
-def test_rows_dev_matches_zlib(S, layout, pipe):
+@pytest.mark.parametrize("wpc", [0, 1])
+def test_rows_dev_matches_zlib(S, layout, wpc):
     import torch
 
     nrows, nb = 3, 5
@@ -81,7 +81,7 @@ def test_rows_dev_matches_zlib(S, layout, pipe):
     dev = host.to("cuda")
     out = torch.full((nb, nrows + 1), 0xDEAD, dtype=torch.int32, device="cuda")
     with rsmi.Codec(4, 2) as c:
-        c.set_option("crc32_pipe", pipe)
+        c.set_option("waves_per_cu", wpc)
         c.crc32_rows_dev(dev.data_ptr() + off, pitch, nrows * pitch, nrows, S, nb, out.data_ptr(), nrows + 1)
         torch.cuda.synchronize()
         assert c.last_kernel() == "rs_crc32_rows_kernel"

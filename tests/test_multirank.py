@@ -63,6 +63,67 @@ def test_two_rank_gloo_partition_and_timing(tmp_path):
     assert ok.all(), ok
 
 
+def test_bench_spawns_ranks_itself_mock():
+    """`bench.py --gpus 2` with no launcher starts its two ranks itself (before any GPU call)
+    and rank 0 prints one line with n_gpus 2.  --mock swaps the device step for a CPU stand-in
+    so the launcher, gloo, the reductions and the JSON line run here without a GPU."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mock", "--steps", "3"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["mock"] and j["steps"] == 3
+    assert sorted(r["rank"] for r in j["config"]["ranks"]) == [0, 1]
+    assert sum(r["blocks"] for r in j["config"]["ranks"]) == 16
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mock"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_bench_device_generator_matches_oracle():
+    """bench.py's torch splitmix64 (int64 arithmetic, logical shifts by masking) is
+    byte-identical to the oracle's numpy generator for several blocks."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle_lib as orc
+
+    got = bench.splitmix_blocks([0, 1, 4095, 77777], 1000, "cpu").numpy()
+    for j, b in enumerate([0, 1, 4095, 77777]):
+        assert np.array_equal(got[j], orc.splitmix64_bytes(bench.SEED ^ b, 1000))
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_share_device_no_launcher():
+    """The exact command the N>1 path needs: `bench.py --gpus 2` with no launcher, both ranks
+    on cuda:0 (--share-device; the 8-GPU run belongs to the driver).  Each rank codes and
+    verifies its own share of the job's blocks."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",
+           "--blocks", "256", "--settle-ms", "0", "--sustained-steps", "0", "--share-device"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["verify"]["verified"] and j["verify"]["ranks_verified"] == 2
+    payload = 2 * 256 * 262144 * 5
+    assert abs(j["value"] - payload / (j["ms_per_step"] * 5e-3) / 2**30) / j["value"] < 0.01
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_torchrun_on_one_gpu():
     """The N>1 bench path on real hardware: `torch.distributed.run` with 2 ranks sharing
@@ -75,7 +136,7 @@ def test_bench_two_ranks_torchrun_on_one_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "5", "--warmup", "1", "--blocks", "256", "--settle-ms", "0",
-           "--share-device"]
+           "--sustained-steps", "0", "--share-device"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]

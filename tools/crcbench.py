@@ -14,8 +14,8 @@ sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
 import rsmi  # noqa: E402
 
 
-# env CRC_FOLDS (e.g. "2,1") and CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
-FOLDS = [f if f.startswith("crc32") else int(f) for f in os.environ.get("CRC_FOLDS", "3,2,1,0,crc32").split(",")]
+# env CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
+FOLDS = ["crc16", "crc32"]
 WPC = int(os.environ.get("CRC_WPC", "0"))
 
 
@@ -31,11 +31,9 @@ def main():
             c = rsmi.Codec(k, m)
             if WPC:
                 c.set_option("waves_per_cu", WPC)
-            if fold in ("crc32", "crc32pipe"):
-                c.set_option("crc32_pipe", int(fold == "crc32pipe"))
+            if fold == "crc32":
                 f = lambda: c.crc32_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             else:
-                c.set_option("crc_fold", fold)
                 f = lambda: c.crc16_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             t_end = time.perf_counter() + 0.2
             while time.perf_counter() < t_end:
@@ -50,7 +48,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
-            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {('crc32 pipelined' if fold == 'crc32pipe' else 'crc32 (mutcask)') if fold in ('crc32', 'crc32pipe') else 'crc16 fold=' + ('nibble-pipelined', 'six-bit', 'nibble', 'byte')[3 - fold]}: "
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 (datanode)'}: "
                   f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
             c.close()
 
@@ -69,8 +67,6 @@ def fused_vs_separate():
     c = rsmi.Codec(k, m)
     if WPC:
         c.set_option("waves_per_cu", WPC)
-    if os.environ.get("CRC_COMBINE_FOLD"):  # 2: the combine kernel's six-bit powers
-        c.set_option("crc_fold", int(os.environ["CRC_COMBINE_FOLD"]))
     sh = st.cuda_stream
     V = {
         "encode only": lambda: c.encode_batch_dev(b, p, n * p, b + k * p, p, n * p, S, nb, sh),

@@ -18,8 +18,10 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter or "rs_fast_kernel" not in r["Kernel_Name"]:
             continue
-        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+|true|false)", r["Kernel_Name"])
-        key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},D={m.group(3)},NT={ {'true': '1', 'false': '0'}.get(m.group(4), m.group(4)) }>"
+        # rs_fast_kernel<K, MT, NT, WPS, UA, CRC> -> the label rsmi_last_kernel reports
+        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", r["Kernel_Name"])
+        key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (",UA" if m.group(5) == "true" else "") + (
+            ",CRC" if m.group(6) == "true" else "")
         d.setdefault(key, []).append(float(r["Counter_Value"]))
     return {k: statistics.mean(v) for k, v in d.items()}
 

@@ -2,7 +2,8 @@
 """Average rocprofv3 kernel-trace durations over bench.py's timed window.
 
 bench.py launches the encode (and reconstruct) kernel once per step; the timed window is
-the LAST `steps` dispatches of each kernel (settle and warmup dispatches come first).
+the `steps` dispatches of each kernel after the settle steps, the warmup steps and one
+label probe (the sustained run and the self check come after it).
 Usage: trace_window.py <kernel_trace.csv> <bench.json>
 Prints, per kernel, the window average next to bench.py's own HIP-event average.
 """
@@ -17,18 +18,20 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
     steps = bench["steps"]
+    first = bench["config"]["settle"]["steps"] + bench["warmup"] + 1
     per = {}
     for r in rows:
-        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+|true|false)", r["Kernel_Name"])
+        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", r["Kernel_Name"])
         if not m:
             continue
-        key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},D={m.group(3)},NT={ {'true': '1', 'false': '0'}.get(m.group(4), m.group(4)) }>"
+        key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (",UA" if m.group(5) == "true" else "") + (
+            ",CRC" if m.group(6) == "true" else "")
         per.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     ev = {bench["roofline"]["kernel"]: bench["roofline"]["avg_launch_ms"] * 1e3}
     if "reconstruct" in bench:
         ev[bench["reconstruct"]["kernel"]] = bench["reconstruct"]["avg_launch_ms_incl_event_gap"] * 1e3
     for k, d in per.items():
-        w = d[-steps:]
+        w = d[first:first + steps]
         avg = sum(w) / len(w)
         e = ev.get(k)
         extra = f"; bench.py HIP events {e:.1f} us ({(e / avg - 1) * 100:+.1f} %)" if e else ""
