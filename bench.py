@@ -365,6 +365,7 @@ def verify(codec, lay, buf, first_block, lost, data_only, lost_ref, stream, raw=
     if rec_rows:
         for i in rec_rows:
             lay.rows(buf, i, i + 1).zero_()
+        torch.cuda.synchronize()  # the zeroing ran on torch's stream, the rebuild runs on the bench's
         codec.reconstruct_batch_dev(buf.data_ptr(), lay.rs, lay.bs, S, nb, [i not in lost for i in range(n)],
                                     data_only, stream)
         torch.cuda.synchronize()
