@@ -35,6 +35,10 @@ Crc16Tables::Crc16Tables() {
                 const uint16_t v = P[i - 1][h][x];
                 P[i][h][x] = uint16_t(P[i - 1][0][v & 0xFF] ^ P[i - 1][1][v >> 8]);
             }
+    for (int p = 0; p < 16; p++)
+        for (int h = 0; h < 2; h++)
+            for (int q = 0; q < 4; q++)
+                for (int v = 0; v < 16; v++) Q[p][h][q][v] = shift(U[15 - p][v << (4 * h)], uint64_t(16 * (3 - q)));
     // the group order the negative shifts rely on: A^32767 = I on a basis
     for (int bit = 0; bit < 16; bit++)
         if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();

@@ -31,6 +31,10 @@ struct Crc16Tables {
     uint16_t U[16][256];              // U[p][b] = A^p(T[b])
     uint16_t N[32][16];               // nibble tables: N[2p][v] = U[15-p][v], N[2p+1][v] = U[15-p][v << 4]
     uint16_t P[kCrcPowers][2][256];   // P[i][0][x] = A^(2^i)(x), P[i][1][x] = A^(2^i)(x << 8)
+    // quad-relative nibble tables of the fused encode + CRC kernels: Q[p][h][q][v] =
+    // A^(16 (3 - q)) (U[15 - p][v << 4h]) -- lane q of a 4-lane quad folds its chunk relative to
+    // the END OF THE QUAD, so the quad's four values combine by plain XOR
+    uint16_t Q[16][2][4][16];
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
     // A^n(s) for any n >= 0 (reduced mod 32767)

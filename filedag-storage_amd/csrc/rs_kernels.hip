@@ -49,11 +49,16 @@ constexpr int rows_in_flight() {
 // overlapped bytes get the same value from both lanes).  This serves the Split layout itself
 // (rows back to back at pitch S, odd for RS(10,4)) and page-locked host memory read and
 // written in place over PCIe.
-// CRC (with UA only): also fold every row the tile reads or writes into per-chunk CRC-16
-// values (crc16.hpp: R of the chunk's bytes relative to the chunk's end, nibble tables) and
-// store them as u16 at crc_out[(block * crc_slots + shard) * tpb * 64 + chunk]; input row c is
-// shard in_row[c], output row j is shard crc_out_slot0 + out_row[j].  rs_crc16_combine_kernel
-// turns them into R(row).
+// CRC (encode plans only: input row c is shard c, output row j shard K + j): also fold every
+// row the tile reads or writes into CRC-16 values (crc16.hpp).  Lane q of each 4-lane quad
+// folds its 16-byte chunk with the quad-relative nibble tables Q (relative to the end of the
+// quad), two DPP XORs sum the quad, and lane q keeps rows r = q mod 4: one dword store per two
+// such rows leaves the tile's record rec[(block * tpb + tile) * ns2 * 64 + s2 * 64 + lane]
+// (rows 8 s2 + q and 8 s2 + 4 + q of quad lane / 4, u16 each).  Bytes at or past S count as
+// zero (aligned layouts: the row's last chunk is masked).  UA: the row's last window ends at S,
+// not on the 16-byte grid, so its chunk stays out of the quad sums and its value (relative to S)
+// goes to tail[block * (K + MT) + r].  rs_crc16_combine_kernel turns records and tails into
+// R(row).
 // Launch geometry: one tile per wave; the loop strides over further tiles only
 // when the caller caps the grid (option waves_per_cu).
 template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false>
@@ -62,18 +67,18 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                        uint32_t ntiles, const uint32_t* __restrict__ crc_tbl,
-                                                       uint16_t* __restrict__ crc_out, uint32_t crc_slots,
-                                                       uint32_t crc_out_slot0) {
-    static_assert(!CRC || UA, "fused chunk CRCs: unaligned-window kernels only");
+                                                       uint32_t* __restrict__ crc_rec, uint32_t* __restrict__ crc_tail) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
+    constexpr int NSH = K + MT;            // CRC: shards of the block (encode plans)
+    constexpr int NSL = (NSH + 3) / 4;     // CRC: rows each lane keeps (r = q mod 4)
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
-    __shared__ uint32_t s_crc[CRC ? kCrcNWords : 1];
+    __shared__ uint32_t s_crc[CRC ? kCrcQWords : 1];
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
         for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
         if constexpr (CRC)
-            for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_crc[i] = crc_tbl[kCrcPWords + i];
+            for (int i = threadIdx.x; i < kCrcQWords; i += kWG) s_crc[i] = crc_tbl[kCrcQOff + i];
     }
     __syncthreads();
 
@@ -110,45 +115,60 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         const uint32_t chl = ch < cpb ? ch : cpb - 1;  // load chunk, clamped: loads stay unconditional
         // UA: byte offset of the lane's 16-byte window
         const uint32_t win = UA ? (chl * 16u < S - 16u ? chl * 16u : S - 16u) : 0u;
-        // CRC: leading bytes of the lane's window that belong to the previous chunk (the last
-        // window only) count as zero, as per-dword keep masks; branch-free so the folds stay in
-        // straight code
+        // CRC: bytes of the lane's 16-byte chunk that are not part of the row's chunk ch count as
+        // zero, as per-dword keep masks -- UA: the leading bytes of the row's overlapping last
+        // window; aligned: the bytes at or past S of the row's last chunk.  Branch-free, so the
+        // folds stay in straight code (a branch inside the column loop lets the compiler sink
+        // every column's GF math past it).
         u32x4 keep = {~0u, ~0u, ~0u, ~0u};
+        uint32_t slot[NSL], tl[(NSH + 1) / 2];  // rows kept by this lane; UA: the last chunk's values
+        bool in_quad = true;
         if constexpr (CRC) {
-            const int lead = int(chl * 16u - win);
+            if constexpr (UA) {
+                const int lead = int(chl * 16u - win);
 #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const int nb = lead - 4 * w;
-                keep[w] = nb >= 4 ? 0u : nb <= 0 ? ~0u : ~((1u << (8 * nb)) - 1u);
+                for (int w = 0; w < 4; w++) {
+                    const int nb = lead - 4 * w;
+                    keep[w] = nb >= 4 ? 0u : nb <= 0 ? ~0u : ~((1u << (8 * nb)) - 1u);
+                }
+                in_quad = ch + 1 < cpb;  // the last chunk is a tail; lanes past it add nothing
+            } else {
+                const int valid = int(S) - int(chl * 16u);
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const int nb = valid - 4 * w;
+                    keep[w] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+                }
+                in_quad = ch < cpb;
             }
+#pragma unroll
+            for (int i = 0; i < NSL; i++) slot[i] = 0;
         }
-        uint16_t* crc_tile = nullptr;  // this lane's chunk slot in shard 0 of the tile's block
-        if constexpr (CRC) {
-            crc_tile = crc_out + uint64_t(blk) * crc_slots * (uint64_t(tpb) * kWave) + ch;
-            asm volatile("" : "+v"(crc_tile));
-        }
-        auto crc_store = [&](u32x4 x, uint32_t shard) {
+        const uint32_t qq = (lane & 3u) * 0x20202020u;  // byte offset of this lane's table set
+        // fold shard r's chunk x into this lane's slot for r (compile-time r after unrolling)
+        auto crc_row = [&](u32x4 x, int r) {
             if constexpr (CRC) {
                 x &= keep;
-                const uint8_t* nbt = reinterpret_cast<const uint8_t*>(s_crc);
+                const uint8_t* qt = reinterpret_cast<const uint8_t*>(s_crc);
                 uint32_t cr = 0;
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
-                    uint32_t lo = (x[w] << 1) & 0x1E1E1E1Eu, hi = (x[w] >> 3) & 0x1E1E1E1Eu;
-                    asm volatile("" : "+v"(lo), "+v"(hi));
+                    uint32_t lo = ((x[w] << 1) & 0x1E1E1E1Eu) | qq, hi = ((x[w] >> 3) & 0x1E1E1E1Eu) | qq;
+                    asm volatile("" : "+v"(lo), "+v"(hi));  // one byte extract per offset
                     uint32_t l[8];
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const int p = 4 * w + q;
-                        l[2 * q] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + ((lo >> (8 * q)) & 0xFF));
-                        l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(nbt + 64 * p + 32 + ((hi >> (8 * q)) & 0xFF));
+                        l[2 * q] = *reinterpret_cast<const uint16_t*>(qt + 256 * p + ((lo >> (8 * q)) & 0xFF));
+                        l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(qt + 256 * p + 128 + ((hi >> (8 * q)) & 0xFF));
                     }
                     cr = xor3(cr, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
                 }
-                // unconditional: lanes past the row's end own padding slots (chunk pitch
-                // tpb * 64), so no branch splits the column loop (a branch there lets the
-                // compiler sink every column's GF math past it)
-                crc_tile[uint64_t(shard) * (uint64_t(tpb) * kWave)] = uint16_t(cr);
+                if constexpr (UA) tl[r / 2] = (r & 1) ? (tl[r / 2] | (cr << 16)) : cr;
+                cr = in_quad ? cr : 0u;
+                cr ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(cr), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+                cr ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(cr), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+                slot[r / 4] = (lane & 3u) == uint32_t(r & 3) ? cr : slot[r / 4];
             }
         };
         auto load_col = [&](int c) {
@@ -214,7 +234,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                     }
                 }
             }
-            if constexpr (CRC) crc_store(v[slot], plan->in_row[c]);
+            if constexpr (CRC) crc_row(v[slot], c);
             if (c + P < K) v[slot] = load_col(c + P);
             if (c + 1 < K) {
 #pragma unroll
@@ -229,15 +249,25 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
             for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
 
+        if constexpr (CRC) {
+#pragma unroll
+            for (int j = 0; j < MT; j++) crc_row(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j);
+            uint32_t* rec = crc_rec + (uint64_t(blk) * tpb + tib) * ((NSL + 1) / 2) * kWave + lane;
+#pragma unroll
+            for (int i = 0; i < NSL; i += 2) rec[i / 2 * kWave] = slot[i] | (i + 1 < NSL ? slot[i + 1] << 16 : 0u);
+            if constexpr (UA) {
+                if (ch + 1 == cpb) {
+                    uint32_t* tp = crc_tail + uint64_t(blk) * NSH;
+#pragma unroll
+                    for (int r = 0; r < NSH; r++) tp[r] = (tl[r / 2] >> (16 * (r & 1))) & 0xFFFFu;
+                }
+            }
+        }
         if (UA && ch < cpb) {
 #pragma unroll
             for (int j = 0; j < MT; j++) {
                 const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
                 st16u<NT == 1>(ob + out_off[j] + win, o);
-                if constexpr (CRC) {
-                    crc_store(o, crc_out_slot0 + plan->out_row[j]);
-                    __builtin_amdgcn_sched_barrier(0);  // one row's 32 table reads in flight at a time
-                }
             }
         } else if (!UA && ch < cpb) {
             const uint32_t boff = ch * 16u;
@@ -538,18 +568,21 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
     }
 }
 
-// R(row) from the fused kernels' per-chunk values (rs_fast_kernel CRC): one wave per row.
-// A wave step covers 512 chunks: lane l loads chunks 8l..8l+7 as one 16-byte load (the chunk
-// values are u16), combines them with a depth-3 tree (A^16, A^32, A^64), and its running
-// register steps by A^8192 between wave steps; a lane scan then combines the lanes
-// (A^(128*2^j)), and lane 63 shifts the total from the 8 KiB grid end to the row end.  Loads
-// for 4 wave steps are issued ahead of the dependent chain.  The row's last chunk is relative
-// to S (its window ends at S), so it first moves onto the 16-byte grid by A^(16*cpb - S).
-// out[row] is written once (host memory allowed).
+// R(row) from the fused encode's tile records (rs_fast_kernel CRC): one wave per block (a
+// persistent grid strides over blocks).  Lane l takes quads i = 64 j + l of the block (quad i =
+// chunks 4i..4i+3, tile i / 16, record lane 4 (i % 16) + q), loads the quad values of every
+// row (two rows per dword, ns2 * 16 bytes), and keeps one running register per row that steps
+// by A^4096 (64 quads) between its quads; a lane scan (A^(64 * 2^j)) leaves the sums, relative
+// to the end of the last step E = 4096 J bytes, in lane 63.  Lane r then takes row r's sum,
+// moves it to the row's end (A^(S - E), mod 32767) and adds the row's tail (UA records: the
+// last chunk, relative to S).  out[block * nsh + r] is written once (host memory allowed).
+template <int NS2>
 __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* __restrict__ tbl,
-                                                               const uint16_t* __restrict__ chunks, uint32_t cpb,
-                                                               uint32_t pitch, uint64_t S, uint64_t nrows,
+                                                               const uint32_t* __restrict__ rec,
+                                                               const uint32_t* __restrict__ tail, uint32_t tpb,
+                                                               uint32_t nsh, uint64_t S, uint64_t nblocks,
                                                                uint32_t* __restrict__ out) {
+    constexpr int R = 8 * NS2;  // rows carried per lane (padding rows stay zero)
     __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcPWords];
     for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
     __syncthreads();
@@ -557,63 +590,61 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    constexpr uint32_t kStep = kWave * 8;  // chunks per wave step
-    const uint32_t T = (cpb + kStep - 1) / kStep;
-    const uint32_t lead = uint32_t((uint64_t(cpb) * 16 - S) % kCrcOrder);  // 16*cpb - S < 16
-    for (uint64_t r = uint64_t(blockIdx.x) * (kWG / kWave) + wid; r < nrows; r += nw) {
-        const uint16_t* rc = chunks + r * pitch;
-        uint32_t acc = 0;
-        for (uint32_t t0 = 0; t0 < T; t0 += 4) {
-            u32x4 v[4];
+    const uint32_t nq = 16 * tpb, J = (nq + kWave - 1) / kWave;
+    int64_t e = (int64_t(S) - int64_t(J) * 4096) % int64_t(kCrcOrder);
+    if (e < 0) e += kCrcOrder;
+    for (uint64_t b = uint64_t(blockIdx.x) * (kWG / kWave) + wid; b < nblocks; b += nw) {
+        uint32_t acc[R];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t g = (t0 + i) * kStep + 8 * lane;
-                v[i] = u32x4{0, 0, 0, 0};
-                if (t0 + i < T && g < pitch) v[i] = *reinterpret_cast<const u32x4*>(rc + g);  // pitch % 64 == 0
+        for (int r = 0; r < R; r++) acc[r] = 0;
+        const uint32_t* rb = rec + uint64_t(b) * tpb * (NS2 * kWave);
+        for (uint32_t j = 0; j < J; j++) {
+            const uint32_t i = j * kWave + lane;
+            u32x4 v[NS2];
+#pragma unroll
+            for (int s = 0; s < NS2; s++) {
+                v[s] = u32x4{0, 0, 0, 0};
+                if (i < nq) v[s] = *reinterpret_cast<const u32x4*>(rb + (i >> 4) * (NS2 * kWave) + s * kWave + (i & 15) * 4);
             }
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (t0 + i >= T) break;
-                const uint32_t g = (t0 + i) * kStep + 8 * lane;
-                uint32_t c[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    c[q] = (v[i][q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-                    if (g + q >= cpb) c[q] = 0;
-                }
-                if (g <= cpb - 1 && cpb - 1 < g + 8) {  // onto the grid: as if followed by 16*cpb - S zero bytes
-                    const uint32_t q = cpb - 1 - g;
-                    uint32_t x = 0;
-#pragma unroll
-                    for (int e = 0; e < 8; e++) x = uint32_t(e) == q ? c[e] : x;
-#pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        if ((lead >> b) & 1) x = pw(b, x);
-#pragma unroll
-                    for (int e = 0; e < 8; e++) c[e] = uint32_t(e) == q ? x : c[e];
-                }
-                const uint32_t p0 = pw(4, c[0]) ^ c[1], p1 = pw(4, c[2]) ^ c[3];
-                const uint32_t p2 = pw(4, c[4]) ^ c[5], p3 = pw(4, c[6]) ^ c[7];
-                const uint32_t x = pw(6, pw(5, p0) ^ p1) ^ (pw(5, p2) ^ p3);
-                acc = pw(13, acc) ^ x;  // earlier wave steps move 8 KiB
+            for (int r = 0; r < R; r++) {
+                // row r = 8 s + 4 h + q: dword q of record s, half h
+                const uint32_t x = (v[r / 8][r % 4] >> (16 * ((r / 4) & 1))) & 0xFFFFu;
+                acc[r] = j ? pw(12, acc[r]) ^ x : x;  // earlier quads of this lane move 4 KiB
             }
         }
 #pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const uint32_t w = pw(7 + j, acc);  // 128 * 2^j bytes
-            const uint32_t t = __shfl_up(w, 1u << j);
-            if (lane >= (1u << j)) acc ^= t;
+        for (int l = 0; l < 6; l++) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const uint32_t w = pw(6 + l, acc[r]);  // 64 * 2^l bytes
+                const uint32_t t = __shfl_up(w, 1u << l);
+                if (lane >= (1u << l)) acc[r] ^= t;
+            }
         }
-        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // uniform: broadcast lookups
-        int64_t e = (int64_t(S) - int64_t(T) * (kStep * 16)) % int64_t(kCrcOrder);
-        if (e < 0) e += kCrcOrder;
-        for (int i = 0; e; i++, e >>= 1)
-            if (e & 1) val = pw(i, val);
-        if (lane == 0) out[r] = val;
+        uint32_t x = 0;  // lane r: row r's sum
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t s = uint32_t(__builtin_amdgcn_readlane(int(acc[r]), kWave - 1));
+            x = lane == uint32_t(r) ? s : x;
+        }
+        for (int k = 0; k < kCrcPowers; k++)
+            if ((e >> k) & 1) x = pw(k, x);
+        if (lane < nsh) {
+            if (tail) x ^= tail[b * nsh + lane];
+            out[b * nsh + lane] = x;
+        }
     }
 }
 
-void* crc16_combine_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_kernel); }
+void* crc16_combine_kernel(int ns2) {
+    switch (ns2) {
+        case 1: return reinterpret_cast<void*>(&rs_crc16_combine_kernel<1>);
+        case 2: return reinterpret_cast<void*>(&rs_crc16_combine_kernel<2>);
+        case 3: return reinterpret_cast<void*>(&rs_crc16_combine_kernel<3>);
+        default: return nullptr;
+    }
+}
 
 // aligned rows: the pipelined pass; any other layout: the plain nibble pass
 void* crc16_rows_kernel(bool aligned) {
@@ -631,8 +662,8 @@ static void fill_km(FastKernelTable& t) {
     constexpr int NT = auto_nt(K, MT);
     t.fn[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT>);
     t.ua[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true>);
-    // 2 waves/SIMD: the chunk folds need registers beyond the 128 the streaming kernels keep to
-    t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, 2, true, true>);
+    t.crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, true>);
+    t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, true>);
 }
 
 template <int K>

@@ -22,11 +22,12 @@ struct RsPlanDev {
 };
 
 // Instantiated fast kernels, one per (K, MT) with the shape's cache policy (null when K has no
-// instantiation): aligned layouts, unaligned-window layouts, and the unaligned-window form
-// with fused per-chunk CRC-16 values.
+// instantiation): aligned layouts, unaligned-window layouts, and both with the datanode CRC-16
+// of every row fused in (encode plans).
 struct FastKernelTable {
     void* fn[17][kMaxMT + 1];
     void* ua[17][kMaxMT + 1];
+    void* crc[17][kMaxMT + 1];
     void* ua_crc[17][kMaxMT + 1];
 };
 
@@ -41,7 +42,9 @@ void* repitch_kernel();
 constexpr int kCrcSegTiles = 8;
 constexpr int kCrcPWords = 15 * 2 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
-constexpr int kCrcTableWords = kCrcPWords + kCrcNWords;
+constexpr int kCrcQWords = 16 * 2 * 4 * 16 / 2;  // quad-relative nibble tables (fused kernels)
+constexpr int kCrcQOff = kCrcPWords + kCrcNWords;
+constexpr int kCrcTableWords = kCrcQOff + kCrcQWords;
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
@@ -54,7 +57,7 @@ struct Crc32Shift {
     uint32_t col[32];
 };
 void* crc16_rows_kernel(bool aligned);
-void* crc16_combine_kernel();
+void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
 void* crc32_rows_kernel(bool aligned);
 
 }  // namespace rsmi

@@ -171,13 +171,14 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                          in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (uint64_t(1) << 31);
     // any other layout with rows of at least 16 bytes: the unaligned-window variant (D = 1)
-    const bool ua = (!aligned || fuse) && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
-    if (fuse && !ua) return RSMI_ERR_INVALID_ARG;  // callers fall back to the separate CRC pass
+    const bool ua = !aligned && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
+    if (fuse && ((!aligned && !ua) || plan.tiles.size() != 1)) return RSMI_ERR_INVALID_ARG;  // callers fall back
+                                                                                              // to the separate pass
     for (const DevTile& t : plan.tiles) {
         const int NT = auto_cache_policy(t.K, t.MT);
         void* fn = nullptr;
         if (t.K <= 16) {
-            if (fuse) fn = fast_kernels().ua_crc[t.K][t.MT];
+            if (fuse) fn = ua ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().crc[t.K][t.MT];
             else if (aligned) fn = fast_kernels().fn[t.K][t.MT];
             else if (ua) fn = fast_kernels().ua[t.K][t.MT];
         }
@@ -204,15 +205,16 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 const uint8_t* inb = in + b0 * in_bs;
                 uint8_t* outb = out + b0 * out_bs;
                 const uint32_t* ctbl = fuse ? fuse->tbl : nullptr;
-                uint16_t* cout = fuse ? fuse->out + b0 * fuse->slots * tpb * kWave : nullptr;
-                uint32_t cslots = fuse ? fuse->slots : 0, cslot0 = fuse ? fuse->out_slot0 : 0;
+                const uint64_t rec_per_block = tpb * uint64_t((((t.K + t.MT) + 3) / 4 + 1) / 2) * kWave;
+                uint32_t* crec = fuse ? fuse->rec + b0 * rec_per_block : nullptr;
+                uint32_t* ctail = fuse && fuse->tail ? fuse->tail + b0 * uint64_t(t.K + t.MT) : nullptr;
                 void* args[] = {&pd,    &inb,   &outb,   &in_bs, &in_rs, &out_bs, &out_rs, &S32,
-                                &cpb32, &tpb32, &ntiles, &ctbl,  &cout,  &cslots, &cslot0};
+                                &cpb32, &tpb32, &ntiles, &ctbl,  &crec,  &ctail};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
             }
             c->last_kernel = kernel_label(t.K, t.MT, NT, true);
-            if (ua || fuse) c->last_kernel += ",UA";
+            if (ua) c->last_kernel += ",UA";
             if (fuse) c->last_kernel += ",CRC";
         } else {
             const uint64_t groups = (S + 3) / 4;

@@ -14,10 +14,11 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.N) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) == size_t(kCrcTableWords) * 4, "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
     std::memcpy(h.data(), t.P, sizeof(t.P));
     std::memcpy(h.data() + kCrcPWords * 2, t.N, sizeof(t.N));
+    std::memcpy(h.data() + kCrcQOff * 2, t.Q, sizeof(t.Q));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -111,31 +112,40 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
     return RSMI_OK;
 }
 
-// Encode with fused per-chunk CRCs, then R(row) of all k+m rows of every block into
-// raw[b * (k+m) + row] (device or page-locked host memory).  Needs S >= 16 and k <= 16.
+// Encode with the CRC-16 fused in, then R(row) of all k+m rows of every block into
+// raw[b * (k+m) + row] (device or page-locked host memory).  Needs k <= 16, m <= 4 and either
+// an aligned layout or S >= 16; returns RSMI_ERR_INVALID_ARG otherwise (callers then run the
+// separate pass).
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                             size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
-    const size_t k = size_t(c->k), n = size_t(c->n);
-    const size_t cpb = (S + 15) / 16, pitch = (cpb + kWave - 1) / kWave * kWave;
+                      size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+    const size_t n = size_t(c->n);
+    if (c->k > 16 || plan.tiles.size() != 1) return RSMI_ERR_INVALID_ARG;
+    const size_t cpb = (S + 15) / 16, tpb = (cpb + kWave - 1) / kWave;
+    const size_t ns2 = ((n + 3) / 4 + 1) / 2;
+    const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * n * 4;
     int rc;
     if ((rc = ensure_crc_tables(c))) return rc;
-    if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * n * pitch * 2))) return rc;
+    if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;
+    const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0;
+    if (!aligned && S < 16) return RSMI_ERR_INVALID_ARG;
     CrcFuse fz;
     fz.tbl = c->d_crc_tbl;
-    fz.out = reinterpret_cast<uint16_t*>(c->d_chunks);
-    fz.slots = uint32_t(n);
-    fz.out_slot0 = uint32_t(k);
+    fz.rec = reinterpret_cast<uint32_t*>(c->d_chunks);
+    fz.tail = aligned ? nullptr : reinterpret_cast<uint32_t*>(c->d_chunks + rec_bytes);
     if ((rc = launch_plan(c, plan, in, in_rs, in_bs, out, out_rs, out_bs, S, nblocks, st, &fz))) return rc;
-    const uint16_t* ch = fz.out;
-    uint32_t cpb32 = uint32_t(cpb), pitch32 = uint32_t(pitch);
-    uint64_t S64 = S, rows = nblocks * n;
     const uint32_t* tb = c->d_crc_tbl;
-    void* args[] = {&tb, &ch, &cpb32, &pitch32, &S64, &rows, &raw};
-    // one wave per row up to 64 waves per CU: the combine is a dependent chain per lane, so
-    // it wants many waves in flight
-    const uint64_t wpc = c->opt_waves_per_cu > 0 ? uint64_t(c->opt_waves_per_cu) : 64;
-    const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, uint64_t(c->num_cu) * wpc / 4)));
-    HIP_TRY(hipLaunchKernel(crc16_combine_kernel(), dim3(grid), dim3(kWG), args, 0, st));
+    const uint32_t* rec = fz.rec;
+    const uint32_t* tail = fz.tail;
+    uint32_t tpb32 = uint32_t(tpb), nsh = uint32_t(n);
+    uint64_t S64 = S, nb64 = nblocks;
+    void* args[] = {&tb, &rec, &tail, &tpb32, &nsh, &S64, &nb64, &raw};
+    // one wave per block, a persistent grid of up to 8 workgroups per CU (the power tables take
+    // 15 KiB of LDS per workgroup, so 10 fit)
+    const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
+    void* fn = crc16_combine_kernel(int(ns2));
+    if (!fn) return RSMI_ERR_INVALID_ARG;
+    HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(kWG), args, 0, st));
     return RSMI_OK;
 }
 
@@ -159,10 +169,11 @@ int rsmi_encode_batch_dev_crc(rsmi_ctx* c, const uint8_t* d_data, size_t data_sh
     if ((rc = encode_plan(c, plan))) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
-    if (S >= 16 && k <= 16)
-        return launch_encode_crc(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
-                                 parity_block_stride, S, nblocks, d_raw_out, st);
-    // S < 16 or k > 16: the encode, then the CRC pass over both row sets
+    rc = launch_encode_crc(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
+                           parity_block_stride, S, nblocks, d_raw_out, st);
+    if (rc != RSMI_ERR_INVALID_ARG) return rc;
+    // k > 16, m > 4, or S < 16 in an unaligned layout: the encode, then the CRC pass over both
+    // row sets
     if ((rc = launch_plan(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
                           parity_block_stride, S, nblocks, st)))
         return rc;

@@ -106,16 +106,16 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
     uint32_t* hraw32 = raw32_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz + raw_sz) : nullptr;
     if (!in || !out) return RSMI_ERR_DEVICE;
     int rc;
-    if (raw_out && S >= 16 && k <= 16) {
-        // fused: the encode stores per-chunk CRCs of every row it reads and writes (the shard
-        // bytes cross PCIe once), then one wave per row combines them into R(row) and stores
-        // it straight into the page-locked staging
+    if (raw_out && S >= 16 && k <= 16 && m <= 4) {
+        // fused: the encode folds every row it reads and writes into per-tile CRC records (the
+        // shard bytes cross PCIe once), then one wave per block combines them into R(row) and
+        // stores it straight into the page-locked staging
         uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, raw_sz));
         if (!draw) return RSMI_ERR_DEVICE;
         if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, draw, st))) return rc;
     } else {
         if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
-        if (raw_out) {  // S < 16 or k > 16: a separate CRC pass over the rows where they lie
+        if (raw_out) {  // S < 16, k > 16 or m > 4: a separate CRC pass over the rows where they lie
             if ((rc = reserve(c->d_crc, c->crc_cap, raw_sz))) return rc;
             uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc);
             HIP_TRY(hipMemsetAsync(cr, 0, raw_sz, st));

@@ -59,12 +59,12 @@ struct Staging {
 };
 
 // Launch every tile of a plan over nblocks blocks.
-// Fused per-chunk CRC output of a launch (rs_fast_kernel CRC variants): chunk values of every
-// row the plan reads or writes, at out[(block * slots + shard) * cpb + chunk].
+// Fused CRC-16 output of an encode launch (rs_fast_kernel CRC variants): per-tile quad records
+// of every shard and, for unaligned-window layouts, the rows' last chunks (rs_kernels.hip).
 struct CrcFuse {
     const uint32_t* tbl = nullptr;
-    uint16_t* out = nullptr;
-    uint32_t slots = 0, out_slot0 = 0;
+    uint32_t* rec = nullptr;
+    uint32_t* tail = nullptr;
 };
 
 }  // namespace impl
@@ -89,7 +89,7 @@ struct rsmi_ctx {
     size_t crc32_cap = 0;
     rsmi::Crc32Shift crc32_shift{};  // launch_crc32's per-S shift matrix, for crc32_shift_S
     uint64_t crc32_shift_S = ~uint64_t(0);
-    uint8_t* d_chunks = nullptr;    // per-chunk CRC-16 values of fused small calls (u16)
+    uint8_t* d_chunks = nullptr;    // fused encode + CRC-16: tile records and tails (CrcFuse)
     size_t chunks_cap = 0;
     // options
     long opt_waves_per_cu = 0;  // grid cap (0 = one tile per wave / the CRC passes' defaults)

@@ -296,21 +296,30 @@ def test_coalesced_reconstruct_concurrent_callers():
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,S,nb,layout", [(10, 4, 26215, 64, "pitched"), (10, 4, 26215, 9, "split"),
                                              (4, 2, 65536, 8, "pitched"), (16, 4, 4097, 5, "split"),
-                                             (3, 2, 7, 6, "split"), (20, 4, 333, 3, "split")])
-def test_encode_batch_dev_crc_fused(k, m, S, nb, layout):
+                                             (3, 2, 7, 6, "split"), (20, 4, 333, 3, "split"),
+                                             (10, 4, 26215, 700, "pitched"), (10, 4, 104858, 5, "split"),
+                                             (16, 4, 262144, 3, "pitched"), (2, 1, 17, 9, "split"),
+                                             (2, 1, 16, 9, "split"), (5, 3, 1000, 7, "pitched"),
+                                             (6, 6, 5000, 4, "split"), (12, 4, 1, 5, "pitched"),
+                                             (1, 1, 33, 5, "split"), (8, 4, 65535, 3, "padded")])
+@pytest.mark.parametrize("wpc", [0, 1])
+def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, wpc):
     """Device-resident encode with the CRC fused into the encode pass: parity and every row's
-    R(row) equal the oracle's (S < 16 and k > 16 take the separate CRC pass)."""
+    R(row) equal the oracle's (k > 16, m > 4, and S < 16 in unaligned layouts take the separate
+    CRC pass).  Row padding in pitched layouts holds garbage, which must not reach the CRC.
+    waves_per_cu=1 makes every wave code many tiles and every combine wave many blocks."""
     import torch
 
     n = k + m
-    rs = rsmi.recommended_pitch(S) if layout == "pitched" else S
+    rs = {"pitched": rsmi.recommended_pitch(S), "split": S, "padded": (S + 15) // 16 * 16 + 32}[layout]
     data = np.random.default_rng(S + k).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
-    host = np.zeros((nb, n, rs), dtype=np.uint8)
+    host = np.random.default_rng(5).integers(0, 256, size=(nb, n, rs), dtype=np.uint8)  # garbage padding
     host[:, :k, :S] = data
     d = torch.from_numpy(host.reshape(-1).copy()).cuda()
     raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
     base = d.data_ptr()
     with rsmi.Codec(k, m) as c:
+        c.set_option("waves_per_cu", wpc)
         c.encode_batch_dev_crc(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, raw.data_ptr(),
                                torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
@@ -318,8 +327,9 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout):
     got = d.cpu().numpy().reshape(nb, n, rs)
     want = orc.encode_fast(k, m, data)
     assert np.array_equal(got[:, k:, :S], want)
-    if S >= 16 and k <= 16:
-        assert ",CRC" in kern
+    if k <= 16 and m <= 4 and (S >= 16 or rs % 16 == 0):
+        assert ",CRC" in kern, kern
+        assert (",UA" in kern) == (rs % 16 != 0), kern
     r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     for b in range(nb):
         rows = list(data[b]) + list(want[b])

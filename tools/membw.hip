@@ -409,3 +409,125 @@ int membw_rows_launch(int K, int M, int NT, const void* in, void* out, uint64_t 
     return hipGetLastError();
 }
 }
+
+// Split-layout study (rows back to back at an odd pitch S, as blocks arrive from the Put path):
+// the memory pattern of rs_fast_kernel's encode with the GF math replaced by an XOR, per
+// access form.  MODE 0: 16-byte windows at any alignment for loads and stores (the UA
+// kernels: window = min(16 ch, S - 16)); 1: the 16-byte-aligned chunk that holds each window's
+// first byte for loads and stores (no funnel shift, wrong bytes: the pattern's floor with
+// aligned accesses); 2: unaligned loads, aligned stores; 3: aligned loads, unaligned stores.
+template <int K, int M, int MODE>
+__global__ __launch_bounds__(256) void membw_split(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                   uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t S,
+                                                   uint32_t cpb, uint32_t tpb, uint32_t ntiles) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t t = blockIdx.x * 4 + wid;
+    if (t >= ntiles) return;
+    const uint32_t blk = t / tpb, tib = t - blk * tpb;
+    const uint32_t ch = tib * 64 + lane;
+    const uint32_t chl = ch < cpb ? ch : cpb - 1;
+    const uint32_t win = chl * 16u < S - 16u ? chl * 16u : S - 16u;
+    const uint8_t* ib = in + uint64_t(blk) * in_bs;
+    uint8_t* ob = out + uint64_t(blk) * out_bs;
+    auto aligned = [](const uint8_t* p) { return reinterpret_cast<const u32x4*>(uintptr_t(p) & ~uintptr_t(15)); };
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        const uint8_t* p = ib + c * rs + win;
+        if constexpr (MODE == 0 || MODE == 2)
+            acc ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
+        else
+            acc ^= __builtin_nontemporal_load(aligned(p));
+    }
+    if (ch < cpb) {
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            uint8_t* q = ob + j * rs + win;
+            if constexpr (MODE == 0 || MODE == 3)
+                __builtin_nontemporal_store(acc + j, reinterpret_cast<u32x4u*>(q));
+            else
+                __builtin_nontemporal_store(acc + j, const_cast<u32x4*>(aligned(q)));
+        }
+    }
+}
+
+extern "C" int membw_split_launch(int K, int M, int MODE, const void* in, void* out, uint64_t in_bs, uint64_t rs,
+                                  uint64_t out_bs, uint32_t S, uint64_t nblocks, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    const uint32_t ntiles = uint32_t(nblocks * tpb);
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+    const int grid = int((ntiles + 3) / 4);
+#define SP(k, m, md) \
+    if (K == k && M == m && MODE == md) membw_split<k, m, md><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, S, cpb, tpb, ntiles); else
+    SP(10, 4, 0) SP(10, 4, 1) SP(10, 4, 2) SP(10, 4, 3) SP(10, 1, 0) SP(10, 1, 1) SP(10, 1, 2) SP(10, 1, 3) return -1;
+#undef SP
+    return hipGetLastError();
+}
+
+// Split-layout tile orders (UA windows, XOR for the math): ORDER 0 block-major (the kernels'),
+// 1 tile-major over all blocks, 2 tile-major within bands of 8 blocks, 3 tile-major within
+// bands of 32 blocks, 4 each block's tiles in two interleaved halves.
+template <int K, int M, int ORDER>
+__global__ __launch_bounds__(256) void membw_split_order(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                         uint64_t in_bs, uint64_t rs, uint64_t out_bs, uint32_t S,
+                                                         uint32_t cpb, uint32_t tpb, uint32_t ntiles, uint32_t nb) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const uint32_t t = blockIdx.x * 4 + wid;
+    if (t >= ntiles) return;
+    uint32_t blk, tib;
+    if constexpr (ORDER == 0) {
+        blk = t / tpb;
+        tib = t - blk * tpb;
+    } else if constexpr (ORDER == 1) {
+        blk = t % nb;
+        tib = t / nb;
+    } else if constexpr (ORDER == 2 || ORDER == 3) {
+        constexpr uint32_t G = ORDER == 2 ? 8 : 32;
+        const uint32_t g = t / (G * tpb), r = t - g * G * tpb;
+        blk = g * G + r % G;
+        tib = r / G;
+        if (blk >= nb) return;
+    } else {
+        blk = t / tpb;
+        const uint32_t r = t - blk * tpb, h = (tpb + 1) / 2;
+        tib = (r & 1) ? h + r / 2 : r / 2;
+        if (tib >= tpb) return;
+    }
+    const uint32_t ch = tib * 64 + lane;
+    const uint32_t chl = ch < cpb ? ch : cpb - 1;
+    const uint32_t win = chl * 16u < S - 16u ? chl * 16u : S - 16u;
+    const uint8_t* ib = in + uint64_t(blk) * in_bs;
+    uint8_t* ob = out + uint64_t(blk) * out_bs;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < K; c++) acc ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(ib + c * rs + win));
+    if (ch < cpb) {
+#pragma unroll
+        for (int j = 0; j < M; j++) __builtin_nontemporal_store(acc + j, reinterpret_cast<u32x4u*>(ob + j * rs + win));
+    }
+}
+
+extern "C" int membw_split_order_launch(int K, int M, int ORDER, const void* in, void* out, uint64_t in_bs,
+                                        uint64_t rs, uint64_t out_bs, uint32_t S, uint64_t nblocks, void* stream) {
+    const uint32_t cpb = (S + 15) / 16, tpb = (cpb + 63) / 64;
+    uint32_t ntiles = uint32_t(nblocks * tpb);
+    if (ORDER == 2) ntiles = uint32_t((nblocks + 7) / 8 * 8 * tpb);
+    if (ORDER == 3) ntiles = uint32_t((nblocks + 31) / 32 * 32 * tpb);
+    if (ORDER == 4) ntiles = uint32_t(nblocks * ((tpb + 1) / 2 * 2));
+    auto st = (hipStream_t)stream;
+    const uint8_t* i = (const uint8_t*)in;
+    uint8_t* o = (uint8_t*)out;
+    const int grid = int((ntiles + 3) / 4);
+    const uint32_t nb = uint32_t(nblocks);
+#define SO(k, m, od) \
+    if (K == k && M == m && ORDER == od) membw_split_order<k, m, od><<<grid, 256, 0, st>>>(i, o, in_bs, rs, out_bs, S, cpb, tpb, ntiles, nb); else
+    SO(10, 4, 0) SO(10, 4, 1) SO(10, 4, 2) SO(10, 4, 3) SO(10, 4, 4) SO(10, 1, 0) SO(10, 1, 1) SO(10, 1, 2) SO(10, 1, 3) SO(10, 1, 4) return -1;
+#undef SO
+    return hipGetLastError();
+}
