@@ -575,7 +575,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 // by A^4096 (64 quads) between its quads; a lane scan (A^(64 * 2^j)) leaves the sums, relative
 // to the end of the last step E = 4096 J bytes, in lane 63.  Lane r then takes row r's sum,
 // moves it to the row's end (A^(S - E), mod 32767) and adds the row's tail (UA records: the
-// last chunk, relative to S).  out[block * nsh + r] is written once (host memory allowed).
+// last chunk, folded with its quad position's tables, so moved back by 16 (3 - q) to S).  out[block * nsh + r] is written once (host memory allowed).
 template <int NS2>
 __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* __restrict__ tbl,
                                                                const uint32_t* __restrict__ rec,
@@ -593,6 +593,8 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
     const uint32_t nq = 16 * tpb, J = (nq + kWave - 1) / kWave;
     int64_t e = (int64_t(S) - int64_t(J) * 4096) % int64_t(kCrcOrder);
     if (e < 0) e += kCrcOrder;
+    const uint32_t qt = uint32_t((S + 15) / 16 - 1) & 3u;            // the tail chunk's lane in its quad
+    const uint32_t et = (kCrcOrder - 16 * (3 - qt)) % kCrcOrder;      // A^-(16 (3 - q))
     for (uint64_t b = uint64_t(blockIdx.x) * (kWG / kWave) + wid; b < nblocks; b += nw) {
         uint32_t acc[R];
 #pragma unroll
@@ -631,7 +633,13 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
         for (int k = 0; k < kCrcPowers; k++)
             if ((e >> k) & 1) x = pw(k, x);
         if (lane < nsh) {
-            if (tail) x ^= tail[b * nsh + lane];
+            if (tail) {
+                // the tail lane folded with its quad position's tables (relative to S + 16 (3 - q))
+                uint32_t y = tail[b * nsh + lane];
+                for (int k = 0; k < kCrcPowers; k++)
+                    if ((et >> k) & 1) y = pw(k, y);
+                x ^= y;
+            }
             out[b * nsh + lane] = x;
         }
     }

@@ -102,6 +102,22 @@ def lib() -> ctypes.CDLL:
         "rsmi_reconstruct_rows_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                                  u8p, ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
+        "rsmi_open_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
+        "rsmi_close_set": (None, [ctypes.c_void_p]),
+        "rsmi_set_size": (ctypes.c_int, [ctypes.c_void_p]),
+        "rsmi_set_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+        "rsmi_partition": (ctypes.c_int, [c_size, ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_size),
+                                          ctypes.POINTER(c_size)]),
+        "rsmi_key_slot": (ctypes.c_int, [u8p, c_size]),
+        "rsmi_set_member_of_key": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size]),
+        "rsmi_set_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
+        "rsmi_set_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
+                                                           ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_set_reconstruct_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+                                                           ctypes.c_int]),
+        "rsmi_set_reconstruct_rows_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+                                                                u8p]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
     for name, (res, args) in sig.items():
@@ -306,6 +322,79 @@ class Codec:
         p = bytearray(1 if x else 0 for x in present)
         _check(lib().rsmi_reconstruct_batch_dev(self._h, d_shards, rs, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                 1 if data_only else 0, stream or None))
+
+
+class DeviceSet:
+    """Several GPUs from one process (rsmi_open_set): batches split into contiguous block
+    ranges, one per member context, run concurrently (include/rsmi.h "device sets").  The
+    reference's Dag Pool runs all its DagNodes in one process (dag/pool/poolservice/cluster.go:
+    28-41); members may repeat a device."""
+
+    def __init__(self, k: int, m: int, devices: Sequence[int]):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _check(lib().rsmi_open_set(k, m, arr, len(devices), ctypes.byref(h)))
+        self.k, self.m, self.n, self.devices = k, m, k + m, list(devices)
+        self._h = h
+
+    def close(self) -> None:
+        if self._h:
+            lib().rsmi_close_set(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def size(self) -> int:
+        return lib().rsmi_set_size(self._h)
+
+    def member_of_key(self, key: bytes) -> int:
+        b = bytearray(key)
+        return lib().rsmi_set_member_of_key(self._h, ctypes.addressof(_buf(b)) if b else None, len(b))
+
+    def encode_batch_host_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
+                              nblocks: int) -> None:
+        _check(lib().rsmi_set_encode_batch_host(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks))
+
+    def encode_batch_host_crcs_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
+                                   nblocks: int, raw16_ptr: Optional[int], raw32_ptr: Optional[int]) -> None:
+        _check(lib().rsmi_set_encode_batch_host_crcs(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
+                                                     raw16_ptr or None, raw32_ptr or None))
+
+    def reconstruct_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
+                                   data_only: bool) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_set_reconstruct_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                     1 if data_only else 0))
+
+    def reconstruct_rows_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
+                                        required: Sequence[bool]) -> None:
+        p = bytearray(1 if x else 0 for x in present)
+        q = bytearray(1 if x else 0 for x in required)
+        _check(lib().rsmi_set_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                          ctypes.addressof(_buf(q))))
+
+
+def partition(nblocks: int, parts: int, i: int):
+    """rsmi_partition: (start, count) of member i's contiguous range."""
+    st, cnt = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(lib().rsmi_partition(nblocks, parts, i, ctypes.byref(st), ctypes.byref(cnt)))
+    return st.value, cnt.value
+
+
+def key_slot(key: bytes) -> int:
+    """keyHashSlot (dag/pool/poolservice/hash_slot.go:20-22) in the library."""
+    b = bytearray(key)
+    return lib().rsmi_key_slot(ctypes.addressof(_buf(b)) if b else None, len(b))
 
 
 def check_shards(lens: Sequence[int], nil_ok: bool):

@@ -1,0 +1,120 @@
+"""Device sets: one process driving several GPUs (include/rsmi.h; the reference's Dag Pool runs
+every DagNode in one process, dag/pool/poolservice/cluster.go:28-41).
+
+CPU tests check the partition and key-routing logic against rsmi.multi (the bench's own
+partition) and the reference's keyHashSlot restated there, and that a set opens and fails
+loudly without a GPU.  GPU tests run sets of one and several contexts on cuda:0 (members may
+repeat a device; the 8-GPU node belongs to the driver) and compare every byte with the oracle.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+import rsmi
+from rsmi import multi
+
+
+@pytest.mark.parametrize("nblocks", [0, 1, 2, 7, 8, 9, 4095, 4096, 8192, 10001])
+@pytest.mark.parametrize("parts", [1, 2, 3, 4, 7, 8])
+def test_partition_matches_bench_partition(nblocks, parts):
+    got = [rsmi.partition(nblocks, parts, i) for i in range(parts)]
+    assert got == [multi.partition_blocks(nblocks, parts, i) for i in range(parts)]
+    # contiguous, ordered, covering, balanced
+    assert got[0][0] == 0 and sum(c for _, c in got) == nblocks
+    for (s0, c0), (s1, _) in zip(got, got[1:]):
+        assert s1 == s0 + c0
+    assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def test_partition_rejects_bad_arguments():
+    L = rsmi.lib()
+    st, cnt = ctypes.c_size_t(), ctypes.c_size_t()
+    assert L.rsmi_partition(10, 0, 0, ctypes.byref(st), ctypes.byref(cnt)) == rsmi.ErrInvalidArg
+    assert L.rsmi_partition(10, 2, 2, ctypes.byref(st), ctypes.byref(cnt)) == rsmi.ErrInvalidArg
+    assert L.rsmi_partition(10, 2, 0, None, ctypes.byref(cnt)) == rsmi.ErrInvalidArg
+
+
+@pytest.mark.parametrize("key", [b"", b"a", b"bafkreigh2akiscaildcqabsyg3dfr6chu3fgpregiymsck7e7aqa4s52zy",
+                                 b"QmYwAPJzv5CZsnA625s3Xf2nemtYgPpHdWEz79ojWnPbdG", bytes(range(256))])
+def test_key_slot_is_reference_hash_slot(key):
+    assert rsmi.key_slot(key) == multi.crc16_ibm(key) & 0x3FFF
+    if key.isascii():
+        assert rsmi.key_slot(key) == multi.key_hash_slot(key.decode())
+
+
+def test_member_of_key_matches_slot_ranges():
+    with rsmi.DeviceSet(10, 4, [0, 0, 0, 0, 0, 0, 0, 0]) as s:
+        assert s.size() == 8
+        seen = set()
+        for i in range(2000):
+            key = f"bafy{i:05d}".encode()
+            mbr = s.member_of_key(key)
+            assert mbr == multi.key_gpu(key.decode(), 8)
+            seen.add(mbr)
+        assert seen == set(range(8))  # every GPU owns some keys
+
+
+def test_open_set_validates_like_open():
+    L = rsmi.lib()
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert L.rsmi_open_set(0, 4, devs, 2, ctypes.byref(h)) == rsmi.ErrInvShardNum
+    assert L.rsmi_open_set(250, 7, devs, 2, ctypes.byref(h)) == rsmi.ErrMaxShardNum
+    assert L.rsmi_open_set(10, 4, devs, 0, ctypes.byref(h)) == rsmi.ErrInvalidArg
+    assert L.rsmi_open_set(10, 4, None, 2, ctypes.byref(h)) == rsmi.ErrInvalidArg
+
+
+def test_set_calls_fail_loudly_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    k, m, S, nb = 4, 2, 1000, 5
+    data = np.zeros((nb, k * S), dtype=np.uint8)
+    par = np.zeros((nb, m * S), dtype=np.uint8)
+    with rsmi.DeviceSet(k, m, [0, 0]) as s:
+        with pytest.raises(rsmi.RsmiError) as e:
+            s.encode_batch_host_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb)
+        assert e.value.code == rsmi.ErrNoDevice
+        s.encode_batch_host_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, 0)  # nothing to do
+        with pytest.raises(rsmi.RsmiError) as e:
+            s.encode_batch_host_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, 0, nb)
+        assert e.value.code == rsmi.ErrShardNoData
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("members", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("k,m,B,nb", [(10, 4, 262144, 7), (16, 4, 4 << 20, 5), (4, 2, 65536 + 5, 9)])
+def test_set_batches_match_oracle(members, k, m, B, nb):
+    """One process, one GPU, one or several member contexts: encode (+ both CRCs) and
+    reconstruct over the set equal the oracle byte for byte."""
+    n = k + m
+    S = (B + k - 1) // k
+    data = np.zeros((nb, k * S), dtype=np.uint8)
+    for b in range(nb):
+        data[b, :B] = orc.splitmix64_bytes(0xF11EDA6 ^ b, B)
+    par = np.zeros((nb, m * S), dtype=np.uint8)
+    raw16 = np.zeros((nb, n), dtype=np.uint32)
+    raw32 = np.zeros((nb, n), dtype=np.uint32)
+    want = orc.encode_fast(k, m, data.reshape(nb, k, S))
+    with rsmi.DeviceSet(k, m, members) as s:
+        s.encode_batch_host_crcs_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, raw16.ctypes.data,
+                                     raw32.ctypes.data)
+        assert np.array_equal(par.reshape(nb, m, S), want)
+        rows = np.concatenate([data.reshape(nb, k, S), want], axis=1)
+        for b in (0, nb // 2, nb - 1):
+            for r in range(n):
+                assert rsmi.crc16_entry(b"", int(raw16[b, r]), S) == orc.crc16_ibm(rows[b, r].tobytes())
+                assert rsmi.crc32_entry(b"", int(raw32[b, r]), S) == orc.crc32_ieee(rows[b, r].tobytes())
+        par2 = np.zeros_like(par)
+        s.encode_batch_host_ptr(data.ctypes.data, k * S, par2.ctypes.data, m * S, S, nb)
+        assert np.array_equal(par2, par)
+        shards = np.ascontiguousarray(rows.reshape(nb, n * S))
+        lost = [0, k]
+        erased = shards.copy().reshape(nb, n, S)
+        erased[:, lost] = 0
+        erased = np.ascontiguousarray(erased.reshape(nb, n * S))
+        s.reconstruct_batch_host_ptr(erased.ctypes.data, n * S, S, nb, [i not in lost for i in range(n)], False)
+        assert np.array_equal(erased, shards)
