@@ -102,21 +102,21 @@ def lib() -> ctypes.CDLL:
         "rsmi_reconstruct_rows_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                                  u8p, ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
-        "rsmi_open_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+        "rsmi_group_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),
-        "rsmi_close_set": (None, [ctypes.c_void_p]),
-        "rsmi_set_size": (ctypes.c_int, [ctypes.c_void_p]),
-        "rsmi_set_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+        "rsmi_group_close": (None, [ctypes.c_void_p]),
+        "rsmi_group_size": (ctypes.c_int, [ctypes.c_void_p]),
+        "rsmi_group_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
         "rsmi_partition": (ctypes.c_int, [c_size, ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_size),
                                           ctypes.POINTER(c_size)]),
         "rsmi_key_slot": (ctypes.c_int, [u8p, c_size]),
-        "rsmi_set_member_of_key": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size]),
-        "rsmi_set_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
-        "rsmi_set_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
+        "rsmi_group_member_of_key": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size]),
+        "rsmi_group_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
+        "rsmi_group_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
                                                            ctypes.c_void_p, ctypes.c_void_p]),
-        "rsmi_set_reconstruct_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+        "rsmi_group_reconstruct_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                            ctypes.c_int]),
-        "rsmi_set_reconstruct_rows_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+        "rsmi_group_reconstruct_rows_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                                 u8p]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
     }
@@ -324,22 +324,22 @@ class Codec:
                                                 1 if data_only else 0, stream or None))
 
 
-class DeviceSet:
-    """Several GPUs from one process (rsmi_open_set): batches split into contiguous block
-    ranges, one per member context, run concurrently (include/rsmi.h "device sets").  The
+class DeviceGroup:
+    """Several GPUs from one process (rsmi_group_open): batches split into contiguous block
+    ranges, one per member context, run concurrently (include/rsmi.h "device groups").  The
     reference's Dag Pool runs all its DagNodes in one process (dag/pool/poolservice/cluster.go:
     28-41); members may repeat a device."""
 
     def __init__(self, k: int, m: int, devices: Sequence[int]):
         arr = (ctypes.c_int * len(devices))(*devices)
         h = ctypes.c_void_p()
-        _check(lib().rsmi_open_set(k, m, arr, len(devices), ctypes.byref(h)))
+        _check(lib().rsmi_group_open(k, m, arr, len(devices), ctypes.byref(h)))
         self.k, self.m, self.n, self.devices = k, m, k + m, list(devices)
         self._h = h
 
     def close(self) -> None:
         if self._h:
-            lib().rsmi_close_set(self._h)
+            lib().rsmi_group_close(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):  # pragma: no cover
@@ -355,32 +355,32 @@ class DeviceSet:
         self.close()
 
     def size(self) -> int:
-        return lib().rsmi_set_size(self._h)
+        return lib().rsmi_group_size(self._h)
 
     def member_of_key(self, key: bytes) -> int:
         b = bytearray(key)
-        return lib().rsmi_set_member_of_key(self._h, ctypes.addressof(_buf(b)) if b else None, len(b))
+        return lib().rsmi_group_member_of_key(self._h, ctypes.addressof(_buf(b)) if b else None, len(b))
 
     def encode_batch_host_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
                               nblocks: int) -> None:
-        _check(lib().rsmi_set_encode_batch_host(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks))
+        _check(lib().rsmi_group_encode_batch_host(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks))
 
     def encode_batch_host_crcs_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
                                    nblocks: int, raw16_ptr: Optional[int], raw32_ptr: Optional[int]) -> None:
-        _check(lib().rsmi_set_encode_batch_host_crcs(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
+        _check(lib().rsmi_group_encode_batch_host_crcs(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks,
                                                      raw16_ptr or None, raw32_ptr or None))
 
     def reconstruct_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
                                    data_only: bool) -> None:
         p = bytearray(1 if x else 0 for x in present)
-        _check(lib().rsmi_set_reconstruct_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+        _check(lib().rsmi_group_reconstruct_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                      1 if data_only else 0))
 
     def reconstruct_rows_batch_host_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
                                         required: Sequence[bool]) -> None:
         p = bytearray(1 if x else 0 for x in present)
         q = bytearray(1 if x else 0 for x in required)
-        _check(lib().rsmi_set_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+        _check(lib().rsmi_group_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                           ctypes.addressof(_buf(q))))
 
 

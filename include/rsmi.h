@@ -255,36 +255,36 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t
                                           size_t nblocks, const uint8_t* present, const uint8_t* required,
                                           uint32_t* raw16_out, uint32_t* raw32_out);
 
-/* ------------------------------------------------------------------ device sets (several GPUs, one process) */
+/* ------------------------------------------------------------------ device groups (several GPUs, one process) */
 
 /* The Dag Pool runs every DagNode of a cluster in one process (dag/pool/poolservice/cluster.go:
- * 28-41).  A device set is one context per entry of devices[] (an entry may repeat: two
+ * 28-41).  A device group is one context per entry of devices[] (an entry may repeat: two
  * contexts on one GPU overlap their copies and kernels).  Its batch calls split the blocks
  * into contiguous ranges, one per member, sizes differing by at most one block (rsmi_partition),
  * and run every range on its member's context from its own host thread -- no data crosses
  * devices, no collective runs -- then return the first failing member's status in member
  * order.  Same arguments, layouts, results and errors as the single-context calls. */
-typedef struct rsmi_set rsmi_set;
-int rsmi_open_set(int k, int m, const int* devices, int ndev, rsmi_set** out);
-void rsmi_close_set(rsmi_set* set);
-int rsmi_set_size(const rsmi_set* set);
-/* Member i's context (owned by the set), for the single-context calls; NULL if out of range. */
-rsmi_ctx* rsmi_set_context(rsmi_set* set, int i);
+typedef struct rsmi_group rsmi_group;
+int rsmi_group_open(int k, int m, const int* devices, int ndev, rsmi_group** out);
+void rsmi_group_close(rsmi_group* group);
+int rsmi_group_size(const rsmi_group* group);
+/* Member i's context (owned by the group), for the single-context calls; NULL if out of range. */
+rsmi_ctx* rsmi_group_context(rsmi_group* group, int i);
 /* The range of blocks member i of parts codes: contiguous, sizes differ by at most one. */
 int rsmi_partition(size_t nblocks, int parts, int i, size_t* start, size_t* count);
 /* keyHashSlot (dag/pool/poolservice/hash_slot.go:20-22): howeyc crc16 IBM of the key & 0x3FFF. */
 int rsmi_key_slot(const uint8_t* key, size_t len);
 /* The member that owns a key: contiguous slot ranges of 16384 / size slots per member, as
  * DagNodes own SlotPairs -- a stable key -> GPU map for per-block callers. */
-int rsmi_set_member_of_key(const rsmi_set* set, const uint8_t* key, size_t len);
-int rsmi_set_encode_batch_host(rsmi_set* set, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+int rsmi_group_member_of_key(const rsmi_group* group, const uint8_t* key, size_t len);
+int rsmi_group_encode_batch_host(rsmi_group* group, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                size_t parity_block_stride, size_t S, size_t nblocks);
-int rsmi_set_encode_batch_host_crcs(rsmi_set* set, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
+int rsmi_group_encode_batch_host_crcs(rsmi_group* group, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                     size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
                                     uint32_t* raw32_out);
-int rsmi_set_reconstruct_batch_host(rsmi_set* set, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+int rsmi_group_reconstruct_batch_host(rsmi_group* group, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                     const uint8_t* present, int data_only);
-int rsmi_set_reconstruct_rows_batch_host(rsmi_set* set, uint8_t* shards, size_t block_stride, size_t S,
+int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, size_t block_stride, size_t S,
                                          size_t nblocks, const uint8_t* present, const uint8_t* required);
 
 /* ------------------------------------------------------------------ tuning / introspection */

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_binding_covers_header():
     L = rsmi.lib()
     for s in declared_symbols():
-        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free"), s
+        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free", "rsmi_group_close"), s
 
 
 def test_abi_version_and_status_strings():

@@ -1,9 +1,9 @@
-"""Device sets: one process driving several GPUs (include/rsmi.h; the reference's Dag Pool runs
+"""Device groups: one process driving several GPUs (include/rsmi.h; the reference's Dag Pool runs
 every DagNode in one process, dag/pool/poolservice/cluster.go:28-41).
 
 CPU tests check the partition and key-routing logic against rsmi.multi (the bench's own
-partition) and the reference's keyHashSlot restated there, and that a set opens and fails
-loudly without a GPU.  GPU tests run sets of one and several contexts on cuda:0 (members may
+partition) and the reference's keyHashSlot restated there, and that a group opens and fails
+loudly without a GPU.  GPU tests run groups of one and several contexts on cuda:0 (members may
 repeat a device; the 8-GPU node belongs to the driver) and compare every byte with the oracle.
 """
 import ctypes
@@ -45,7 +45,7 @@ def test_key_slot_is_reference_hash_slot(key):
 
 
 def test_member_of_key_matches_slot_ranges():
-    with rsmi.DeviceSet(10, 4, [0, 0, 0, 0, 0, 0, 0, 0]) as s:
+    with rsmi.DeviceGroup(10, 4, [0, 0, 0, 0, 0, 0, 0, 0]) as s:
         assert s.size() == 8
         seen = set()
         for i in range(2000):
@@ -56,17 +56,17 @@ def test_member_of_key_matches_slot_ranges():
         assert seen == set(range(8))  # every GPU owns some keys
 
 
-def test_open_set_validates_like_open():
+def test_group_open_validates_like_open():
     L = rsmi.lib()
     h = ctypes.c_void_p()
     devs = (ctypes.c_int * 2)(0, 0)
-    assert L.rsmi_open_set(0, 4, devs, 2, ctypes.byref(h)) == rsmi.ErrInvShardNum
-    assert L.rsmi_open_set(250, 7, devs, 2, ctypes.byref(h)) == rsmi.ErrMaxShardNum
-    assert L.rsmi_open_set(10, 4, devs, 0, ctypes.byref(h)) == rsmi.ErrInvalidArg
-    assert L.rsmi_open_set(10, 4, None, 2, ctypes.byref(h)) == rsmi.ErrInvalidArg
+    assert L.rsmi_group_open(0, 4, devs, 2, ctypes.byref(h)) == rsmi.ErrInvShardNum
+    assert L.rsmi_group_open(250, 7, devs, 2, ctypes.byref(h)) == rsmi.ErrMaxShardNum
+    assert L.rsmi_group_open(10, 4, devs, 0, ctypes.byref(h)) == rsmi.ErrInvalidArg
+    assert L.rsmi_group_open(10, 4, None, 2, ctypes.byref(h)) == rsmi.ErrInvalidArg
 
 
-def test_set_calls_fail_loudly_without_gpu():
+def test_group_calls_fail_loudly_without_gpu():
     import torch
 
     if torch.cuda.is_available():
@@ -74,7 +74,7 @@ def test_set_calls_fail_loudly_without_gpu():
     k, m, S, nb = 4, 2, 1000, 5
     data = np.zeros((nb, k * S), dtype=np.uint8)
     par = np.zeros((nb, m * S), dtype=np.uint8)
-    with rsmi.DeviceSet(k, m, [0, 0]) as s:
+    with rsmi.DeviceGroup(k, m, [0, 0]) as s:
         with pytest.raises(rsmi.RsmiError) as e:
             s.encode_batch_host_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb)
         assert e.value.code == rsmi.ErrNoDevice
@@ -87,9 +87,9 @@ def test_set_calls_fail_loudly_without_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("members", [[0], [0, 0], [0, 0, 0]])
 @pytest.mark.parametrize("k,m,B,nb", [(10, 4, 262144, 7), (16, 4, 4 << 20, 5), (4, 2, 65536 + 5, 9)])
-def test_set_batches_match_oracle(members, k, m, B, nb):
+def test_group_batches_match_oracle(members, k, m, B, nb):
     """One process, one GPU, one or several member contexts: encode (+ both CRCs) and
-    reconstruct over the set equal the oracle byte for byte."""
+    reconstruct over the group equal the oracle byte for byte."""
     n = k + m
     S = (B + k - 1) // k
     data = np.zeros((nb, k * S), dtype=np.uint8)
@@ -99,7 +99,7 @@ def test_set_batches_match_oracle(members, k, m, B, nb):
     raw16 = np.zeros((nb, n), dtype=np.uint32)
     raw32 = np.zeros((nb, n), dtype=np.uint32)
     want = orc.encode_fast(k, m, data.reshape(nb, k, S))
-    with rsmi.DeviceSet(k, m, members) as s:
+    with rsmi.DeviceGroup(k, m, members) as s:
         s.encode_batch_host_crcs_ptr(data.ctypes.data, k * S, par.ctypes.data, m * S, S, nb, raw16.ctypes.data,
                                      raw32.ctypes.data)
         assert np.array_equal(par.reshape(nb, m, S), want)
