@@ -116,44 +116,40 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         // UA: byte offset of the lane's 16-byte window
         const uint32_t win = UA ? (chl * 16u < S - 16u ? chl * 16u : S - 16u) : 0u;
         // CRC: bytes of the lane's 16-byte chunk that are not part of the row's chunk ch count as
-        // zero, as per-dword keep masks -- UA: the leading bytes of the row's overlapping last
-        // window; aligned: the bytes at or past S of the row's last chunk.  Branch-free, so the
-        // folds stay in straight code (a branch inside the column loop lets the compiler sink
-        // every column's GF math past it).
-        u32x4 keep = {~0u, ~0u, ~0u, ~0u};
+        // zero -- UA: the leading bytes of the row's overlapping last window; aligned: the bytes
+        // at or past S of the row's last chunk.  The mask lives in the nibble-offset masks (a
+        // zero nibble looks up a zero entry: the tables are linear), so it costs nothing per
+        // row, and it is branch-free, so the folds stay in straight code (a branch inside the
+        // column loop lets the compiler sink every column's GF math past it).
+        uint32_t nm[4];  // per dword: 0x1E in every byte lane that counts
         uint32_t slot[NSL], tl[(NSH + 1) / 2];  // rows kept by this lane; UA: the last chunk's values
         bool in_quad = true;
         if constexpr (CRC) {
-            if constexpr (UA) {
-                const int lead = int(chl * 16u - win);
+            const int lead = UA ? int(chl * 16u - win) : 0;          // UA: bytes before the chunk
+            const int valid = UA ? 16 : int(S) - int(chl * 16u);     // aligned: bytes before S
 #pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    const int nb = lead - 4 * w;
-                    keep[w] = nb >= 4 ? 0u : nb <= 0 ? ~0u : ~((1u << (8 * nb)) - 1u);
-                }
-                in_quad = ch + 1 < cpb;  // the last chunk is a tail; lanes past it add nothing
-            } else {
-                const int valid = int(S) - int(chl * 16u);
+            for (int w = 0; w < 4; w++) {
+                uint32_t m = 0;
 #pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    const int nb = valid - 4 * w;
-                    keep[w] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+                for (int b = 0; b < 4; b++) {
+                    const int pos = 4 * w + b;
+                    if (pos >= lead && pos < valid) m |= 0x1Eu << (8 * b);
                 }
-                in_quad = ch < cpb;
+                nm[w] = m;
             }
+            in_quad = UA ? ch + 1 < cpb : ch < cpb;  // UA: the last chunk is a tail; lanes past it add nothing
 #pragma unroll
             for (int i = 0; i < NSL; i++) slot[i] = 0;
         }
         const uint32_t qq = (lane & 3u) * 0x20202020u;  // byte offset of this lane's table set
         // fold shard r's chunk x into this lane's slot for r (compile-time r after unrolling)
-        auto crc_row = [&](u32x4 x, int r) {
+        auto crc_row = [&](const u32x4& x, int r) {
             if constexpr (CRC) {
-                x &= keep;
                 const uint8_t* qt = reinterpret_cast<const uint8_t*>(s_crc);
                 uint32_t cr = 0;
 #pragma unroll
                 for (int w = 0; w < 4; w++) {
-                    uint32_t lo = ((x[w] << 1) & 0x1E1E1E1Eu) | qq, hi = ((x[w] >> 3) & 0x1E1E1E1Eu) | qq;
+                    uint32_t lo = ((x[w] << 1) & nm[w]) | qq, hi = ((x[w] >> 3) & nm[w]) | qq;
                     asm volatile("" : "+v"(lo), "+v"(hi));  // one byte extract per offset
                     uint32_t l[8];
 #pragma unroll
@@ -162,7 +158,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                         l[2 * q] = *reinterpret_cast<const uint16_t*>(qt + 256 * p + ((lo >> (8 * q)) & 0xFF));
                         l[2 * q + 1] = *reinterpret_cast<const uint16_t*>(qt + 256 * p + 128 + ((hi >> (8 * q)) & 0xFF));
                     }
-                    cr = xor3(cr, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+                    // 8 lookups and the running value: four 3-input XORs
+                    cr = xor3(xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5]), xor3(l[6], l[7], cr));
                 }
                 if constexpr (UA) tl[r / 2] = (r & 1) ? (tl[r / 2] | (cr << 16)) : cr;
                 cr = in_quad ? cr : 0u;
