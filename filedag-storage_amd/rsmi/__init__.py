@@ -15,7 +15,8 @@ import os
 from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
+# RSMI_LIB: a diagnostic build of the library (tools/Makefile variants) for A/B runs
+LIB_PATH = os.environ.get("RSMI_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librsmi.so")
 
 # status codes (include/rsmi.h) -- names follow the upstream sentinels
 OK = 0
