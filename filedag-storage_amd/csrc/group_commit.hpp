@@ -1,0 +1,62 @@
+// group_commit.hpp -- group commit of concurrent single-item requests, with no thread of its own
+// (rsmi_coalesce.cpp; plain C++, so tests/cpp runs it under ThreadSanitizer without a device).
+//
+// DagNode.Put hands the engine one block per call (node.go:358-408) from many goroutines at
+// once.  A caller that finds no batch executing becomes the executor: it takes every request
+// queued so far (optionally waiting up to wait_us for the queue to reach cap), runs them as one
+// batch through exec(batch) with the lock released, marks them done and wakes the others.
+// Requests that arrive while a batch runs form the next batch.  A lone caller never waits: its
+// batch is itself.  Req needs a `bool done` member, false on submission.
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+namespace rsmi {
+
+template <class Req>
+class GroupCommit {
+public:
+    template <class Exec>
+    void submit(Req& req, size_t cap, long wait_us, Exec&& exec) {
+        calls_++;
+        std::unique_lock<std::mutex> lk(mu_);
+        pending_.push_back(&req);
+        cv_.notify_all();  // an executor waiting out wait_us may now have enough
+        while (!req.done) {
+            if (executing_) {
+                cv_.wait(lk);
+                continue;
+            }
+            executing_ = true;
+            cap = std::max<size_t>(cap, 1);
+            if (wait_us > 0 && pending_.size() < cap)
+                cv_.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return pending_.size() >= cap; });
+            const size_t take = std::min(cap, pending_.size());
+            std::vector<Req*> batch(pending_.begin(), pending_.begin() + take);
+            pending_.erase(pending_.begin(), pending_.begin() + take);
+            lk.unlock();
+            exec(batch);
+            batches_++;
+            lk.lock();
+            for (Req* r : batch) r->done = true;
+            executing_ = false;
+            cv_.notify_all();
+        }
+    }
+    uint64_t calls() const { return calls_.load(); }
+    uint64_t batches() const { return batches_.load(); }
+
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Req*> pending_;
+    bool executing_ = false;
+    std::atomic<uint64_t> calls_{0}, batches_{0};
+};
+
+}  // namespace rsmi

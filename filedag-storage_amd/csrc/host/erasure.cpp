@@ -61,9 +61,20 @@ PinnedBuf& thread_staging() {
     return buf;
 }
 
+namespace {
+std::mutex g_ctx_mu;
+std::map<std::tuple<int, int, int>, rsmi_ctx*> g_ctx_cache;  // lives for the process
+}  // namespace
+
+void release_shared_contexts() {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    for (auto& e : g_ctx_cache) rsmi_close(e.second);
+    g_ctx_cache.clear();
+}
+
 rsmi_ctx* shared_context(int k, int m, int device, int* rc) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, int>, rsmi_ctx*> cache;  // lives for the process
+    auto& mu = g_ctx_mu;
+    auto& cache = g_ctx_cache;
     std::lock_guard<std::mutex> g(mu);
     auto key = std::make_tuple(k, m, device);
     auto it = cache.find(key);

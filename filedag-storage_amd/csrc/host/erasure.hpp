@@ -24,6 +24,8 @@ int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
 // Process-wide context per (k, m, device): NewErasure runs per block in the reference
 // (node.go:277,376) but the matrix / device plans are built once.
 rsmi_ctx* shared_context(int k, int m, int device, int* rc);
+// Close every shared context (process shutdown, with no call in flight).
+void release_shared_contexts();
 
 // Host staging for the batch calls: page-locked (rsmi_host_alloc) so the batch copies run
 // as DMA at full PCIe rate instead of bouncing through the runtime's own pinned pool.

@@ -1,12 +1,7 @@
-// rsmi_coalesce.cpp -- group commit of concurrent single-block calls (see rsmi_impl.hpp).
-//
-// DagNode.Put hands the engine one block per call (node.go:358-408), from many goroutines at
-// once.  Group commit turns those calls into GPU batches without a thread of our own: a
-// caller that finds no batch executing becomes the executor, takes every request queued so
-// far (optionally waiting coalesce_us for more), runs them grouped by key (kind, shard size
-// and, for reconstruct, the erasure pattern) through the host batch paths, and wakes their
-// callers.  Requests that arrive while a batch runs form the next batch.  A lone caller
-// never waits: its batch is itself.
+// rsmi_coalesce.cpp -- group commit of concurrent single-block calls (group_commit.hpp has the
+// queue).  DagNode.Put hands the engine one block per call (node.go:358-408), from many
+// goroutines at once; each executing batch runs its requests grouped by key (kind, shard size
+// and, for reconstruct, the erasure pattern) through the host batch paths.
 
 #include "rsmi_impl.hpp"
 
@@ -92,38 +87,15 @@ void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
     }
 }
 
-// Queue a request and either wait for the executor or become it (group commit).
+// Queue a request and either wait for the executor or become it (group_commit.hpp).
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
     {
         std::lock_guard<std::mutex> g(c->mu);
         int rc = ensure_device(c);
         if (rc) return rc;
     }
-    c->stat_coal_calls++;
-    std::unique_lock<std::mutex> lk(c->q_mu);
-    c->q_pending.push_back(&req);
-    c->q_cv.notify_all();  // an executor waiting out coalesce_us may now have enough
-    while (!req.done) {
-        if (c->q_executing) {
-            c->q_cv.wait(lk);
-            continue;
-        }
-        c->q_executing = true;
-        const size_t cap = size_t(c->opt_coalesce_max);
-        if (c->opt_coalesce_us > 0 && c->q_pending.size() < cap)
-            c->q_cv.wait_for(lk, std::chrono::microseconds(c->opt_coalesce_us),
-                             [&] { return c->q_pending.size() >= cap; });
-        const size_t take = std::min(cap, c->q_pending.size());
-        std::vector<rsmi_ctx::CoalReq*> batch(c->q_pending.begin(), c->q_pending.begin() + take);
-        c->q_pending.erase(c->q_pending.begin(), c->q_pending.begin() + take);
-        lk.unlock();
-        run_coalesced(c, batch);
-        c->stat_coal_batches++;
-        lk.lock();
-        for (auto* r : batch) r->done = true;
-        c->q_executing = false;
-        c->q_cv.notify_all();
-    }
+    c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us,
+                   [c](std::vector<rsmi_ctx::CoalReq*>& batch) { run_coalesced(c, batch); });
     return req.rc;
 }
 
@@ -163,8 +135,8 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
 
 long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
     if (!c || !key) return -1;
-    if (!std::strcmp(key, "coalesced_calls")) return long(c->stat_coal_calls.load());
-    if (!std::strcmp(key, "coalesced_batches")) return long(c->stat_coal_batches.load());
+    if (!std::strcmp(key, "coalesced_calls")) return long(c->coal.calls());
+    if (!std::strcmp(key, "coalesced_batches")) return long(c->coal.batches());
     return -1;
 }
 

@@ -255,16 +255,4 @@ int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size
     return RSMI_OK;
 }
 
-uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
-
-uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n) { return crc32_checksum(p, n); }
-
-uint32_t rsmi_crc32_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
-    return crc32_entry(head, head_len, raw, data_len);
-}
-
-uint16_t rsmi_crc16_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
-    return crc16_entry(head, head_len, raw, data_len);
-}
-
 }  // extern "C"

@@ -23,13 +23,6 @@ namespace {
 
 constexpr int kClusterSlots = 16384;  // dag/slotsmgr/slots_mgr.go:8
 
-// part i of n over nblocks: contiguous, sizes differ by at most one block (rsmi/multi.py)
-void partition(size_t nblocks, size_t parts, size_t i, size_t& start, size_t& count) {
-    const size_t base = nblocks / parts, extra = nblocks % parts;
-    start = i * base + std::min(i, extra);
-    count = base + (i < extra ? 1 : 0);
-}
-
 // Run f(i, start, count) for every non-empty part on its own thread (part 0 on the caller's);
 // the first failing part's status in part order, so results do not depend on timing.
 template <class F>
@@ -39,11 +32,11 @@ int run_parts(const rsmi_group* s, size_t nblocks, F f) {
     std::vector<std::thread> th;
     for (size_t i = 1; i < parts; i++) {
         size_t st, cnt;
-        partition(nblocks, parts, i, st, cnt);
+        rsmi_partition(nblocks, int(parts), int(i), &st, &cnt);
         if (cnt) th.emplace_back([&, i, st, cnt] { rc[i] = f(i, st, cnt); });
     }
     size_t st0, cnt0;
-    partition(nblocks, parts, 0, st0, cnt0);
+    rsmi_partition(nblocks, int(parts), 0, &st0, &cnt0);
     if (cnt0) rc[0] = f(size_t(0), st0, cnt0);
     for (auto& t : th) t.join();
     for (int r : rc)
@@ -88,17 +81,6 @@ int rsmi_group_size(const rsmi_group* s) { return s ? int(s->ctx.size()) : 0; }
 rsmi_ctx* rsmi_group_context(rsmi_group* s, int i) {
     if (!s || i < 0 || size_t(i) >= s->ctx.size()) return nullptr;
     return s->ctx[size_t(i)];
-}
-
-int rsmi_partition(size_t nblocks, int parts, int i, size_t* start, size_t* count) {
-    if (parts <= 0 || i < 0 || i >= parts || !start || !count) return RSMI_ERR_INVALID_ARG;
-    partition(nblocks, size_t(parts), size_t(i), *start, *count);
-    return RSMI_OK;
-}
-
-int rsmi_key_slot(const uint8_t* key, size_t len) {
-    if (!key && len) return -1;
-    return int(crc16_checksum(key, len) & 0x3FFF);
 }
 
 int rsmi_group_member_of_key(const rsmi_group* s, const uint8_t* key, size_t len) {

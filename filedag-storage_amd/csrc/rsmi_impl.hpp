@@ -25,6 +25,7 @@
 #include "crc16.hpp"
 #include "crc32.hpp"
 #include "gf256.hpp"
+#include "group_commit.hpp"
 #include "rs_plan.hpp"
 
 namespace rsmi {
@@ -113,13 +114,9 @@ struct rsmi_ctx {
         int rc;
         bool done;
     };
-    std::mutex q_mu;
-    std::condition_variable q_cv;
-    std::vector<CoalReq*> q_pending;
-    bool q_executing = false;
+    rsmi::GroupCommit<CoalReq> coal;
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;
-    std::atomic<uint64_t> stat_coal_calls{0}, stat_coal_batches{0};
 };
 
 namespace rsmi {

@@ -1,0 +1,212 @@
+// fake_rsmi.cpp -- TEST INFRASTRUCTURE, never linked into the product.
+//
+// A stand-in for the device entry points of include/rsmi.h that the C++ host mirror calls
+// (csrc/host/*), coding with the CPU oracle (oracle/rs_oracle.c) and the host CRC halves, so
+// the mirror's concurrency -- datanode fan-out, quorum replay, the read-repair queue and
+// worker, GetMany / PutMany key concurrency, and the group-commit queue itself (the product's
+// csrc/group_commit.hpp, used here unchanged) -- runs under ThreadSanitizer and
+// AddressSanitizer on a host without a GPU (tests/cpp/Makefile sanitizer targets).  The
+// device-free entry points (status strings, shard checks, checksum host halves) are the
+// product's own csrc/rsmi_common.cpp.  Outputs are checked against the oracle by the tests as
+// usual; what the sanitizers check is the host code around the calls.
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../filedag-storage_amd/csrc/crc16.hpp"
+#include "../../filedag-storage_amd/csrc/crc32.hpp"
+#include "../../filedag-storage_amd/csrc/group_commit.hpp"
+#include "../../include/rsmi.h"
+#include "../../oracle/rs_oracle.h"
+
+namespace {
+
+struct Req {
+    bool encode;
+    const uint8_t* block;
+    size_t B;
+    uint8_t* out;  // encode: (k+m)*S shards; reconstruct: n*S shards in place
+    size_t S;
+    const uint8_t* present;
+    int data_only;
+    uint32_t* raw16;
+    uint32_t* raw32;
+    int rc;
+    bool done;
+};
+
+uint32_t r16(const uint8_t* p, size_t n) { return rsmi::crc16_tables().fold(0, p, n); }
+uint32_t r32(const uint8_t* p, size_t n) { return rsmi::crc32_tables().fold(0, p, n); }
+
+}  // namespace
+
+struct rsmi_ctx {
+    int k = 0, m = 0, n = 0;
+    rsmi::GroupCommit<Req> coal;
+};
+
+namespace {
+
+int encode_one(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
+    std::vector<uint8_t> sh(size_t(c->n) * S);
+    std::memcpy(sh.data(), data, size_t(c->k) * S);
+    if (rs_oracle_encode(c->k, c->m, sh.data(), S)) return RSMI_ERR_INVALID_ARG;
+    std::memcpy(parity, sh.data() + size_t(c->k) * S, size_t(c->m) * S);
+    return RSMI_OK;
+}
+
+// rebuild the rows flagged in want (and missing) of one block of n rows at p
+int reconstruct_one(rsmi_ctx* c, uint8_t* p, size_t S, const uint8_t* present, const uint8_t* want) {
+    std::vector<uint8_t> sh(p, p + size_t(c->n) * S);
+    if (rs_oracle_reconstruct(c->k, c->m, sh.data(), S, present, 0)) return RSMI_ERR_TOO_FEW_SHARDS;
+    for (int i = 0; i < c->n; i++)
+        if (!present[i] && want[i]) std::memcpy(p + size_t(i) * S, sh.data() + size_t(i) * S, S);
+    return RSMI_OK;
+}
+
+void run_batch(rsmi_ctx* c, std::vector<Req*>& batch) {
+    for (Req* r : batch) {
+        if (r->encode) {
+            const size_t S = r->S, k = size_t(c->k), n = size_t(c->n);
+            std::memset(r->out, 0, n * S);
+            std::memcpy(r->out, r->block, r->B);
+            r->rc = encode_one(c, r->out, r->out + k * S, S);
+            for (size_t i = 0; i < n && r->rc == RSMI_OK; i++) {
+                if (r->raw16) r->raw16[i] = r16(r->out + i * S, S);
+                if (r->raw32) r->raw32[i] = r32(r->out + i * S, S);
+            }
+        } else {
+            std::vector<uint8_t> want(size_t(c->n));
+            for (int i = 0; i < c->n; i++) want[size_t(i)] = !r->present[i] && (i < c->k || !r->data_only);
+            r->rc = reconstruct_one(c, r->out, r->S, r->present, want.data());
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsmi_open(int k, int m, int device, rsmi_ctx** out) {
+    (void)device;
+    if (!out) return RSMI_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (k <= 0 || m <= 0) return RSMI_ERR_INV_SHARD_NUM;
+    if (k + m > 256) return RSMI_ERR_MAX_SHARD_NUM;
+    auto* c = new rsmi_ctx();
+    c->k = k;
+    c->m = m;
+    c->n = k + m;
+    *out = c;
+    return RSMI_OK;
+}
+
+void rsmi_close(rsmi_ctx* c) { delete c; }
+
+void* rsmi_host_alloc(size_t bytes) { return std::malloc(bytes ? bytes : 1); }
+void rsmi_host_free(void* p) { std::free(p); }
+
+int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs, size_t S,
+                                size_t nblocks, uint32_t* raw16, uint32_t* raw32) {
+    if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    for (size_t b = 0; b < nblocks; b++) {
+        const int rc = encode_one(c, data + b * dbs, parity + b * pbs, S);
+        if (rc) return rc;
+        for (size_t i = 0; i < n; i++) {
+            const uint8_t* row = i < k ? data + b * dbs + i * S : parity + b * pbs + (i - k) * S;
+            if (raw16) raw16[b * n + i] = r16(row, S);
+            if (raw32) raw32[b * n + i] = r32(row, S);
+        }
+    }
+    (void)m;
+    return RSMI_OK;
+}
+
+int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs, size_t S,
+                           size_t nblocks) {
+    return rsmi_encode_batch_host_crcs(c, data, dbs, parity, pbs, S, nblocks, nullptr, nullptr);
+}
+
+int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                                          const uint8_t* present, const uint8_t* required, uint32_t* raw16,
+                                          uint32_t* raw32) {
+    if (!c || !shards || !present || !required) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    const size_t n = size_t(c->n);
+    for (size_t b = 0; b < nblocks; b++) {
+        const int rc = reconstruct_one(c, shards + b * bs, S, present, required);
+        if (rc) return rc;
+        for (size_t i = 0; i < n; i++) {
+            const bool rebuilt = !present[i] && required[i];
+            if (raw16) raw16[b * n + i] = rebuilt ? r16(shards + b * bs + i * S, S) : 0;
+            if (raw32) raw32[b * n + i] = rebuilt ? r32(shards + b * bs + i * S, S) : 0;
+        }
+    }
+    return RSMI_OK;
+}
+
+int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                                     const uint8_t* present, const uint8_t* required) {
+    return rsmi_reconstruct_rows_batch_host_crcs(c, shards, bs, S, nblocks, present, required, nullptr, nullptr);
+}
+
+int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                                const uint8_t* present, int data_only) {
+    if (!c || !present) return RSMI_ERR_INVALID_ARG;
+    std::vector<uint8_t> want(size_t(c->n));
+    for (int i = 0; i < c->n; i++) want[size_t(i)] = !present[i] && (i < c->k || !data_only);
+    return rsmi_reconstruct_rows_batch_host(c, shards, bs, S, nblocks, present, want.data());
+}
+
+int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size_t nrows, size_t S,
+                       uint32_t* raw16, uint32_t* raw32) {
+    if (!c || !rows || (!raw16 && !raw32)) return RSMI_ERR_INVALID_ARG;
+    for (size_t r = 0; r < nrows; r++) {
+        if (raw16) raw16[r] = r16(rows + r * row_stride, S);
+        if (raw32) raw32[r] = r32(rows + r * row_stride, S);
+    }
+    return RSMI_OK;
+}
+
+int rsmi_encode_block_coalesced_crcs(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
+                                     uint32_t* raw16, uint32_t* raw32) {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    if (B == 0) return RSMI_ERR_SHORT_DATA;
+    if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
+    Req req{true, block, B, shards_out, rsmi_shard_size(B, c->k), nullptr, 0, raw16, raw32, RSMI_OK, false};
+    c->coal.submit(req, 256, 0, [c](std::vector<Req*>& batch) { run_batch(c, batch); });
+    return req.rc;
+}
+
+int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw) {
+    return rsmi_encode_block_coalesced_crcs(c, block, B, shards_out, raw, nullptr);
+}
+
+int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+    if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    int np = 0;
+    bool any = false;
+    for (int i = 0; i < c->n; i++) {
+        np += present[i] ? 1 : 0;
+        any |= !present[i] && (i < c->k || !data_only);
+    }
+    if (!any) return RSMI_OK;
+    if (np < c->k) return RSMI_ERR_TOO_FEW_SHARDS;
+    Req req{false, nullptr, 0, shards, S, present, data_only, nullptr, nullptr, RSMI_OK, false};
+    c->coal.submit(req, 256, 0, [c](std::vector<Req*>& batch) { run_batch(c, batch); });
+    return req.rc;
+}
+
+long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
+    if (!c || !key) return -1;
+    if (!std::strcmp(key, "coalesced_calls")) return long(c->coal.calls());
+    if (!std::strcmp(key, "coalesced_batches")) return long(c->coal.batches());
+    return -1;
+}
+
+}  // extern "C"

@@ -42,6 +42,13 @@ static int g_fail = 0, g_checks = 0;
 
 static Bytes str(const char* s) { return Bytes(s, s + std::strlen(s)); }
 
+// Block sizes of the Dag Node tests: the bench shape (256 KiB) and a dag-pb 1 MiB leaf.  The
+// sanitizer builds (mode "sanitize": fake_rsmi.cpp codes with the scalar oracle, under
+// ThreadSanitizer / AddressSanitizer) run the same tests at a scale of 1/32.
+static size_t g_big = 262144, g_leaf = 1048590, g_huge = 4194304;
+static size_t g_fanout_min = size_t(128) << 10;  // sanitize: 0, so the fan-out pool runs at the small sizes
+static size_t big(long d = 0) { return size_t(long(g_big) + d); }
+
 static Bytes rand_bytes(std::mt19937_64& r, size_t n) {
     Bytes b(n);
     for (auto& x : b) x = uint8_t(r());
@@ -67,6 +74,7 @@ struct Cluster {
             std::fprintf(stderr, "NewDagNode: %s\n", s.err.c_str());
             std::exit(2);
         }
+        node->SetFanoutMinBytes(g_fanout_min);
         node->HealthCheckAll();
     }
 };
@@ -269,7 +277,7 @@ static void test_rs10_4_failures() {
     const int k = 10, m = 4, n = k + m;
     Cluster c(k, m);
     std::mt19937_64 r(0xF11EDA6);
-    const size_t sizes[] = {1, 6, 9, 10, 11, 4099, 65536, 262143, 262144, 262145, 1048590};
+    const size_t sizes[] = {1, 6, 9, 10, 11, 4099, 65536, big(-1), big(), big(1), g_leaf};
     std::vector<std::string> keys;
     std::vector<Bytes> blocks;
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); i++) {
@@ -310,7 +318,7 @@ static void test_read_repair() {
     const int k = 10, m = 4;
     Cluster c(k, m);
     std::mt19937_64 r(7);
-    const Bytes block = rand_bytes(r, 262144);
+    const Bytes block = rand_bytes(r, big());
     CHECK_OK(c.node->Put("blk", block));
     auto want = oracle_shards(k, m, block);
     // a datanode loses two shards of the block (data 3 and parity 12)
@@ -349,7 +357,7 @@ static void test_repair_datanode(bool batched) {
     std::vector<Bytes> blocks;
     for (int i = 0; i < 40; i++) {
         keys.push_back("key-" + std::to_string(i));
-        blocks.push_back(rand_bytes(r, i % 3 == 0 ? 262144 : (i % 3 == 1 ? 1000 + i : 65536)));
+        blocks.push_back(rand_bytes(r, i % 3 == 0 ? big() : (i % 3 == 1 ? 1000 + i : 65536)));
         CHECK_OK(c.node->Put(keys.back(), blocks.back()));
     }
     // datanode 6 is replaced by an empty one; one more node is down during the repair
@@ -379,7 +387,7 @@ static void test_putmany_batch() {
     std::vector<Bytes> blocks;
     for (int i = 0; i < 64; i++) {
         keys.push_back("pm-" + std::to_string(i));
-        blocks.push_back(rand_bytes(r, i % 2 ? 262144 : 4097));
+        blocks.push_back(rand_bytes(r, i % 2 ? big() : 4097));
     }
     blocks[7].clear();  // an empty block travels the per-block path
     CHECK_OK(c.node->PutMany(keys, blocks));
@@ -408,7 +416,7 @@ static void test_getmany() {
     std::vector<Bytes> blocks;
     for (int i = 0; i < 60; i++) {
         keys.push_back("gm-" + std::to_string(i));
-        blocks.push_back(rand_bytes(r, i % 4 == 0 ? 262144 : (i % 4 == 1 ? 6 : (i % 4 == 2 ? 65537 : 1048590))));
+        blocks.push_back(rand_bytes(r, i % 4 == 0 ? big() : (i % 4 == 1 ? 6 : (i % 4 == 2 ? 65537 : g_leaf))));
         CHECK_OK(c.node->Put(keys.back(), blocks.back()));
     }
     // shards lost in different patterns: node 1 down, some keys missing a data shard on
@@ -445,7 +453,7 @@ static void test_batches_span_staging_chunks() {
     std::vector<Bytes> blocks;
     for (int i = 0; i < 30; i++) {
         keys.push_back("big-" + std::to_string(i));
-        blocks.push_back(rand_bytes(r, 4194304));
+        blocks.push_back(rand_bytes(r, g_huge));
     }
     CHECK_OK(c.node->PutMany(keys, blocks));
     for (int i : {0, 11, 12, 23, 24, 29}) {  // chunk edges
@@ -470,7 +478,7 @@ static void test_migrate() {
     std::vector<Bytes> blocks;
     for (int i = 0; i < 24; i++) {
         keys.push_back("mig-" + std::to_string(i));
-        blocks.push_back(rand_bytes(r, i % 2 ? 262144 : 777));
+        blocks.push_back(rand_bytes(r, i % 2 ? big() : 777));
         CHECK_OK(from.node->Put(keys.back(), blocks.back()));
     }
     from.dn[0]->SetOffline(true);  // the source set is degraded during the move
@@ -502,7 +510,7 @@ static void test_gpu_entry_checksums() {
         std::mt19937_64 r(77 + k);
         std::vector<std::string> keys;
         std::vector<Bytes> blocks;
-        const size_t sizes[] = {1, 6, 17, 4099, 262144, 262145, 1048590};
+        const size_t sizes[] = {1, 6, 17, 4099, big(), big(1), g_leaf};
         for (size_t sz : sizes) {
             keys.push_back("single-" + std::to_string(sz));
             blocks.push_back(rand_bytes(r, sz));
@@ -513,7 +521,7 @@ static void test_gpu_entry_checksums() {
         std::vector<Bytes> bb;
         for (int i = 0; i < 37; i++) {
             bk.push_back("batch-" + std::to_string(i));
-            bb.push_back(rand_bytes(r, 262144));
+            bb.push_back(rand_bytes(r, big()));
         }
         CHECK_OK(gpu.node->PutMany(bk, bb));
         CHECK_OK(host.node->PutMany(bk, bb));
@@ -551,13 +559,13 @@ static void test_gpu_value_checksums() {
         std::mt19937_64 r(91 + k);
         std::vector<std::string> keys;
         std::vector<Bytes> blocks;
-        for (size_t sz : {size_t(6), size_t(4099), size_t(262144)}) {
+        for (size_t sz : {size_t(6), size_t(4099), big()}) {
             keys.push_back("single-" + std::to_string(sz));
             blocks.push_back(rand_bytes(r, sz));
             CHECK_OK(gpu.node->Put(keys.back(), blocks.back()));
             CHECK_OK(host.node->Put(keys.back(), blocks.back()));
         }
-        for (size_t sz : {size_t(17), size_t(262144), size_t(1048590)}) {
+        for (size_t sz : {size_t(17), big(), g_leaf}) {
             std::vector<std::string> bk;
             std::vector<Bytes> bb;
             for (int i = 0; i < 9; i++) {
@@ -644,7 +652,7 @@ static void test_gpu_verified_reads() {
         std::mt19937_64 r(21);
         std::vector<std::string> keys;
         std::vector<Bytes> blocks;
-        for (size_t sz : {size_t(6), size_t(4099), size_t(262144), size_t(1048590)}) {
+        for (size_t sz : {size_t(6), size_t(4099), big(), g_leaf}) {
             keys.push_back("v-" + std::to_string(sz));
             blocks.push_back(rand_bytes(r, sz));
             CHECK_OK(node->Put(keys.back(), blocks.back()));
@@ -686,7 +694,7 @@ static void test_concurrent_puts() {
     std::mt19937_64 r(99);
     for (int i = 0; i < T * per; i++) {
         keys[i] = "conc-" + std::to_string(i);
-        blocks[i] = rand_bytes(r, i % 7 == 0 ? 4099 : 262144);
+        blocks[i] = rand_bytes(r, i % 7 == 0 ? 4099 : big());
     }
     int rc;
     rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
@@ -750,7 +758,13 @@ int main(int argc, char** argv) {
     test_datanode_mutcask();
     test_quorum_helpers();
     test_config_and_slots();
-    if (mode == "gpu") {
+    if (mode == "sanitize") {  // the Dag Node suite at 1/32 scale on the fake device layer
+        g_big /= 32;
+        g_leaf = g_leaf / 32 + 14;
+        g_huge /= 32;
+        g_fanout_min = 0;
+    }
+    if (mode == "gpu" || mode == "sanitize") {
         test_dagnode_123456();
         test_rs10_4_failures();
         test_read_repair();
@@ -765,6 +779,7 @@ int main(int argc, char** argv) {
         test_gpu_verified_reads();
         test_concurrent_puts();
     }
+    release_shared_contexts();
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
     return g_fail ? 1 : 0;
 }

@@ -29,3 +29,24 @@ def test_dagnode_put_get_repair_gpu():
     out = subprocess.run([_binary(), "gpu"], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failed" in out.stdout
+
+
+def _sanitized(kind):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp"), "sanitize"])
+    return os.path.join(ROOT, "tests", "cpp", "build", f"test_dagnode_{kind}")
+
+
+@pytest.mark.parametrize("kind,marker", [("tsan", "WARNING: ThreadSanitizer"), ("asan", "ERROR: AddressSanitizer")])
+def test_host_mirror_under_sanitizers(kind, marker):
+    """The whole Dag Node suite (quorum, datanode fan-out pool, read-repair queue and worker,
+    GetMany / PutMany key concurrency, 12-thread concurrent Puts and degraded Gets through the
+    group-commit queue) at 1/32 scale under ThreadSanitizer and AddressSanitizer + UBSan, on
+    the test-only fake device layer (tests/cpp/fake_rsmi.cpp: the CPU oracle stands in for
+    the GPU, so no device is needed).  Clean means: every check passes and the sanitizer
+    reports nothing."""
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
+               ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1")
+    out = subprocess.run([_sanitized(kind), "sanitize"], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "sanitize: " in out.stdout and " 0 failed" in out.stdout
+    assert marker not in out.stderr and "runtime error" not in out.stderr
