@@ -372,7 +372,7 @@ Status DagNode::DeleteBlock(const std::string& key) {  // node.go:191-208
 }
 
 // ------------------------------------------------------------------ read path
-Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:220-275
+Status DagNode::fetch_for_get(const std::string& key, Fetched* f, bool defer_verify) {  // node.go:220-275
     std::vector<StorageNode*> online;
     Status s = get_meta_info(key, &f->meta, &online);
     if (!s.ok()) return s;
@@ -406,7 +406,7 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
                 got[j] = gpu_verified_reads_ ? online[j]->client->GetForVerify(key, &metas[j], &data[j], &stored[j])
                                              : online[j]->client->Get(key, &metas[j], &data[j]);
             }, size_t(ceil_frac(f->meta.block_size, config_.data_blocks)));
-            if (gpu_verified_reads_) verify_wave(wave, metas, data, stored, got);
+            if (gpu_verified_reads_ && !defer_verify) verify_wave(wave, metas, data, stored, got);
             for (int j : wave) fetched[j] = 1;
         }
         if (!got[i].ok()) {
@@ -418,7 +418,60 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f) {  // node.go:
         w.add(got[i]);
     }
     std::sort(f->repair.begin(), f->repair.end());
+    if (gpu_verified_reads_ && defer_verify) {
+        f->metas = std::move(metas);
+        f->stored = std::move(stored);
+    }
     return w.result(kErrReadQuorum);
+}
+
+void DagNode::verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>& st, const std::vector<char>& skip,
+                             std::vector<char>* bad) {
+    bad->assign(fs.size(), 0);
+    // (key, node) of every accepted shard with a stored checksum to check, by shard size
+    std::map<size_t, std::vector<std::pair<size_t, int>>> by_size;
+    for (size_t q = 0; q < fs.size(); q++) {
+        if (!st[q].ok() || fs[q].stored.empty() || skip[q]) continue;
+        for (size_t i = 0; i < fs[q].shards.size(); i++)
+            if (!fs[q].shards[i].empty() && !fs[q].stored[i].verified)
+                by_size[fs[q].shards[i].size()].push_back({q, int(i)});
+    }
+    for (auto& g : by_size) {
+        const size_t S = g.first, w = g.second.size();
+        bool want32 = false;
+        for (auto& e : g.second) want32 |= fs[e.first].stored[size_t(e.second)].has_value_crc;
+        std::vector<uint32_t> r16(w, 0), r32(w, 0);
+        int rc = RSMI_OK;
+        rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+        // rows gathered into page-locked staging by the key pool, then read in place by one GPU
+        // pass (staging_blocks bounds the buffer; a huge GetMany takes several passes)
+        const size_t per = std::max<size_t>(1, kStagingBytes / S);
+        for (size_t r0 = 0; ctx && r0 < w && rc == RSMI_OK; r0 += per) {
+            const size_t nr = std::min(per, w - r0);
+            uint8_t* flat = thread_staging().reserve(nr * S);
+            if (!flat) {
+                rc = RSMI_ERR_DEVICE;
+                break;
+            }
+            const int parts = int(std::min<size_t>(nr, 64));
+            fan_keys(parts, [&](int t) {
+                for (size_t i = size_t(t); i < nr; i += size_t(parts)) {
+                    const auto& e = g.second[r0 + i];
+                    std::memcpy(flat + i * S, fs[e.first].shards[size_t(e.second)].data(), S);
+                }
+            });
+            rc = rsmi_crc_rows_host(ctx, flat, S, nr, S, r16.data() + r0, want32 ? r32.data() + r0 : nullptr);
+        }
+        for (size_t i = 0; i < w; i++) {
+            const size_t q = g.second[i].first, j = size_t(g.second[i].second);
+            const Bytes& meta = fs[q].metas[j];
+            const DataNodeClient::Stored& sd = fs[q].stored[j];
+            // no device: the read fails loudly, through the per-key path (there is no CPU path)
+            if (rc || (sd.has_value_crc && value_checksum(meta, S, sd.crc, r32[i]) != sd.value_crc) ||
+                entry_checksum(meta, S, r16[i]) != sd.crc)
+                (*bad)[q] = 1;
+        }
+    }
 }
 
 void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas,
@@ -504,21 +557,64 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
         std::vector<Fetched> fs(nk);
         // the keys' fetches run concurrently, like the reference's concurrent Gets (one
         // goroutine per dag pool request), each with its own node fan-out
-        fan_keys(int(nk), [&](int q) { (*statuses)[k0 + q] = fetch_for_get(keys[k0 + q], &fs[q]); });
+        // With GPU-verified reads, the first waves of all keys are checked together: one GPU
+        // pass per shard size instead of one per key and wave.  A key with a bad shard runs the
+        // per-key fetch again (checked wave by wave), so quorum, repair list and errors are
+        // exactly Get's; its first attempt only read.
+        fan_keys(int(nk), [&](int q) { (*statuses)[k0 + q] = fetch_for_get(keys[k0 + q], &fs[q], true); });
+        // does key q's data need the batched decode below (else the per-key path decides)
+        auto needs_decode = [&](size_t q) {
+            if (!(*statuses)[k0 + q].ok() || fs[q].meta.block_size <= 0) return false;
+            bool data_missing = false, any = false;
+            for (int c = 0; c < k; c++) data_missing |= fs[q].shards[c].empty();
+            for (auto& sh : fs[q].shards) any |= !sh.empty();
+            return data_missing && any;
+        };
+        // keys whose check rides on the batched decode: exactly k survivors (the decode reads
+        // them all) and entry checksums only (the decode kernel yields R, not R32)
+        std::vector<char> fused(nk, 0), redo_after(nk, 0);
+        auto refetch = [&](const std::vector<char>& mask) {
+            std::vector<int> redo;
+            for (size_t q = 0; q < nk; q++)
+                if (mask[q]) redo.push_back(int(q));
+            fan_keys(int(redo.size()), [&](int t) {
+                const size_t q = size_t(redo[size_t(t)]);
+                fs[q] = Fetched();
+                (*statuses)[k0 + q] = fetch_for_get(keys[k0 + q], &fs[q]);
+            });
+        };
+        if (gpu_verified_reads_) {
+            for (size_t q = 0; q < nk; q++) {
+                if (!needs_decode(q) || fs[q].stored.empty()) continue;
+                int np = 0;
+                bool r32 = false;
+                for (int c = 0; c < n; c++)
+                    if (!fs[q].shards[c].empty()) {
+                        np++;
+                        r32 |= fs[q].stored[c].has_value_crc;
+                    }
+                fused[q] = np == k && !r32;
+            }
+            std::vector<Status> st(statuses->begin() + long(k0), statuses->begin() + long(k0 + nk));
+            std::vector<char> bad;
+            verify_fetched(fs, st, fused, &bad);
+            refetch(bad);
+        }
         // (block size, survivor pattern) -> chunk positions of keys whose data shards need decoding
         std::map<std::pair<int32_t, std::string>, std::vector<size_t>> groups;
         for (size_t q = 0; q < nk; q++) {
-            const Status& st = (*statuses)[k0 + q];
-            if (!st.ok()) continue;
-            bool data_missing = false;
-            for (int c = 0; c < k; c++) data_missing |= fs[q].shards[c].empty();
-            bool any = false;
-            for (auto& sh : fs[q].shards) any |= !sh.empty();
-            if (!data_missing || !any || fs[q].meta.block_size <= 0) continue;  // per-key path decides
+            if (!needs_decode(q)) {
+                if (fused[q]) redo_after[q] = 1;  // cannot happen; checked the per-key way regardless
+                continue;
+            }
             std::string pat(static_cast<size_t>(n), '0');
             for (int c = 0; c < n; c++) pat[c] = fs[q].shards[c].empty() ? '0' : '1';
             groups[{fs[q].meta.block_size, pat}].push_back(q);
         }
+        // a fused key whose decode did not run is checked by a per-key fetch again
+        auto unchecked = [&](const std::vector<size_t>& qs, size_t b0, size_t nb) {
+            for (size_t j = b0; j < b0 + nb; j++) redo_after[qs[j]] |= fused[qs[j]];
+        };
         for (auto& g : groups) {
             const size_t S = rsmi_shard_size(size_t(g.first.first), k);
             std::vector<uint8_t> present(static_cast<size_t>(n));
@@ -526,21 +622,48 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
             bool sizes_ok = true;  // every present shard must have the common size (else per-key errors)
             for (size_t q : g.second)
                 for (int c = 0; c < n; c++) sizes_ok &= !present[c] || fs[q].shards[c].size() == S;
-            if (!sizes_ok) continue;
             int rc;
-            rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
-            if (!ctx) continue;  // finish_get reports the device error per key
+            rsmi_ctx* ctx = sizes_ok ? shared_context(k, m, device_, &rc) : nullptr;
+            if (!ctx) {  // finish_get reports the size or device error per key
+                unchecked(g.second, 0, g.second.size());
+                continue;
+            }
+            bool verify = false;
+            for (size_t q : g.second) verify |= fused[q] != 0;
+            std::vector<int> used;  // the survivors the decode reads, as rsmi_reconstruct_batch_host_verify
+            for (int c = 0; c < n && int(used.size()) < k; c++)
+                if (present[c]) used.push_back(c);
             const size_t chunk = staging_blocks(size_t(n) * S);
+            std::vector<uint32_t> r16(verify ? chunk * size_t(k) : 0);
             for (size_t b0 = 0; b0 < g.second.size(); b0 += chunk) {
                 const size_t nb = std::min(chunk, g.second.size() - b0);
                 uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
-                if (!flat) continue;
+                if (!flat) {
+                    unchecked(g.second, b0, nb);
+                    continue;
+                }
                 fan_keys(int(nb), [&](int j) {
                     for (int c = 0; c < n; c++)
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
-                if (rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1) != RSMI_OK)
+                // with verified reads the same kernel returns R of every survivor it read
+                const int drc = verify ? rsmi_reconstruct_batch_host_verify(ctx, flat, size_t(n) * S, S, nb,
+                                                                            present.data(), 1, r16.data())
+                                       : rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1);
+                if (drc != RSMI_OK) {
+                    unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
+                }
+                for (size_t j = 0; verify && j < nb; j++) {
+                    const size_t q = g.second[b0 + j];
+                    if (!fused[q]) continue;
+                    for (int c = 0; c < k; c++) {
+                        const size_t i = size_t(used[size_t(c)]);
+                        const DataNodeClient::Stored& sd = fs[q].stored[i];
+                        if (!sd.verified && entry_checksum(fs[q].metas[i], S, r16[j * size_t(k) + size_t(c)]) != sd.crc)
+                            redo_after[q] = 1;
+                    }
+                }
                 fan_keys(int(nb), [&](int j) {
                     for (int c = 0; c < k; c++)
                         if (!present[c]) {
@@ -550,6 +673,9 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                 });
             }
         }
+        // a bad survivor: that key's fetch again, checked wave by wave (quorum, repair list and
+        // errors exactly Get's, as above)
+        refetch(redo_after);
         fan_keys(int(nk), [&](int q) {
             if ((*statuses)[k0 + q].ok()) (*statuses)[k0 + q] = finish_get(keys[k0 + q], fs[q], &(*blocks)[k0 + q]);
         });

@@ -129,8 +129,17 @@ private:
         Meta meta;
         std::vector<Bytes> shards;
         std::vector<int> repair;
+        // deferred verification (GetMany): the accepted shards' entry metas and stored checksums
+        std::vector<Bytes> metas;
+        std::vector<DataNodeClient::Stored> stored;
     };
-    Status fetch_for_get(const std::string& key, Fetched* f);
+    // defer_verify: with GPU-verified reads on, accept the first wave's shards unchecked and keep
+    // their stored checksums in f, for one batched check across many keys (verify_fetched)
+    Status fetch_for_get(const std::string& key, Fetched* f, bool defer_verify = false);
+    // the batched check of deferred fetches: one GPU call per shard size over every key's
+    // accepted shards; bad[q] is set for keys with a shard that fails
+    void verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>& st, const std::vector<char>& skip,
+                        std::vector<char>* bad);
     Status finish_get(const std::string& key, Fetched& f, Bytes* block);
     Status get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online);
     Status repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,

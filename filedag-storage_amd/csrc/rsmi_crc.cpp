@@ -112,17 +112,18 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
     return RSMI_OK;
 }
 
-// Encode with the CRC-16 fused in, then R(row) of all k+m rows of every block into
-// raw[b * (k+m) + row] (device or page-locked host memory).  Needs k <= 16, m <= 4 and either
-// an aligned layout or S >= 16; returns RSMI_ERR_INVALID_ARG otherwise (callers then run the
-// separate pass).
-int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                      size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
-    const size_t n = size_t(c->n);
-    if (c->k > 16 || plan.tiles.size() != 1) return RSMI_ERR_INVALID_ARG;
+// Any single-tile plan with the CRC-16 fused in (rs_fast_kernel CRC variants), then R(row) of
+// its K input rows and MT output rows into raw[b * (K + MT) + r] (input row c at r = c, output
+// row j at r = K + j; device or page-locked host memory).  Needs K <= 16, one plan tile
+// (MT <= 4) and either an aligned layout or S >= 16; returns RSMI_ERR_INVALID_ARG otherwise
+// (callers then run the separate pass).
+int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+    if (plan.tiles.size() != 1 || plan.tiles[0].K > 16) return RSMI_ERR_INVALID_ARG;
+    const size_t nsh = size_t(plan.tiles[0].K + plan.tiles[0].MT);
     const size_t cpb = (S + 15) / 16, tpb = (cpb + kWave - 1) / kWave;
-    const size_t ns2 = ((n + 3) / 4 + 1) / 2;
-    const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * n * 4;
+    const size_t ns2 = ((nsh + 3) / 4 + 1) / 2;
+    const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * nsh * 4;
     int rc;
     if ((rc = ensure_crc_tables(c))) return rc;
     if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;
@@ -137,9 +138,9 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
     const uint32_t* tb = c->d_crc_tbl;
     const uint32_t* rec = fz.rec;
     const uint32_t* tail = fz.tail;
-    uint32_t tpb32 = uint32_t(tpb), nsh = uint32_t(n);
+    uint32_t tpb32 = uint32_t(tpb), nsh32 = uint32_t(nsh);
     uint64_t S64 = S, nb64 = nblocks;
-    void* args[] = {&tb, &rec, &tail, &tpb32, &nsh, &S64, &nb64, &raw};
+    void* args[] = {&tb, &rec, &tail, &tpb32, &nsh32, &S64, &nb64, &raw};
     // one wave per block, a persistent grid of up to 8 workgroups per CU (the power tables take
     // 15 KiB of LDS per workgroup, so 10 fit)
     const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
@@ -147,6 +148,12 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
     if (!fn) return RSMI_ERR_INVALID_ARG;
     HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(kWG), args, 0, st));
     return RSMI_OK;
+}
+
+// Encode with the CRC-16 fused in: raw[b * (k+m) + row] = R(row) of all k+m rows.
+int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                      size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+    return launch_plan_crc(c, plan, in, in_rs, in_bs, out, out_rs, out_bs, S, nblocks, raw, st);
 }
 
 }  // namespace impl

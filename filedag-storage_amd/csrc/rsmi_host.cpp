@@ -494,4 +494,55 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t b
     return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required, raw16_out, raw32_out);
 }
 
+int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                       const uint8_t* present, int data_only, uint32_t* raw16_in) {
+    if (!c || !shards || !present || !raw16_in) return RSMI_ERR_INVALID_ARG;
+    if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    if (block_stride < size_t(c->n) * S) return RSMI_ERR_INVALID_ARG;
+    const size_t k = size_t(c->k), n = size_t(c->n);
+    std::vector<int> used;
+    for (int i = 0; i < c->n && used.size() < k; i++)
+        if (present[i]) used.push_back(i);
+    if (used.size() < k) return RSMI_ERR_TOO_FEW_SHARDS;
+    if (nblocks == 0) return RSMI_OK;
+    const std::vector<uint8_t> want = want_mask(c, present, data_only);
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        int rc = ensure_device(c);
+        if (rc) return rc;
+        HIP_TRY(hipSetDevice(c->device));
+        uint8_t* dev = host_alias(shards, (nblocks - 1) * block_stride + n * S);
+        std::shared_ptr<Plan> plan;
+        if (dev && c->opt_zero_copy && reconstruct_precheck(c, present, want.data()) == 0 &&
+            (rc = reconstruct_plan(c, present, want.data(), plan)) == RSMI_OK) {
+            // one kernel reads every survivor once, in place over PCIe, for both the rebuild and
+            // its R(row); the combine lands R of the K inputs and MT outputs per block
+            const size_t nsh = size_t(plan->tiles.empty() ? 0 : plan->tiles[0].K + plan->tiles[0].MT);
+            if ((rc = reserve(c->d_crc, c->crc_cap, nblocks * nsh * 4))) return rc;
+            hipStream_t st = c->staging[0].stream;
+            uint32_t* d = reinterpret_cast<uint32_t*>(c->d_crc);
+            rc = launch_plan_crc(c, *plan, dev, S, block_stride, dev, S, block_stride, S, nblocks, d, st);
+            if (rc == RSMI_OK) {
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<uint32_t> all(nblocks * nsh);
+                HIP_TRY(hipMemcpy(all.data(), d, all.size() * 4, hipMemcpyDeviceToHost));
+                for (size_t b = 0; b < nblocks; b++)
+                    std::memcpy(raw16_in + b * k, all.data() + b * nsh, k * 4);
+                return RSMI_OK;
+            }
+            if (rc != RSMI_ERR_INVALID_ARG) return rc;
+        }
+    }
+    // any other layout or plan: the rebuild, then a CRC pass over each survivor row
+    int rc = rsmi_reconstruct_batch_host(c, shards, block_stride, S, nblocks, present, data_only);
+    if (rc) return rc;
+    std::vector<uint32_t> r(nblocks);
+    for (size_t j = 0; j < k; j++) {
+        if ((rc = rsmi_crc_rows_host(c, shards + size_t(used[j]) * S, block_stride, nblocks, S, r.data(), nullptr)))
+            return rc;
+        for (size_t b = 0; b < nblocks; b++) raw16_in[b * k + j] = r[b];
+    }
+    return RSMI_OK;
+}
+
 }  // extern "C"

@@ -175,6 +175,8 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
                uint64_t nblocks, uint32_t* out, uint64_t out_bs, hipStream_t stream, bool zero = true);
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                              size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
+int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
 void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb);
 void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch);

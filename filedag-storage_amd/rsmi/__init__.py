@@ -100,6 +100,8 @@ def lib() -> ctypes.CDLL:
                                                ctypes.c_void_p, c_size, ctypes.c_void_p]),
         "rsmi_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
                                                        ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_reconstruct_batch_host_verify": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
+                                                              ctypes.c_int, ctypes.c_void_p]),
         "rsmi_reconstruct_rows_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                                  u8p, ctypes.c_void_p, ctypes.c_void_p]),
         "rsmi_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_long]),
@@ -290,6 +292,14 @@ class Codec:
         """R32(row) of the mutcask value checksum (CRC-32 IEEE, raw) for every row, on the device."""
         _check(lib().rsmi_crc32_rows_dev(self._h, d_rows, rs, bs, nrows, S, nblocks, d_out, out_bs,
                                          stream or None))
+
+    def reconstruct_batch_host_verify_ptr(self, ptr: int, bs: int, S: int, nblocks: int, present: Sequence[bool],
+                                          data_only: bool, raw16_ptr: int) -> None:
+        """reconstruct_batch_host_ptr that also writes R(row) of the k survivor rows it read into
+        raw16_ptr[b*k + c] (uint32; survivors = the first k present shards)."""
+        p = bytearray(1 if x else 0 for x in present)
+        _check(lib().rsmi_reconstruct_batch_host_verify(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
+                                                        1 if data_only else 0, raw16_ptr))
 
     def reconstruct_rows_batch_host_crcs_ptr(self, shards_ptr: int, block_stride: int, S: int, nblocks: int,
                                              present: Sequence[bool], required: Sequence[bool],

@@ -246,6 +246,15 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* ctx, const uint8_t* data, size_t data_
                                 size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
                                 uint32_t* raw32_out);
 
+/* rsmi_reconstruct_batch_host (same arguments, results and errors) that also returns R(row), the
+ * datanode CRC-16 of the entry's shard bytes, of the k survivor rows it read: raw16_in[b*k + c] =
+ * R(shard used[c]), used = the first k present shards (rsmi_decode_matrix's used_rows).  A
+ * reader that fetched shards unchecked (the datanodes' stored checksums, server.go:93-97) checks
+ * them for free on a degraded read: with page-locked shards one kernel reads each survivor once
+ * for both; otherwise a CRC pass over the survivors follows the rebuild. */
+int rsmi_reconstruct_batch_host_verify(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
+                                       const uint8_t* present, int data_only, uint32_t* raw16_in);
+
 /* rsmi_reconstruct_rows_batch_host plus the raw checksums of every row it rebuilt, from the
  * GPU where the rows land: raw16_out / raw32_out[b*(k+m) + r] = R(row) / R32(row) for rows r
  * that are required and missing, 0 for the others; either may be NULL.  RepairDataNode's

@@ -162,6 +162,19 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t 
     return rsmi_reconstruct_rows_batch_host(c, shards, bs, S, nblocks, present, want.data());
 }
 
+int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t S, size_t nblocks,
+                                       const uint8_t* present, int data_only, uint32_t* raw16_in) {
+    if (!c || !shards || !present || !raw16_in) return RSMI_ERR_INVALID_ARG;
+    std::vector<int> used;
+    for (int i = 0; i < c->n && int(used.size()) < c->k; i++)
+        if (present[i]) used.push_back(i);
+    if (int(used.size()) < c->k) return RSMI_ERR_TOO_FEW_SHARDS;
+    for (size_t b = 0; b < nblocks; b++)
+        for (size_t j = 0; j < used.size(); j++)
+            raw16_in[b * used.size() + j] = r16(shards + b * bs + size_t(used[j]) * S, S);
+    return rsmi_reconstruct_batch_host(c, shards, bs, S, nblocks, present, data_only);
+}
+
 int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size_t nrows, size_t S,
                        uint32_t* raw16, uint32_t* raw32) {
     if (!c || !rows || (!raw16 && !raw32)) return RSMI_ERR_INVALID_ARG;

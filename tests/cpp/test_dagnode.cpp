@@ -678,6 +678,23 @@ static void test_gpu_verified_reads() {
             CHECK(gm[j] == blocks[j]);
         }
         dn[1]->flip = false;
+        // degraded GetMany: data node 0 down, so every key decodes from 10 survivors whose
+        // checksums (badger) come out of the decode kernel itself; first all clean, then a
+        // survivor corrupted in transit, which the decode's check catches
+        dn[0]->SetOffline(true);
+        for (int pass = 0; pass < 2; pass++) {
+            dn[3]->flip = pass == 1;
+            node->GetMany(keys, &gm, &st, 8);
+            for (size_t j = 0; j < keys.size(); j++) {
+                CHECK_OK(st[j]);
+                CHECK(gm[j] == blocks[j]);
+                Bytes one;
+                CHECK_OK(node->Get(keys[j], &one));
+                CHECK(one == blocks[j]);
+            }
+        }
+        dn[3]->flip = false;
+        dn[0]->SetOffline(false);
         node->Close();
     }
 }

@@ -336,3 +336,43 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, wpc):
         for i in range(n):
             assert r[b, i] < 0x10000
             assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (b, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,S,nb,lost,pinned", [(10, 4, 26215, 24, [0], True), (10, 4, 26215, 24, [3, 11], False),
+                                                  (10, 4, 26215, 9, [2, 5, 7, 9], True), (4, 2, 65536, 8, [1], True),
+                                                  (16, 4, 4097, 5, [0, 15], True), (3, 2, 7, 6, [1], True),
+                                                  (20, 4, 333, 3, [4], True), (10, 4, 26215, 4, [], True),
+                                                  (10, 4, 26215, 4, [12], True), (2, 1, 16, 7, [0], True)])
+def test_reconstruct_verify_survivor_crcs(k, m, S, nb, lost, pinned):
+    """rsmi_reconstruct_batch_host_verify: the rebuild equals the oracle's and raw16[b*k + c] is
+    R of survivor used[c] (the first k present rows), whether one fused kernel read page-locked
+    shards (k <= 16, rows >= 16 B) or the separate pass ran (pageable, k > 16, S < 16, nothing
+    to rebuild)."""
+    n = k + m
+    data = np.random.default_rng(S + k + len(lost)).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+    full = np.concatenate([data, orc.encode_fast(k, m, data)], axis=1)
+    present = [i not in lost for i in range(n)]
+    used = [i for i in range(n) if present[i]][:k]
+    with rsmi.Codec(k, m) as c:
+        if pinned:
+            ptr = rsmi.lib().rsmi_host_alloc(nb * n * S)
+            sh = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * n * S)).from_address(ptr)).reshape(nb, n, S)
+        else:
+            sh = np.empty((nb, n, S), dtype=np.uint8)
+        try:
+            sh[:] = full
+            sh[:, lost] = 0
+            raw = np.zeros((nb, k), dtype=np.uint32)
+            c.reconstruct_batch_host_verify_ptr(sh.ctypes.data, n * S, S, nb, present, False, raw.ctypes.data)
+            kern = c.last_kernel()
+            assert np.array_equal(sh, full)
+            if pinned and lost and k <= 16 and S >= 16:
+                assert ",CRC" in kern, kern
+            for b in range(nb):
+                for j, r in enumerate(used):
+                    assert rsmi.crc16_entry(b"", int(raw[b, j]), S) == orc.crc16_ibm(full[b, r].tobytes()), (b, j)
+        finally:
+            if pinned:
+                del sh
+                rsmi.lib().rsmi_host_free(ptr)
