@@ -81,6 +81,10 @@ def parse(argv=None):
                    help="rehearsal only: every rank uses cuda:0 (multi-rank path on a 1-GPU box)")
     p.add_argument("--copy-inclusive", action="store_true",
                    help="also time host->device->host through pinned buffers (reported, never `value`)")
+    p.add_argument("--group", default="", metavar="DEVS",
+                   help="with --copy-inclusive: also run the host batch through one device group "
+                        "(rsmi_group_*, one process over several GPUs) of these devices, e.g. 0,1,2,3 or "
+                        "0,0 (two contexts on one GPU); 'all' = every visible GPU")
     p.add_argument("--no-verify", action="store_true", help="skip the post-run self check")
     p.add_argument("--mock", action="store_true",
                    help="test only: a CPU stand-in for the device step, to exercise the launcher, the "
@@ -285,7 +289,7 @@ def load_traffic(label):
         return None
 
 
-def copy_inclusive(codec, k, m, S, nb, lost, data_only, world):
+def copy_inclusive(codec, k, m, S, nb, lost, data_only, world, group=None):
     """Host-resident encode(+reconstruct) through page-locked buffers (the zero-copy direct
     path).  Every rank runs each leg at the same time, so the aggregate shows
     what the ranks' PCIe links and the shared host memory give together.  PCIe-bound; reported
@@ -347,6 +351,16 @@ def copy_inclusive(codec, k, m, S, nb, lost, data_only, world):
         other.close()
         if errs:
             raise errs[0]
+    if group:
+        # the same host batch spread over a device group from this one process: contiguous
+        # block ranges, one member context (own streams and staging) and host thread each
+        with rsmi.DeviceGroup(k, m, group) as g:
+            gr = {"devices": list(group)}
+            gr["encode_GiBs"] = round(leg(lambda: g.encode_batch_host_ptr(din, k * S, dpar, m * S, S, nb)), 2)
+            if lost:
+                gr["reconstruct_GiBs"] = round(leg(lambda: g.reconstruct_batch_host_ptr(
+                    dsh, n * S, S, nb, present, data_only)), 2)
+        res["group"] = gr
     for p in (din, dpar, dsh):
         L.rsmi_host_free(p)
     return res
@@ -601,8 +615,12 @@ def main():
             "avg_launch_ms_incl_event_gap": round(rec_ms, 4),
         }
     if a.copy_inclusive:
+        group = None
+        if a.group and world == 1:
+            group = (list(range(torch.cuda.device_count())) if a.group == "all"
+                     else [int(x) for x in a.group.split(",")])
         out["copy_inclusive"] = copy_inclusive(codec, k, m, S, min(nb, max(1, (1 << 30) // B)), lost, data_only,
-                                               world)
+                                               world, group)
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         data_host = lay.rows(buf, 0, k).cpu().numpy()  # the bench's own blocks
         out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds)

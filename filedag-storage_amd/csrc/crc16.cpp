@@ -39,6 +39,12 @@ Crc16Tables::Crc16Tables() {
         for (int h = 0; h < 2; h++)
             for (int q = 0; q < 4; q++)
                 for (int v = 0; v < 16; v++) Q[p][h][q][v] = shift(U[15 - p][v << (4 * h)], uint64_t(16 * (3 - q)));
+    for (int i = 0; i < kCrcPowers; i++)
+        for (int h = 0; h < 4; h++)
+            for (int v = 0; v < 16; v++) P4[i][h][v] = pow2(i, uint16_t(v << (4 * h)));
+    for (int k = 0; k < 8; k++)
+        for (int p = 0; p < 32; p++)
+            for (int v = 0; v < 16; v++) G[k][p][v] = shift(N[p][v], uint64_t(1024 * (7 - k)));
     // the group order the negative shifts rely on: A^32767 = I on a basis
     for (int bit = 0; bit < 16; bit++)
         if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();

@@ -35,6 +35,12 @@ struct Crc16Tables {
     // A^(16 (3 - q)) (U[15 - p][v << 4h]) -- lane q of a 4-lane quad folds its chunk relative to
     // the END OF THE QUAD, so the quad's four values combine by plain XOR
     uint16_t Q[16][2][4][16];
+    // tile-set nibble tables of the rows pass: G[k] = A^(1024 (7 - k)) (N) -- tile k of an
+    // 8-tile group folds relative to the END OF THE GROUP, so the group's tiles combine by XOR
+    uint16_t G[8][32][16];
+    // nibble-sliced power tables of the rows pass: P4[i][h][v] = A^(2^i)(v << 4h) (16-entry
+    // tables never conflict; 1.9 KiB where P takes 15 KiB)
+    uint16_t P4[kCrcPowers][4][16];
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
     // A^n(s) for any n >= 0 (reduced mod 32767)

@@ -387,19 +387,30 @@ __global__ __launch_bounds__(kWG) void rs_repitch_kernel(const uint8_t* __restri
 void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 
 // ------------------------------------------------------------------ CRC-16 of shard rows
-// R(row) of the datanode entry checksum (crc16.hpp has the algebra).  A wave owns one
-// segment of kCrcSegTiles consecutive 1 KiB tiles of one row: each lane loads its 16-byte
-// chunk of every tile (all loads in flight first), folds each chunk with positional LDS
-// lookups -- 32 nibble lookups in 16-entry tables (every wave-wide lookup reads 8 distinct
-// dwords in 8 distinct banks, so it never conflicts) -- and carries a running register
-// across the tiles (A^1024 between tiles).  A
-// Hillis-Steele scan over the 64 lanes (A^(16*2^j) per level) leaves the segment's value,
-// relative to the segment's end, in lane 63; shifting it by (S - segment end) mod 32767
-// bytes places it relative to the row's end, and one atomic XOR adds it into the row's
-// word.  Bytes at or past S read as zero (zero bytes contribute nothing to R, they only
-// move the reference point, which the final shift accounts for).
+// R(row) of the datanode entry checksum (crc16.hpp has the algebra).  A wave owns one item: a
+// super-segment of up to kCrcSupGroups groups of kCrcSegTiles = 8 consecutive 1 KiB tiles of
+// one row.  Each lane folds its 16-byte chunk of every tile with positional LDS lookups -- 32
+// nibble lookups in 16-entry tables (every wave-wide lookup reads 8 distinct dwords in 8
+// distinct banks, so it never conflicts).  Tile k of a group uses its own table set G[k]
+// (relative to the group's end), so the folds of a group are independent and combine by XOR,
+// and a running register carries the groups (A^8192 between them): no dependent power step per
+// tile.  A Hillis-Steele scan over the 64 lanes (A^(16*2^j) per level) leaves the item's
+// value, relative to the item's end, in lane 63; shifting it by (S - item end) mod 32767 bytes
+// places it relative to the row's end, and one atomic XOR adds it into the row's word.  The
+// scan and the shift cost about as much as 8 tiles of folding, so items span 32 tiles
+// (8-tile items spent 30 % of the pass there).  Powers use nibble-sliced tables
+// (P4, conflict-free, 1.9 KiB), so a workgroup stages 12 KiB of LDS.  Bytes at or past S read
+// as zero (zero bytes contribute nothing to R, they only move the reference point, which the
+// final shift accounts for).
 __device__ __forceinline__ uint32_t crc_pow(const uint16_t* sP, int i, uint32_t s) {
     return uint32_t(sP[i * 512 + (s & 0xFF)]) ^ uint32_t(sP[i * 512 + 256 + (s >> 8)]);
+}
+
+// A^(2^i)(s) through the nibble-sliced tables P4[i][4][16]
+__device__ __forceinline__ uint32_t crc_pow4(const uint16_t* sQ, int i, uint32_t s) {
+    const uint16_t* t = sQ + i * 64;
+    return xor3(uint32_t(t[s & 15]), uint32_t(t[16 + ((s >> 4) & 15)]), uint32_t(t[32 + ((s >> 8) & 15)])) ^
+           uint32_t(t[48 + ((s >> 12) & 15)]);
 }
 
 __device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4& v) {
@@ -420,110 +431,147 @@ __device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4
     return c;
 }
 
+// The item's value -> row word: lane scan, shift to the row's end, one atomic XOR (lane 63).
+__device__ __forceinline__ void crc_item_out(const uint16_t* sQ, uint32_t lane, uint32_t acc, uint64_t S,
+                                             uint64_t item_end, uint32_t* word) {
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
+        const uint32_t t = __shfl_up(w, 1u << j);
+        if (lane >= (1u << j)) acc ^= t;
+    }
+    int64_t e = (int64_t(S) - int64_t(item_end)) % int64_t(kCrcOrder);
+    if (e < 0) e += kCrcOrder;
+#pragma unroll
+    for (int i = 0; i < kCrcPowers; i++)
+        if ((e >> i) & 1) acc = crc_pow4(sQ, i, acc);
+    if (lane == kWave - 1) atomicXor(word, acc);
+}
+
+// Position of item `it` (nsup items per row): its row and first tile.
+struct CrcItem {
+    uint64_t b;
+    uint32_t r, t0, nt;  // block, row in block, first tile, tiles in the item
+};
+__device__ __forceinline__ CrcItem crc_item(uint64_t it, uint32_t nsup, uint32_t nrows, uint32_t tpb) {
+    constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;
+    CrcItem x;
+    uint32_t sup;
+    if (it < (uint64_t(1) << 32)) {  // 32-bit divisions (scalar), the common case
+        const uint32_t i32 = uint32_t(it), rid = i32 / nsup;
+        sup = i32 - rid * nsup;
+        const uint32_t b = rid / nrows;
+        x.b = b;
+        x.r = rid - b * nrows;
+    } else {
+        sup = uint32_t(it % nsup);
+        const uint64_t rid = it / nsup;
+        x.b = rid / nrows;
+        x.r = uint32_t(rid - x.b * nrows);
+    }
+    x.t0 = sup * kSup;
+    x.nt = tpb - x.t0 < kSup ? tpb - x.t0 : kSup;
+    return x;
+}
+// the byte the item's value is relative to: the end of its last group, counted as 8 tiles
+__device__ __forceinline__ uint64_t crc_item_end(const CrcItem& x) {
+    return (uint64_t(x.t0) + (x.nt + kCrcSegTiles - 1) / kCrcSegTiles * kCrcSegTiles) * (kWave * 16);
+}
+
+// LDS staging shared by the rows passes: P4, then G
+#define RSMI_CRC_ROWS_STAGE()                                                                             \
+    __shared__ uint32_t s_tbl[kCrcP4Words + kCrcGWords];                                                  \
+    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_tbl[i] = tbl[kCrcP4Off + i];                   \
+    for (int i = threadIdx.x; i < kCrcGWords; i += kWG) s_tbl[kCrcP4Words + i] = tbl[kCrcGOff + i];       \
+    __syncthreads();                                                                                      \
+    const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_tbl);                                        \
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl + kCrcP4Words); /* G[8][32][16] */
+
 template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
-                                                            uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
+                                                            uint32_t nsup, uint64_t nitems, uint32_t* __restrict__ out,
                                                             uint64_t out_bs) {
-    __shared__ uint32_t s_tbl[kCrcPWords + kCrcNWords];
-    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
-    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + i];
-    __syncthreads();
-    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
-    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sP + kCrcPWords * 2);  // N[32][16]
-
+    RSMI_CRC_ROWS_STAGE()
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
     for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
-        const uint32_t seg = uint32_t(it % nseg);
-        const uint64_t rid = it / nseg;
-        const uint64_t b = rid / nrows;
-        const uint32_t r = uint32_t(rid - b * nrows);
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-        const uint32_t t0 = seg * kCrcSegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
-        u32x4 v[kCrcSegTiles];
-#pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++)
-            if (uint32_t(i) < nt) {
-                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
-                // wave-uniform: only a row's last tile needs the per-lane bounds and masks
-                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-                else
-                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
-            }
+        const CrcItem x = crc_item(it, nsup, nrows, tpb);
+        const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
         uint32_t acc = 0;
+        for (uint32_t g0 = 0; g0 < x.nt; g0 += kCrcSegTiles) {
+            const uint32_t t0 = x.t0 + g0;
+            const uint32_t nt = x.nt - g0 < uint32_t(kCrcSegTiles) ? x.nt - g0 : uint32_t(kCrcSegTiles);
+            u32x4 v[kCrcSegTiles];
 #pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++) {
-            if (uint32_t(i) < nt) {
-                const uint32_t c = crc_nib_chunk(nb, v[i]);
-                acc = crc_pow(sP, 10, acc) ^ c;  // previous tiles move 1 KiB further from the end
-            }
+            for (int i = 0; i < kCrcSegTiles; i++)
+                if (uint32_t(i) < nt) {
+                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
+                    // wave-uniform: only a row's last tile needs the per-lane bounds and masks
+                    if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
+                        v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+                    else
+                        v[i] = crc_chunk_load<ALIGNED>(row, off, S);
+                }
+            uint32_t gs = 0;  // the group's value, relative to the end of its 8th tile
+#pragma unroll
+            for (int i = 0; i < kCrcSegTiles; i++)
+                if (uint32_t(i) < nt) gs ^= crc_nib_chunk(nb + 1024 * i, v[i]);
+            acc = crc_pow4(sQ, 13, acc) ^ gs;  // earlier groups move 8 KiB further from the end
         }
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const uint32_t w = crc_pow(sP, 4 + j, acc);  // 16 * 2^j bytes
-            const uint32_t t = __shfl_up(w, 1u << j);
-            if (lane >= (1u << j)) acc ^= t;
-        }
-        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
-        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
-        if (e < 0) e += kCrcOrder;
-#pragma unroll
-        for (int i = 0; i < kCrcPowers; i++)
-            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
-        if (lane == kWave - 1) atomicXor(out + b * out_bs + r, acc);
+        crc_item_out(sQ, lane, acc, S, crc_item_end(x), out + x.b * out_bs + x.r);
     }
 }
 
 // The nibble rows pass, software-pipelined, for 16-byte-aligned rows (the default).  A wave
-// issues the 8 tile loads of its next item before it folds the current one (two register sets,
-// the loop unrolled by two), so its own fold covers the next item's memory latency instead of
-// only the other waves on the SIMD.  Loads are unconditional -- chunks past the row's end read
-// the row's last chunk and are masked to zero in the fold, and the prefetch past the last item
-// re-reads that item -- so no load sits behind a branch and the compiler's vmcnt waits count
-// only the older set.
+// works in units of half a group (4 tiles) and issues the loads of its next unit (of this item
+// or its next one) before it folds the current one (two register sets of 16 VGPRs, the loop
+// unrolled by two), so its own fold covers the next unit's memory latency instead of only the
+// other waves on the SIMD; half-group units keep the kernel under 64 VGPRs (8 waves per SIMD,
+// with 12 KiB of LDS per workgroup).  Loads are unconditional -- chunks past the row's end read
+// the row's last chunk and are masked to zero in the fold, and the prefetch past the wave's
+// last unit re-reads that unit -- so no load sits behind a branch and the compiler's vmcnt
+// waits count only the older set.
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
-                                                                 uint32_t tpb, uint32_t nseg, uint64_t nitems,
+                                                                 uint32_t tpb, uint32_t nsup, uint64_t nitems,
                                                                  uint32_t* __restrict__ out, uint64_t out_bs) {
-    __shared__ uint32_t s_tbl[kCrcPWords + kCrcNWords];
-    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
-    for (int i = threadIdx.x; i < kCrcNWords; i += kWG) s_tbl[kCrcPWords + i] = tbl[kCrcPWords + i];
-    __syncthreads();
-    const uint16_t* sP = reinterpret_cast<const uint16_t*>(s_tbl);
-    const uint8_t* nb = reinterpret_cast<const uint8_t*>(sP + kCrcPWords * 2);
-
+    RSMI_CRC_ROWS_STAGE()
+    constexpr int kU = kCrcSegTiles / 2;  // tiles per unit
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
     const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
-    auto issue = [&](uint64_t it, u32x4(&v)[kCrcSegTiles]) {
-        const uint32_t seg = uint32_t(it % nseg);
-        const uint64_t rid = it / nseg;
-        const uint64_t b = rid / nrows;
-        const uint32_t r = uint32_t(rid - b * nrows);
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+    // a unit of work: tiles t0 + 4 h .. t0 + 4 h + 3 of item it (its position computed once per item)
+    struct Unit {
+        uint64_t it;
+        CrcItem x;
+        uint32_t h;
+    };
+    auto at = [&](uint64_t it) -> Unit { return Unit{it, crc_item(it, nsup, nrows, tpb), 0}; };
+    auto next = [&](const Unit& u) -> Unit {
+        if ((u.h + 1) * kU < u.x.nt) return Unit{u.it, u.x, u.h + 1};
+        return at(u.it + nw);
+    };
+    auto issue = [&](const Unit& u, u32x4(&v)[kU]) {
+        const uint8_t* row = base + u.x.b * bstride + uint64_t(u.x.r) * rpitch;
 #pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++) {
-            const uint64_t off = (uint64_t(seg * kCrcSegTiles + i) * kWave + lane) * 16;
+        for (int i = 0; i < kU; i++) {
+            const uint64_t off = (uint64_t(u.x.t0 + u.h * kU + i) * kWave + lane) * 16;
             v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
         }
     };
-    auto finish = [&](uint64_t it, u32x4(&v)[kCrcSegTiles]) {
-        const uint32_t seg = uint32_t(it % nseg);
-        const uint64_t rid = it / nseg;
-        const uint64_t b = rid / nrows;
-        const uint32_t r = uint32_t(rid - b * nrows);
-        const uint32_t t0 = seg * kCrcSegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrcSegTiles) ? tpb - t0 : uint32_t(kCrcSegTiles);
-        uint32_t acc = 0;
+    uint32_t acc = 0, gs = 0;
+    auto finish = [&](const Unit& u, u32x4(&v)[kU]) {
+        const CrcItem& x = u.x;
+        const uint32_t u0 = u.h * kU, t0 = x.t0 + u0;
+        const uint32_t nt = x.nt - u0 < uint32_t(kU) ? x.nt - u0 : uint32_t(kU);
+        const uint8_t* gt = nb + 1024 * kU * (u.h & 1);  // table sets of this half of the group
 #pragma unroll
-        for (int i = 0; i < kCrcSegTiles; i++) {
+        for (int i = 0; i < kU; i++) {
             if (uint32_t(i) < nt) {
                 if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
                     const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
@@ -533,35 +581,37 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
                         v[i][w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
                     }
                 }
-                acc = crc_pow(sP, 10, acc) ^ crc_nib_chunk(nb, v[i]);  // earlier tiles move 1 KiB
+                gs ^= crc_nib_chunk(gt + 1024 * i, v[i]);
             }
         }
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            const uint32_t w = crc_pow(sP, 4 + j, acc);  // 16 * 2^j bytes
-            const uint32_t t = __shfl_up(w, 1u << j);
-            if (lane >= (1u << j)) acc ^= t;
+        const bool item_end = u0 + kU >= x.nt;
+        if ((u.h & 1) || item_end) {  // the group is complete
+            acc = crc_pow4(sQ, 13, acc) ^ gs;  // earlier groups move 8 KiB further from the end
+            gs = 0;
         }
-        const int64_t seg_end = int64_t(t0 + nt) * (kWave * 16);
-        int64_t e = (int64_t(S) - seg_end) % int64_t(kCrcOrder);
-        if (e < 0) e += kCrcOrder;
-#pragma unroll
-        for (int i = 0; i < kCrcPowers; i++)
-            if ((e >> i) & 1) acc = crc_pow(sP, i, acc);
-        if (lane == kWave - 1) atomicXor(out + b * out_bs + r, acc);
+        if (item_end) {
+            crc_item_out(sQ, lane, acc, S, crc_item_end(x), out + x.b * out_bs + x.r);
+            acc = 0;
+        }
     };
     const uint64_t it0 = uint64_t(blockIdx.x) * (kWG / kWave) + wid;
     if (it0 >= nitems) return;
-    const uint64_t itmax = nitems - 1;
-    u32x4 va[kCrcSegTiles], vb[kCrcSegTiles];
-    issue(it0, va);
-    for (uint64_t it = it0;; it += 2 * nw) {
-        issue(it + nw < itmax ? it + nw : itmax, vb);
-        finish(it, va);
-        if (it + nw > itmax) break;
-        issue(it + 2 * nw < itmax ? it + 2 * nw : itmax, va);
-        finish(it + nw, vb);
-        if (it + 2 * nw > itmax) break;
+    Unit cur = at(it0);
+    u32x4 va[kU], vb[kU];
+    issue(cur, va);
+    for (;;) {
+        Unit nx = next(cur);
+        bool more = nx.it < nitems;
+        issue(more ? nx : cur, vb);
+        finish(cur, va);
+        if (!more) break;
+        cur = nx;
+        nx = next(cur);
+        more = nx.it < nitems;
+        issue(more ? nx : cur, va);
+        finish(cur, vb);
+        if (!more) break;
+        cur = nx;
     }
 }
 

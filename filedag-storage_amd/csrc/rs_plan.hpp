@@ -39,12 +39,17 @@ void* repitch_kernel();
 // A^(2^i), byte-sliced) and N[32][16] (u16); a wave folds kCrcSegTiles 1 KiB tiles of one row
 // with one N lookup per nibble (16-entry tables: each wave-wide lookup touches 8 distinct
 // banks, so it never conflicts).
-constexpr int kCrcSegTiles = 8;
+constexpr int kCrcSegTiles = 8;   // tiles a wave loads at once (one group)
+constexpr int kCrcSupGroups = 4;  // groups per item: the scan and the end shift run once per 32 tiles
 constexpr int kCrcPWords = 15 * 2 * 256 / 2;
 constexpr int kCrcNWords = 32 * 16 / 2;
 constexpr int kCrcQWords = 16 * 2 * 4 * 16 / 2;  // quad-relative nibble tables (fused kernels)
 constexpr int kCrcQOff = kCrcPWords + kCrcNWords;
-constexpr int kCrcTableWords = kCrcQOff + kCrcQWords;
+constexpr int kCrcGWords = 8 * 32 * 16 / 2;     // tile-set nibble tables (rows pass)
+constexpr int kCrcGOff = kCrcQOff + kCrcQWords;
+constexpr int kCrcP4Words = 15 * 4 * 16 / 2;     // nibble-sliced powers (rows pass)
+constexpr int kCrcP4Off = kCrcGOff + kCrcGWords;
+constexpr int kCrcTableWords = kCrcP4Off + kCrcP4Words;
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;

@@ -14,11 +14,13 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) + sizeof(t.G) + sizeof(t.P4) == size_t(kCrcTableWords) * 4, "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
     std::memcpy(h.data(), t.P, sizeof(t.P));
     std::memcpy(h.data() + kCrcPWords * 2, t.N, sizeof(t.N));
     std::memcpy(h.data() + kCrcQOff * 2, t.Q, sizeof(t.Q));
+    std::memcpy(h.data() + kCrcGOff * 2, t.G, sizeof(t.G));
+    std::memcpy(h.data() + kCrcP4Off * 2, t.P4, sizeof(t.P4));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -36,17 +38,18 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     void* fn = crc16_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16;
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
-    uint32_t nseg = (tpb + kCrcSegTiles - 1) / kCrcSegTiles;
-    uint64_t nitems = nblocks * nrows * nseg;
-    // 96 waves per CU: several dispatch rounds, so the hardware balances CUs, while each
-    // workgroup still amortizes its LDS table staging over ~6 items per wave (+3 % over
-    // occupancy x CUs, -25 % at one item per wave).  The pipelined pass (aligned rows) keeps
-    // its next item's loads in flight itself and does best at 48
-    uint64_t cap = uint64_t(c->num_cu) * (aligned ? 48 : 96) / 4;
+    constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;
+    uint32_t nsup = (tpb + kSup - 1) / kSup;
+    uint64_t nitems = nblocks * nrows * nsup;
+    // 96 waves per CU: several dispatch rounds, so the hardware balances CUs (items differ in
+    // length at a row's end), while each workgroup still amortizes its LDS table staging over
+    // a few items per wave.  Level with 48 and 64 at 26 KB rows, +10 % at 256 KB rows
+    // (profiles/r02/crc/crc_rows_grid.txt).
+    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
-    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs};
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nsup, &nitems, &out, &out_bs};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
     return RSMI_OK;
 }
