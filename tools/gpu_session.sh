@@ -24,6 +24,10 @@ if [[ $STEP == all || $STEP == side ]]; then
     timeout -k 10 300 python bench.py $args --cpu-seconds 0 > $f 2> $f.err || { echo "bench $args failed"; tail -30 $f.err; exit 1; }
     cat $f
   done
+  timeout -k 10 300 python bench.py --config rs16_4_4m --copy-inclusive --group 0,0 --cpu-seconds 0 > gpurun_out/side_group.json 2> gpurun_out/side_group.err || { echo "bench --group failed"; tail -30 gpurun_out/side_group.err; exit 1; }
+  cat gpurun_out/side_group.json
+  timeout -k 10 300 python tools/crcbench.py > gpurun_out/crcbench.txt 2>&1 || { echo "crcbench failed"; tail -30 gpurun_out/crcbench.txt; exit 1; }
+  cat gpurun_out/crcbench.txt
   timeout -k 10 300 python bench.py --gpus 2 --share-device --cpu-seconds 0 > gpurun_out/side_gpus2.json 2> gpurun_out/side_gpus2.err || { echo "bench --gpus 2 failed"; tail -30 gpurun_out/side_gpus2.err; exit 1; }
   cat gpurun_out/side_gpus2.json
 fi
