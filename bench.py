@@ -130,12 +130,31 @@ def launch(a):
     return rc
 
 
+_JSON_OUT = None  # multi-rank: the real stdout, kept for the one JSON line
+
+
+def emit(line):
+    """The run's JSON line, alone on stdout."""
+    if _JSON_OUT is not None:
+        _JSON_OUT.write(line + "\n")
+        _JSON_OUT.flush()
+    else:
+        print(line, flush=True)
+
+
 def dist_setup():
+    global _JSON_OUT
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+
+        # gloo and the runtime print connection chatter on fd 1; send everything but the JSON
+        # line to stderr, so stdout carries exactly one line under any launcher
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -433,11 +452,11 @@ def run_mock(a, world, rank):
     el = max_over_ranks(time.perf_counter() - t0, world)
     per = gather({"rank": rank, "blocks": count}, world)
     if rank == 0:
-        print(json.dumps({"metric": "mock", "mock": True, "value": round(nb * world * k * S * a.steps / el / 2**30, 4),
+        emit(json.dumps({"metric": "mock", "mock": True, "value": round(nb * world * k * S * a.steps / el / 2**30, 4),
                           "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(el * 1e3 / a.steps, 4), "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "u8", "data": "mock (CPU stand-in, orchestration test only)",
-                          "config": {"ranks": per}}), flush=True)
+                          "config": {"ranks": per}}))
 
 
 def main():
@@ -625,7 +644,7 @@ def main():
         data_host = lay.rows(buf, 0, k).cpu().numpy()  # the bench's own blocks
         out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(json.dumps(out))
     codec.close()
     if world > 1:
         import torch.distributed as dist

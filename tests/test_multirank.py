@@ -74,8 +74,8 @@ def test_bench_spawns_ranks_itself_mock():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mock", "--steps", "3"],
                          capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout holds the JSON line only
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["mock"] and j["steps"] == 3
     assert sorted(r["rank"] for r in j["config"]["ranks"]) == [0, 1]
@@ -116,8 +116,8 @@ def test_bench_gpus2_share_device_no_launcher():
            "--blocks", "256", "--settle-ms", "0", "--sustained-steps", "0", "--share-device"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout holds the JSON line only
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["verify"]["verified"] and j["verify"]["ranks_verified"] == 2
     payload = 2 * 256 * 262144 * 5
@@ -139,8 +139,8 @@ def test_bench_two_ranks_torchrun_on_one_gpu():
            "--sustained-steps", "0", "--share-device"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout holds the JSON line only
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["steps"] == 5 and j["scaling"] == "weak"
     payload = 2 * 256 * 262144 * 5
