@@ -23,6 +23,7 @@ constexpr int kCrc32InvPowers = 14;  // A^-(2^i): backward shifts up to 8192 byt
 constexpr int kCrc32SegTiles = 8;    // device segment: 8 tiles of 1 KiB (rs_crc32_rows_kernel)
 constexpr int kCrc32ScanPowers = 6;  // A^(16 * 2^j), j < 6: the 64-lane scan of a tile
 constexpr int kCrc32SegPowers = 19;  // A^(8192 * 2^i), i < 19: whole-segment shifts
+constexpr int kCrc32SupGroups = 4;   // 8-tile groups per device item (scan and end shift once per item)
 
 struct Crc32Tables {
     uint32_t T[256];                          // reflected 0xEDB88320
@@ -35,6 +36,7 @@ struct Crc32Tables {
     // SC[i][b] = A^(8192 * 2^i)(1 << b), column-form segment powers, and SC[19] = A^-8192
     uint32_t NT[kCrc32SegTiles][32][16];
     uint32_t SN[kCrc32ScanPowers][8][16];
+    uint32_t SG[8][16];  // A^8192 nibble-sliced: the step between an item's 8-tile groups
     uint32_t SC[kCrc32SegPowers + 1][32];
     Crc32Tables();
     static uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {

@@ -2,8 +2,8 @@
 // kv/mutcask/cask.go:73-97; algebra in crc32.hpp), the CRC-32 sibling of
 // rs_crc16_rows_kernel (rs_kernels.hip).
 //
-// Work item = (row, segment of kCrc32SegTiles = 8 consecutive 1 KiB tiles).  Each lane loads
-// its 16-byte chunk of every tile of the segment (all loads in flight first) and folds each
+// Work item = (row, up to kCrc32SupGroups segments of kCrc32SegTiles = 8 consecutive 1 KiB
+// tiles).  Each lane loads its 16-byte chunk of every tile of a segment and folds each
 // chunk with 32 nibble lookups into 16-entry u32 tables (a wave-wide lookup into one table
 // touches at most 16 dwords in 16 distinct banks, so it never conflicts).  Tile t of the
 // segment has its own tables (NT[t] = A^(1024 * (7 - t)) o N), so every chunk's value comes
@@ -68,19 +68,24 @@ __device__ __forceinline__ uint32_t apply_lanes(uint32_t col, uint32_t s, uint32
 
 }  // namespace
 
-// tbl: NT[8][32][16] | SN[6][8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).  (A software-
-// pipelined loop like rs_crc16_rows_pipe_kernel's measured level with this one, -3% to +5%.)
+// tbl: NT[8][32][16] | SN[6][8][16] | SG[8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).
+// An item is up to kCrc32SupGroups 8-tile groups of one row: each group folds through the
+// tile-set tables into a value relative to its end, a running register steps by A^8192 (SG)
+// between groups, and the scan and the end shift run once per item (the CRC-16 pass's
+// round-2 structure; 8-tile items spent a quarter of the pass there).  (A software-pipelined
+// loop measured level with the plain one in round 1, -3% to +5%.)
 template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
-                                                            uint32_t nseg, uint64_t nitems, uint32_t* __restrict__ out,
-                                                            uint64_t out_bs, Crc32Shift sh) {
+                                                            uint32_t nseg, uint32_t nsup, uint64_t nitems,
+                                                            uint32_t* __restrict__ out, uint64_t out_bs, Crc32Shift sh) {
     __shared__ uint32_t s_tbl[kCrc32LdsWords];
     for (int i = threadIdx.x; i < kCrc32LdsWords; i += kWG) s_tbl[i] = tbl[i];
     __syncthreads();
     const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl);
     const uint32_t* sS = s_tbl + kCrc32FoldWords;
+    const uint32_t* sG = sS + kCrc32ScanPowers * kCrc32PowWords;
     const uint32_t* sC = tbl + kCrc32LdsWords;
     const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024)), r8 = uint32_t(S % (kCrc32SegTiles * 1024));
     const uint32_t l32 = threadIdx.x & 31;
@@ -90,39 +95,61 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    auto row_of = [&](uint64_t it, uint32_t& seg, uint64_t& b, uint32_t& r) {
-        seg = uint32_t(it % nseg);
-        const uint64_t rid = it / nseg;
-        b = rid / nrows;
-        r = uint32_t(rid - b * nrows);
-    };
-    // fold, scan, shift to the row's end, atomic XOR
-    auto finish = [&](uint64_t it, u32x4(&v)[kCrc32SegTiles]) {
-        uint32_t seg, r;
+    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
+        uint32_t sup, r;
         uint64_t b;
-        row_of(it, seg, b, r);
-        const uint32_t t0 = seg * kCrc32SegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
+        if (it < (uint64_t(1) << 32)) {  // 32-bit divisions (scalar), the common case
+            const uint32_t i32 = uint32_t(it), rid = i32 / nsup;
+            sup = i32 - rid * nsup;
+            const uint32_t b32 = rid / nrows;
+            b = b32;
+            r = rid - b32 * nrows;
+        } else {
+            sup = uint32_t(it % nsup);
+            const uint64_t rid = it / nsup;
+            b = rid / nrows;
+            r = uint32_t(rid - b * nrows);
+        }
+        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
+        const uint32_t g0 = sup * kCrc32SupGroups;
+        const uint32_t g1 = nseg - g0 < uint32_t(kCrc32SupGroups) ? nseg : g0 + kCrc32SupGroups;  // past the last
         uint32_t acc = 0;
+        for (uint32_t g = g0; g < g1; g++) {
+            const uint32_t t0 = g * kCrc32SegTiles;
+            const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
+            u32x4 v[kCrc32SegTiles];
 #pragma unroll
-        for (int i = 0; i < kCrc32SegTiles; i++) {
-            if (uint32_t(i) < nt) {
+            for (int i = 0; i < kCrc32SegTiles; i++)
+                if (uint32_t(i) < nt) {
+                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
+                    // wave-uniform: only a row's last tile needs the per-lane bounds and masks
+                    if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
+                        v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
+                    else
+                        v[i] = crc_chunk_load<ALIGNED>(row, off, S);
+                }
+            uint32_t gs = 0;  // the group's value, relative to the end of its 8-tile span
 #pragma unroll
-                for (int w = 0; w < 4; w++) {
-                    // byte offsets 4 x nibble into the 16-entry u32 tables (64 B each)
-                    uint32_t lo = (v[i][w] << 2) & 0x3C3C3C3Cu, hi = (v[i][w] >> 2) & 0x3C3C3C3Cu;
-                    asm volatile("" : "+v"(lo), "+v"(hi));  // keep the two masks (one extract per offset)
-                    uint32_t l[8];
+            for (int i = 0; i < kCrc32SegTiles; i++) {
+                if (uint32_t(i) < nt) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int p = 4 * w + q;
-                        const int o = 2048 * i + 128 * p;
-                        l[2 * q] = *reinterpret_cast<const uint32_t*>(nb + o + ((lo >> (8 * q)) & 0xFF));
-                        l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(nb + o + 64 + ((hi >> (8 * q)) & 0xFF));
+                    for (int w = 0; w < 4; w++) {
+                        // byte offsets 4 x nibble into the 16-entry u32 tables (64 B each)
+                        uint32_t lo = (v[i][w] << 2) & 0x3C3C3C3Cu, hi = (v[i][w] >> 2) & 0x3C3C3C3Cu;
+                        asm volatile("" : "+v"(lo), "+v"(hi));  // keep the two masks (one extract per offset)
+                        uint32_t l[8];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int p = 4 * w + q;
+                            const int o = 2048 * i + 128 * p;
+                            l[2 * q] = *reinterpret_cast<const uint32_t*>(nb + o + ((lo >> (8 * q)) & 0xFF));
+                            l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(nb + o + 64 + ((hi >> (8 * q)) & 0xFF));
+                        }
+                        gs = xor3(gs, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
                     }
-                    acc = xor3(acc, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
                 }
             }
+            acc = (g == g0 ? 0u : pow_nib(sG, acc)) ^ gs;  // earlier groups move 8 KiB further
         }
 #pragma unroll
         for (int j = 0; j < kCrc32ScanPowers; j++) {
@@ -130,11 +157,12 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
             const uint32_t t = __shfl_up(w, 1u << j);
             if (lane >= (1u << j)) acc ^= t;
         }
-        // lane 63's value, wave-uniform from here on
+        // lane 63's value, relative to the end of group g1 - 1, wave-uniform from here on
         uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));
-        if (seg + 1 < nseg) {
+        const uint32_t gl = g1 - 1;
+        if (gl + 1 < nseg) {
             // whole segments, then the remainder r
-            uint32_t a = q8 - seg - 1;
+            uint32_t a = q8 - gl - 1;
             for (int i = 0; a; i++, a >>= 1)
                 if (a & 1) val = apply_lanes(sC[32 * i + l32], val, l32);
             val = apply_lanes(col_r, val, l32);
@@ -142,27 +170,6 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
             val = apply_lanes(col_r, apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32), l32);
         }
         if (lane == 0) atomicXor(out + b * out_bs + r, val);
-    };
-    const uint64_t it0 = uint64_t(blockIdx.x) * (kWG / kWave) + wid;
-    for (uint64_t it = it0; it < nitems; it += nw) {
-        uint32_t seg, r;
-        uint64_t b;
-        row_of(it, seg, b, r);
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-        const uint32_t t0 = seg * kCrc32SegTiles;
-        const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
-        u32x4 v[kCrc32SegTiles];
-#pragma unroll
-        for (int i = 0; i < kCrc32SegTiles; i++)
-            if (uint32_t(i) < nt) {
-                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
-                // wave-uniform: only a row's last tile needs the per-lane bounds and masks
-                if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-                else
-                    v[i] = crc_chunk_load<ALIGNED>(row, off, S);
-            }
-        finish(it, v);
     }
 }
 

@@ -54,7 +54,7 @@ constexpr int kCrcTableWords = kCrcP4Off + kCrcP4Words;
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
 constexpr int kCrc32PowWords = 8 * 16;  // one nibble-sliced power
-constexpr int kCrc32LdsWords = kCrc32FoldWords + 6 * kCrc32PowWords;
+constexpr int kCrc32LdsWords = kCrc32FoldWords + 7 * kCrc32PowWords;  // NT | SN[6] | SG
 constexpr int kCrc32TableWords = kCrc32LdsWords + 20 * 32;
 // per-launch shift to the row's end, column form (crc32.hpp), passed by value: A^(S mod 8192),
 // the end of an inner segment moved over whatever of the row follows whole segments

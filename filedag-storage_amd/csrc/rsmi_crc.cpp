@@ -58,10 +58,12 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 int ensure_crc32_tables(rsmi_ctx* c) {
     if (c->d_crc32_tbl) return RSMI_OK;
     const Crc32Tables& t = crc32_tables();
-    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SC) == size_t(kCrc32TableWords) * 4, "CRC-32 table layout");
+    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SG) + sizeof(t.SC) == size_t(kCrc32TableWords) * 4,
+                  "CRC-32 table layout");
     std::vector<uint32_t> h(static_cast<size_t>(kCrc32TableWords));
     std::memcpy(h.data(), t.NT, sizeof(t.NT));
     std::memcpy(h.data() + kCrc32FoldWords, t.SN, sizeof(t.SN));
+    std::memcpy(h.data() + kCrc32FoldWords + 6 * kCrc32PowWords, t.SG, sizeof(t.SG));
     std::memcpy(h.data() + kCrc32LdsWords, t.SC, sizeof(t.SC));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc32_tbl), h.size() * 4));
     HIP_TRY(hipMemcpy(c->d_crc32_tbl, h.data(), h.size() * 4, hipMemcpyHostToDevice));
@@ -82,19 +84,20 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     if (S / span >= (uint64_t(1) << kCrc32SegPowers)) return RSMI_ERR_INVALID_ARG;  // rows below 4 GiB
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrc32SegTiles - 1) / kCrc32SegTiles;
+    uint32_t nsup = (nseg + kCrc32SupGroups - 1) / kCrc32SupGroups;
     // the per-launch shift to the row's end (crc32.hpp), cached for the last S
     if (c->crc32_shift_S != S) {
         crc32_tables().shift_columns(S % span, c->crc32_shift.col);
         c->crc32_shift_S = S;
     }
     Crc32Shift sh = c->crc32_shift;
-    uint64_t nitems = nblocks * nrows * nseg;
-    // 96 waves per CU as for the plain CRC-16 pass
+    uint64_t nitems = nblocks * nrows * nsup;
+    // 96 waves per CU as for the CRC-16 pass
     uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc32_tbl;
-    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nitems, &out, &out_bs, &sh};
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nsup, &nitems, &out, &out_bs, &sh};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
     return RSMI_OK;
 }
