@@ -89,12 +89,14 @@ def _device_rows(nb, nrows, S, pitch, offset, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1024, 1025, 8191, 8192, 8193, 26215, 104858, 262144])
+@pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1024, 1025, 4095, 4097, 8191, 8192, 8193, 26215, 32767, 32768,
+                               32769, 36865, 65536, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 @pytest.mark.parametrize("wpc", [0, 1])
 def test_rows_dev_matches_oracle(S, layout, wpc):
     """Aligned rows take the pipelined pass, others the plain one; waves_per_cu=1 makes each
-    wave walk many items (the pipelined pass's two register sets alternate)."""
+    wave walk many items (the pipelined pass's two register sets alternate).  Row sizes cover
+    half-group, group (8 KiB) and item (32 KiB) boundaries on both sides."""
     import torch
 
     nrows, nb = 3, 5
@@ -302,8 +304,8 @@ def test_coalesced_reconstruct_concurrent_callers():
                                              (2, 1, 16, 9, "split"), (5, 3, 1000, 7, "pitched"),
                                              (6, 6, 5000, 4, "split"), (12, 4, 1, 5, "pitched"),
                                              (1, 1, 33, 5, "split"), (8, 4, 65535, 3, "padded")])
-@pytest.mark.parametrize("wpc", [0, 1])
-def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, wpc):
+@pytest.mark.parametrize("opt", [("waves_per_cu", 0), ("waves_per_cu", 1)])
+def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opt):
     """Device-resident encode with the CRC fused into the encode pass: parity and every row's
     R(row) equal the oracle's (k > 16, m > 4, and S < 16 in unaligned layouts take the separate
     CRC pass).  Row padding in pitched layouts holds garbage, which must not reach the CRC.
@@ -319,7 +321,7 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, wpc):
     raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
     base = d.data_ptr()
     with rsmi.Codec(k, m) as c:
-        c.set_option("waves_per_cu", wpc)
+        c.set_option(*opt)
         c.encode_batch_dev_crc(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, raw.data_ptr(),
                                torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()

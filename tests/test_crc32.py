@@ -65,7 +65,8 @@ def test_oracle_mutcask_entry_crc_is_checksum_of_framed_entry():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1023, 1024, 1025, 8191, 8192, 8193, 16384, 24577, 26215, 73729, 104858, 262144, 1048579])
+@pytest.mark.parametrize("S", [1, 7, 15, 16, 17, 1000, 1023, 1024, 1025, 8191, 8192, 8193, 16384, 24577, 26215, 32767,
+                               32768, 32769, 40961, 65536, 73729, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 @pytest.mark.parametrize("wpc", [0, 1])
 def test_rows_dev_matches_zlib(S, layout, wpc):

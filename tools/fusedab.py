@@ -32,6 +32,9 @@ def main():
     st = torch.cuda.current_stream()
     sh = st.cuda_stream
     c = rsmi.Codec(k, m)
+    for kv in filter(None, os.environ.get("FUSED_OPT", "").split(",")):  # e.g. crc_parts=4
+        key, val = kv.split("=")
+        c.set_option(key, int(val))
     raw = torch.empty((nb, n), dtype=torch.int32, device="cuda")
     res = []
     for lay, rs in (("pitched", rsmi.recommended_pitch(S)), ("split", S)):
@@ -47,7 +50,8 @@ def main():
         te, tf = med(enc, st), med(fz, st)
         res.append(f"{lay}: encode {te:.1f} us, fused {tf:.1f} us ({tf / te:.2f}x)")
         del buf
-    print(os.path.basename(os.path.dirname(os.path.dirname(rsmi.LIB_PATH))) + ": " + "; ".join(res), flush=True)
+    tag = os.path.basename(os.path.dirname(os.path.dirname(rsmi.LIB_PATH))) + " " + os.environ.get("FUSED_OPT", "")
+    print(tag + ": " + "; ".join(res), flush=True)
 
 
 if __name__ == "__main__":
