@@ -431,21 +431,37 @@ __device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4
     return c;
 }
 
+// M(s) for a 16x16 matrix held lane-distributed (lane l < 16 of every 16-lane row holds M's
+// image of 1 << l) and a wave-uniform s: each lane keeps its column if bit l of s is set, and an
+// XOR scan over the 16-lane row (DPP row_shr 1, 2, 4, 8) leaves the image in lane 15.  No LDS.
+__device__ __forceinline__ uint32_t crc_apply_cols(uint32_t col, uint32_t s, uint32_t l16) {
+    uint32_t x = ((s >> l16) & 1u) ? col : 0u;
+    x ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, false));  // row_shr:1
+    x ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, false));  // row_shr:2
+    x ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, false));  // row_shr:4
+    x ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, false));  // row_shr:8
+    return uint32_t(__builtin_amdgcn_readlane(int(x), 15));
+}
+
 // The item's value -> row word: lane scan, shift to the row's end, one atomic XOR (lane 63).
-__device__ __forceinline__ void crc_item_out(const uint16_t* sQ, uint32_t lane, uint32_t acc, uint64_t S,
-                                             uint64_t item_end, uint32_t* word) {
+// The shift is A^d (d = the bytes between the item's end and the last item's end, mod 32767:
+// a few power steps, none for the row's last item) and then the launch's A^E (E = S - the last
+// item's end) in column form.
+__device__ __forceinline__ void crc_item_out(const uint16_t* sQ, uint32_t lane, uint32_t acc, uint64_t item_end,
+                                             uint64_t last_end, uint32_t col_e, uint32_t* word) {
 #pragma unroll
     for (int j = 0; j < 6; j++) {
         const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
         const uint32_t t = __shfl_up(w, 1u << j);
         if (lane >= (1u << j)) acc ^= t;
     }
-    int64_t e = (int64_t(S) - int64_t(item_end)) % int64_t(kCrcOrder);
-    if (e < 0) e += kCrcOrder;
+    uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // wave-uniform from here
+    const uint32_t d = uint32_t((last_end - item_end) % kCrcOrder);
 #pragma unroll
     for (int i = 0; i < kCrcPowers; i++)
-        if ((e >> i) & 1) acc = crc_pow4(sQ, i, acc);
-    if (lane == kWave - 1) atomicXor(word, acc);
+        if ((d >> i) & 1) val = crc_pow4(sQ, i, val);
+    val = crc_apply_cols(col_e, val, lane & 15u);
+    if (lane == kWave - 1) atomicXor(word, val);
 }
 
 // Position of item `it` (nsup items per row): its row and first tile.
@@ -485,14 +501,17 @@ __device__ __forceinline__ uint64_t crc_item_end(const CrcItem& x) {
     for (int i = threadIdx.x; i < kCrcGWords; i += kWG) s_tbl[kCrcP4Words + i] = tbl[kCrcGOff + i];       \
     __syncthreads();                                                                                      \
     const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_tbl);                                        \
-    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl + kCrcP4Words); /* G[8][32][16] */
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl + kCrcP4Words); /* G[8][32][16] */  \
+    uint32_t col_e = 0; /* A^E, lane-distributed */                                                    \
+    _Pragma("unroll") for (int b_ = 0; b_ < 16; b_++) col_e = (threadIdx.x & 15u) == uint32_t(b_) ? sh.col[b_] : col_e; \
+    const uint64_t last_end = (uint64_t(tpb) + kCrcSegTiles - 1) / kCrcSegTiles * kCrcSegTiles * (kWave * 16);
 
 template <bool ALIGNED>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __restrict__ tbl,
                                                             const uint8_t* __restrict__ base, uint64_t bstride,
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nsup, uint64_t nitems, uint32_t* __restrict__ out,
-                                                            uint64_t out_bs) {
+                                                            uint64_t out_bs, Crc16Shift sh) {
     RSMI_CRC_ROWS_STAGE()
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_kernel(const uint32_t* __re
                 if (uint32_t(i) < nt) gs ^= crc_nib_chunk(nb + 1024 * i, v[i]);
             acc = crc_pow4(sQ, 13, acc) ^ gs;  // earlier groups move 8 KiB further from the end
         }
-        crc_item_out(sQ, lane, acc, S, crc_item_end(x), out + x.b * out_bs + x.r);
+        crc_item_out(sQ, lane, acc, crc_item_end(x), last_end, col_e, out + x.b * out_bs + x.r);
     }
 }
 
@@ -538,7 +557,8 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
                                                                  uint32_t tpb, uint32_t nsup, uint64_t nitems,
-                                                                 uint32_t* __restrict__ out, uint64_t out_bs) {
+                                                                 uint32_t* __restrict__ out, uint64_t out_bs,
+                                                                 Crc16Shift sh) {
     RSMI_CRC_ROWS_STAGE()
     constexpr int kU = kCrcSegTiles / 2;  // tiles per unit
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -590,7 +610,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
             gs = 0;
         }
         if (item_end) {
-            crc_item_out(sQ, lane, acc, S, crc_item_end(x), out + x.b * out_bs + x.r);
+            crc_item_out(sQ, lane, acc, crc_item_end(x), last_end, col_e, out + x.b * out_bs + x.r);
             acc = 0;
         }
     };

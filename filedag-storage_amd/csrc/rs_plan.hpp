@@ -61,6 +61,11 @@ constexpr int kCrc32TableWords = kCrc32LdsWords + 20 * 32;
 struct Crc32Shift {
     uint32_t col[32];
 };
+// the CRC-16 rows pass's per-launch shift, column form: A^E with E = (S - end of the row's last
+// item) mod 32767, col[b] = A^E(1 << b)
+struct Crc16Shift {
+    uint32_t col[16];
+};
 void* crc16_rows_kernel(bool aligned);
 void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
 void* crc32_rows_kernel(bool aligned);

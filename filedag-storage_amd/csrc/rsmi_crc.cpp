@@ -41,6 +41,11 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;
     uint32_t nsup = (tpb + kSup - 1) / kSup;
     uint64_t nitems = nblocks * nrows * nsup;
+    // A^E, E = S - (end of the last item, counted in whole 8-tile groups), mod 32767
+    const uint64_t last_end = (uint64_t(tpb) + kCrcSegTiles - 1) / kCrcSegTiles * kCrcSegTiles * tile;
+    const int64_t E = ((int64_t(S) - int64_t(last_end)) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder;
+    Crc16Shift sh;
+    for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), uint64_t(E));
     // 96 waves per CU: several dispatch rounds, so the hardware balances CUs (items differ in
     // length at a row's end), while each workgroup still amortizes its LDS table staging over
     // a few items per wave.  Level with 48 and 64 at 26 KB rows, +10 % at 256 KB rows
@@ -49,7 +54,7 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
     const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
     const uint32_t* tb = c->d_crc_tbl;
-    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nsup, &nitems, &out, &out_bs};
+    void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nsup, &nitems, &out, &out_bs, &sh};
     HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
     return RSMI_OK;
 }
