@@ -537,6 +537,17 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
 }
 
 Status DagNode::Get(const std::string& key, Bytes* block) {
+    if (gpu_verified_reads_) {
+        // one key through GetMany's path (which holds the Active guard, so a lone caller keeps
+        // its node fan-out): the shards are fetched unchecked, and a degraded read's survivors
+        // are checked by the decode kernel itself (one GPU call, not one per fetch wave plus the
+        // decode); quorum, repair list and errors are Get's (see GetMany)
+        std::vector<Bytes> blocks;
+        std::vector<Status> st;
+        GetMany({key}, &blocks, &st, 1);
+        if (st[0].ok()) *block = std::move(blocks[0]);
+        return st[0];
+    }
     Active act(active_);
     Fetched f;
     Status s = fetch_for_get(key, &f);
