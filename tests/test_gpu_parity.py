@@ -41,7 +41,8 @@ def test_encode_matrix_matches_oracle():
 
 @pytest.mark.parametrize("k,m", CONFIGS)
 def test_encode_block_grid(k, m):
-    sizes = sorted({1, max(1, k - 1), k, k + 1, 6, 4095, 65537, 262143, 262144, 262145})
+    # SURVEY.md 8(d)'s correctness grid, with the dag-pb leaf (1 MiB + 14) and 4 MiB blocks
+    sizes = sorted({1, max(1, k - 1), k, k + 1, 6, 4095, 65537, 262143, 262144, 262145, 1048576 + 14, 4 << 20})
     with rsmi.Codec(k, m) as c:
         for B in sizes:
             block = _rng_bytes(B, B).tobytes()
