@@ -90,7 +90,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     // the 8 XCDs) takes one contiguous eighth of the tiles.  A row's 1 KiB tile at an odd address
     // shares its first and last 64-byte lines with the neighbouring tiles; with the neighbours on
     // the same XCD those lines come from one L2 (Split layout: encode +4-5%).
-    // Aligned layouts share no lines and keep the plain order (round 1: -1.5 to +1.1%).
+    // Aligned layouts share no lines and keep the plain order (re-measured in round 2: +1.2% on
+    // RS(10,4) 256 KiB, -1.3 to -3% on the other BASELINE shapes, profiles/r02/cfg_ab_xcd.txt).
     uint32_t wg = blockIdx.x;
     if (UA && (gridDim.x & 7u) == 0u) wg = (wg & 7u) * (gridDim.x >> 3) + (wg >> 3);
     uint32_t t = wg * kWavesPerWG + wid;
