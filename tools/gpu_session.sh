@@ -38,5 +38,6 @@ if [[ $STEP == all || $STEP == prof ]]; then
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_fetch.log" 2>&1) || { echo "pmc fetch failed"; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_write.log" 2>&1) || { echo "pmc write failed"; tail -20 gpurun_out/pmc_write.log; exit 1; }
   python tools/pmc_summary.py gpurun_out/pmc_fetch/pmc_counter_collection.csv gpurun_out/pmc_write/pmc_counter_collection.csv gpurun_out/pmc_traffic.json
+  bash tools/pmc_layouts.sh || { echo "pmc layouts failed"; exit 1; }
 fi
 done

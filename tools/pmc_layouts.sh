@@ -11,3 +11,12 @@ for mode in split fused; do
   done
   python3 tools/pmc_summary.py gpurun_out/pmc_${mode}_FETCH_SIZE/pmc_counter_collection.csv gpurun_out/pmc_${mode}_WRITE_SIZE/pmc_counter_collection.csv gpurun_out/pmc_traffic_${mode}.json
 done
+# fold the UA kernels' figures into the bench's table (bench.py reads profiles/pmc_traffic.json
+# by kernel label; the fused line's label names two kernels and stays without one)
+python3 - <<'PY'
+import json, os
+path = "gpurun_out/pmc_traffic.json"
+table = json.load(open(path)) if os.path.exists(path) else {}
+table.update({k: v for k, v in json.load(open("gpurun_out/pmc_traffic_split.json")).items() if ",UA" in k})
+json.dump(table, open(path, "w"), indent=1)
+PY
