@@ -66,7 +66,93 @@ __device__ __forceinline__ uint32_t apply_lanes(uint32_t col, uint32_t s, uint32
     return uint32_t(__builtin_amdgcn_readlane(int(x), 15)) ^ uint32_t(__builtin_amdgcn_readlane(int(x), 31));
 }
 
+// R(chunk) relative to the end of its table set's span: 32 nibble lookups into the 16-entry
+// u32 tables t[32][16] (64 B each; byte offsets 4 x nibble)
+__device__ __forceinline__ uint32_t crc32_nib_chunk(const uint8_t* t, const u32x4& v) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint32_t lo = (v[w] << 2) & 0x3C3C3C3Cu, hi = (v[w] >> 2) & 0x3C3C3C3Cu;
+        asm volatile("" : "+v"(lo), "+v"(hi));  // keep the two masks (one extract per offset)
+        uint32_t l[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int p = 4 * w + q;
+            l[2 * q] = *reinterpret_cast<const uint32_t*>(t + 128 * p + ((lo >> (8 * q)) & 0xFF));
+            l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(t + 128 * p + 64 + ((hi >> (8 * q)) & 0xFF));
+        }
+        c = xor3(c, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
+    }
+    return c;
+}
+
+// The item's value -> row word: lane scan (lane 63 ends with the value relative to the end of
+// group gl), the shift to the row's end, one atomic XOR.  With S = 8192 q8 + r8, an inner group
+// gl moves by 8192 (q8 - gl - 1) + r8; the row's last group ends at 8192 q8 (r8 = 0: the row's
+// end) or at the row's end + 8192 - r8, so it moves by r8 - 8192.
+__device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_t* sC, uint32_t col_r, uint32_t lane,
+                                               uint32_t l32, uint32_t acc, uint32_t gl, uint32_t nseg, uint32_t q8,
+                                               uint32_t r8, uint32_t* word) {
+#pragma unroll
+    for (int j = 0; j < kCrc32ScanPowers; j++) {
+        const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
+        const uint32_t t = __shfl_up(w, 1u << j);
+        if (lane >= (1u << j)) acc ^= t;
+    }
+    uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // wave-uniform from here on
+    if (gl + 1 < nseg) {
+        // whole segments, then the remainder r8
+        uint32_t a = q8 - gl - 1;
+        for (int i = 0; a; i++, a >>= 1)
+            if (a & 1) val = apply_lanes(sC[32 * i + l32], val, l32);
+        val = apply_lanes(col_r, val, l32);
+    } else if (r8) {
+        val = apply_lanes(col_r, apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32), l32);
+    }
+    if (lane == 0) atomicXor(word, val);
+}
+
+// Position of item `it` (nsup items per row): its row, first tile and tile count.
+struct Crc32Item {
+    uint64_t b;
+    uint32_t r, t0, nt;
+};
+__device__ __forceinline__ Crc32Item crc32_item(uint64_t it, uint32_t nsup, uint32_t nrows, uint32_t tpb) {
+    constexpr uint32_t kSup = kCrc32SupGroups * kCrc32SegTiles;
+    Crc32Item x;
+    uint32_t sup;
+    if (it < (uint64_t(1) << 32)) {  // 32-bit divisions (scalar), the common case
+        const uint32_t i32 = uint32_t(it), rid = i32 / nsup;
+        sup = i32 - rid * nsup;
+        const uint32_t b = rid / nrows;
+        x.b = b;
+        x.r = rid - b * nrows;
+    } else {
+        sup = uint32_t(it % nsup);
+        const uint64_t rid = it / nsup;
+        x.b = rid / nrows;
+        x.r = uint32_t(rid - x.b * nrows);
+    }
+    x.t0 = sup * kSup;
+    x.nt = tpb - x.t0 < kSup ? tpb - x.t0 : kSup;
+    return x;
+}
+
 }  // namespace
+
+// LDS staging shared by the rows passes: NT | SN | SG (19 KiB); SC stays in global memory
+#define RSMI_CRC32_ROWS_STAGE()                                                                           \
+    __shared__ uint32_t s_tbl[kCrc32LdsWords];                                                            \
+    for (int i = threadIdx.x; i < kCrc32LdsWords; i += kWG) s_tbl[i] = tbl[i];                            \
+    __syncthreads();                                                                                      \
+    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl);                                          \
+    const uint32_t* sS = s_tbl + kCrc32FoldWords;                                                         \
+    const uint32_t* sG = sS + kCrc32ScanPowers * kCrc32PowWords;                                          \
+    const uint32_t* sC = tbl + kCrc32LdsWords;                                                            \
+    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024)), r8 = uint32_t(S % (kCrc32SegTiles * 1024)); \
+    const uint32_t l32 = threadIdx.x & 31;                                                                \
+    uint32_t col_r = 0; /* A^r8, lane-distributed */                                                      \
+    _Pragma("unroll") for (int b_ = 0; b_ < 32; b_++) col_r = l32 == uint32_t(b_) ? sh.col[b_] : col_r;
 
 // tbl: NT[8][32][16] | SN[6][8][16] | SG[8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).
 // An item is up to kCrc32SupGroups 8-tile groups of one row: each group folds through the
@@ -80,18 +166,7 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
                                                             uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
                                                             uint32_t nseg, uint32_t nsup, uint64_t nitems,
                                                             uint32_t* __restrict__ out, uint64_t out_bs, Crc32Shift sh) {
-    __shared__ uint32_t s_tbl[kCrc32LdsWords];
-    for (int i = threadIdx.x; i < kCrc32LdsWords; i += kWG) s_tbl[i] = tbl[i];
-    __syncthreads();
-    const uint8_t* nb = reinterpret_cast<const uint8_t*>(s_tbl);
-    const uint32_t* sS = s_tbl + kCrc32FoldWords;
-    const uint32_t* sG = sS + kCrc32ScanPowers * kCrc32PowWords;
-    const uint32_t* sC = tbl + kCrc32LdsWords;
-    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024)), r8 = uint32_t(S % (kCrc32SegTiles * 1024));
-    const uint32_t l32 = threadIdx.x & 31;
-    uint32_t col_r = 0;  // A^r, lane-distributed
-#pragma unroll
-    for (int b = 0; b < 32; b++) col_r = l32 == uint32_t(b) ? sh.col[b] : col_r;
+    RSMI_CRC32_ROWS_STAGE()
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
@@ -130,51 +205,104 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __re
                 }
             uint32_t gs = 0;  // the group's value, relative to the end of its 8-tile span
 #pragma unroll
-            for (int i = 0; i < kCrc32SegTiles; i++) {
-                if (uint32_t(i) < nt) {
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        // byte offsets 4 x nibble into the 16-entry u32 tables (64 B each)
-                        uint32_t lo = (v[i][w] << 2) & 0x3C3C3C3Cu, hi = (v[i][w] >> 2) & 0x3C3C3C3Cu;
-                        asm volatile("" : "+v"(lo), "+v"(hi));  // keep the two masks (one extract per offset)
-                        uint32_t l[8];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const int p = 4 * w + q;
-                            const int o = 2048 * i + 128 * p;
-                            l[2 * q] = *reinterpret_cast<const uint32_t*>(nb + o + ((lo >> (8 * q)) & 0xFF));
-                            l[2 * q + 1] = *reinterpret_cast<const uint32_t*>(nb + o + 64 + ((hi >> (8 * q)) & 0xFF));
-                        }
-                        gs = xor3(gs, xor3(l[0], l[1], l[2]), xor3(l[3], l[4], l[5])) ^ (l[6] ^ l[7]);
-                    }
-                }
-            }
+            for (int i = 0; i < kCrc32SegTiles; i++)
+                if (uint32_t(i) < nt) gs ^= crc32_nib_chunk(nb + 2048 * i, v[i]);
             acc = (g == g0 ? 0u : pow_nib(sG, acc)) ^ gs;  // earlier groups move 8 KiB further
         }
+        crc32_item_out(sS, sC, col_r, lane, l32, acc, g1 - 1, nseg, q8, r8, out + b * out_bs + r);
+    }
+}
+
+// The nibble rows pass, software-pipelined, for 16-byte-aligned rows (the default): the CRC-16
+// pass's structure (rs_crc16_rows_pipe_kernel).  A wave works in units of half a group (4
+// tiles) and issues the loads of its next unit, of this item or its next one, before it folds
+// the current one (two register sets of 16 VGPRs, the loop unrolled by two).  Loads are
+// unconditional: chunks past the row's end re-read the row's last chunk and are masked to zero
+// in the fold, and the prefetch past the wave's last unit re-reads that unit.
+__global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t* __restrict__ tbl,
+                                                                 const uint8_t* __restrict__ base, uint64_t bstride,
+                                                                 uint64_t rpitch, uint32_t nrows, uint64_t S,
+                                                                 uint32_t tpb, uint32_t nseg, uint32_t nsup,
+                                                                 uint64_t nitems, uint32_t* __restrict__ out,
+                                                                 uint64_t out_bs, Crc32Shift sh) {
+    RSMI_CRC32_ROWS_STAGE()
+    constexpr int kU = kCrc32SegTiles / 2;  // tiles per unit
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
+    struct Unit {
+        uint64_t it;
+        Crc32Item x;
+        uint32_t h;  // half group within the item
+    };
+    auto at = [&](uint64_t it) -> Unit { return Unit{it, crc32_item(it, nsup, nrows, tpb), 0}; };
+    auto next = [&](const Unit& u) -> Unit {
+        if ((u.h + 1) * kU < u.x.nt) return Unit{u.it, u.x, u.h + 1};
+        return at(u.it + nw);
+    };
+    auto issue = [&](const Unit& u, u32x4(&v)[kU]) {
+        const uint8_t* row = base + u.x.b * bstride + uint64_t(u.x.r) * rpitch;
 #pragma unroll
-        for (int j = 0; j < kCrc32ScanPowers; j++) {
-            const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
-            const uint32_t t = __shfl_up(w, 1u << j);
-            if (lane >= (1u << j)) acc ^= t;
+        for (int i = 0; i < kU; i++) {
+            const uint64_t off = (uint64_t(u.x.t0 + u.h * kU + i) * kWave + lane) * 16;
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
         }
-        // lane 63's value, relative to the end of group g1 - 1, wave-uniform from here on
-        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));
-        const uint32_t gl = g1 - 1;
-        if (gl + 1 < nseg) {
-            // whole segments, then the remainder r
-            uint32_t a = q8 - gl - 1;
-            for (int i = 0; a; i++, a >>= 1)
-                if (a & 1) val = apply_lanes(sC[32 * i + l32], val, l32);
-            val = apply_lanes(col_r, val, l32);
-        } else if (r8) {
-            val = apply_lanes(col_r, apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32), l32);
+    };
+    uint32_t acc = 0, gs = 0;
+    auto finish = [&](const Unit& u, u32x4(&v)[kU]) {
+        const Crc32Item& x = u.x;
+        const uint32_t u0 = u.h * kU, t0 = x.t0 + u0;
+        const uint32_t nt = x.nt - u0 < uint32_t(kU) ? x.nt - u0 : uint32_t(kU);
+        const uint8_t* gt = nb + 2048 * kU * (u.h & 1);  // table sets of this half of the group
+#pragma unroll
+        for (int i = 0; i < kU; i++) {
+            if (uint32_t(i) < nt) {
+                if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
+                    const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const int64_t n = valid - 4 * w;
+                        v[i][w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                    }
+                }
+                gs ^= crc32_nib_chunk(gt + 2048 * i, v[i]);
+            }
         }
-        if (lane == 0) atomicXor(out + b * out_bs + r, val);
+        const bool item_end = u0 + kU >= x.nt;
+        if ((u.h & 1) || item_end) {  // the group is complete
+            acc = pow_nib(sG, acc) ^ gs;  // earlier groups move 8 KiB further from the end
+            gs = 0;
+        }
+        if (item_end) {
+            crc32_item_out(sS, sC, col_r, lane, l32, acc, (x.t0 + x.nt - 1) / kCrc32SegTiles, nseg, q8, r8,
+                           out + x.b * out_bs + x.r);
+            acc = 0;
+        }
+    };
+    const uint64_t it0 = uint64_t(blockIdx.x) * (kWG / kWave) + wid;
+    if (it0 >= nitems) return;
+    Unit cur = at(it0);
+    u32x4 va[kU], vb[kU];
+    issue(cur, va);
+    for (;;) {
+        Unit nx = next(cur);
+        bool more = nx.it < nitems;
+        issue(more ? nx : cur, vb);
+        finish(cur, va);
+        if (!more) break;
+        cur = nx;
+        nx = next(cur);
+        more = nx.it < nitems;
+        issue(more ? nx : cur, va);
+        finish(cur, vb);
+        if (!more) break;
+        cur = nx;
     }
 }
 
 void* crc32_rows_kernel(bool aligned) {
-    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_kernel<true>)
+    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_pipe_kernel)
                    : reinterpret_cast<void*>(&rs_crc32_rows_kernel<false>);
 }
 
