@@ -1,5 +1,6 @@
 """Host logic of the Erasure mirror (dag/node/dagnode/erasure.go) that runs without a GPU:
 validation, ShardSize, the EncodeData/DecodeDataBlocks short-circuits and error paths."""
+import numpy as np
 import pytest
 
 import rsmi
@@ -104,17 +105,40 @@ def test_key_gpu_stable_and_balanced():
     assert min(counts) > 300
 
 
+_CLMUL_LENGTHS = [0, 1, 7, 8, 9, 15, 16, 17, 100, 255, 256, 257, 271, 272, 511, 512, 513, 1000, 4099, 26215,
+                  26227, 104858, 262147]
+
+
 def test_datanode_crc_slice_by_8_matches_byte_serial():
-    """The datanode entry CRC (slice-by-8, csrc/host/datanode.cpp) equals the byte-serial
-    restatement of howeyc/crc16 Checksum(IBMTable) on every length class."""
+    """The datanode entry CRC (slice-by-8 below 256 bytes, carry-less-multiply folding from 256,
+    csrc/host/datanode.cpp + crc_clmul.cpp) equals the byte-serial restatement of
+    howeyc/crc16 Checksum(IBMTable) on every length class, from any register start value."""
     import ctypes
-    import random
 
     L = ctypes.CDLL(rsmi.LIB_PATH)
     f = L._ZN4rsmi4host9crc16_ibmEPKhmt
     f.restype = ctypes.c_uint16
     f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint16]
-    r = random.Random(5)
-    for n in [0, 1, 7, 8, 9, 15, 16, 17, 100, 1000, 4099, 26215]:
-        b = bytes(r.randrange(256) for _ in range(n))
+    rng = np.random.default_rng(5)
+    for n in _CLMUL_LENGTHS:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert f(b, n, 0) == multi.crc16_ibm(b), n
+        # a continued checksum (the entry's header first, then the shard) equals the whole one
+        h = n // 3
+        assert f(b[h:], n - h, f(b[:h], h, 0)) == multi.crc16_ibm(b), n
+
+
+def test_datanode_value_crc32_matches_zlib():
+    """The mutcask value CRC-32 of the in-process datanode (slice-by-8 / carry-less-multiply
+    folding) equals zlib's crc32 (Go crc32.ChecksumIEEE) on every length class."""
+    import ctypes
+    import zlib
+
+    L = ctypes.CDLL(rsmi.LIB_PATH)
+    f = L._ZN4rsmi4host10crc32_ieeeEPKhm
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    rng = np.random.default_rng(6)
+    for n in _CLMUL_LENGTHS:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert f(b, n) == zlib.crc32(b), n

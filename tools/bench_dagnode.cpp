@@ -197,7 +197,7 @@ int main(int argc, char** argv) {
                 gib / rep1, gib / repb, rep);
     std::printf("Put, mutcask       %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / put1m, gib / put1mh);
     std::printf("PutMany, mutcask   %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / putm, gib / putmh);
-    std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes)\n", gib / crc);
-    std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, slice-by-8)\n", gib / c32);
+    std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / crc);
+    std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / c32);
     return 0;
 }
