@@ -256,7 +256,7 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     std::vector<Bytes> shards;
     std::vector<uint32_t> raw, raw32;
     bool want32 = false;  // mutcask-backed datanodes keep a CRC-32 of every value as well
-    for (auto& sn : nodes_) want32 |= gpu_checksums_ && sn.client->WantsValueChecksum();
+    for (auto& sn : nodes_) want32 |= gpu_checksums_ && gpu_value_checksums_ && sn.client->WantsValueChecksum();
     s = gpu_checksums_ ? enc.EncodeDataWithCrcs(block, &shards, &raw, want32 ? &raw32 : nullptr)
                        : enc.EncodeData(block, &shards);
     if (!s.ok()) return s;
@@ -304,9 +304,10 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         const size_t chunk = staging_blocks(size_t(n) * S);
         const Bytes meta = encode_meta(int32_t(B));
         const int wq = EntryQuorum().second;
-        // datanodes over mutcask keep a CRC-32 of every value: the GPU pass supplies it too
+        // datanodes over mutcask keep a CRC-32 of every value: the GPU pass supplies it too when
+        // asked (SetGpuValueChecksums), else each datanode folds its own
         bool want32 = false;
-        for (auto& sn : nodes_) want32 |= sn.client->WantsValueChecksum();
+        for (auto& sn : nodes_) want32 |= gpu_value_checksums_ && sn.client->WantsValueChecksum();
         std::vector<uint32_t> raw, raw32;
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
@@ -879,7 +880,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 if (present[i]) std::memcpy(flat + (j * n + i) * S, pend[j].shards[i].data(), S);
         // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
         DataNodeClient& target = *nodes_[to].client;
-        const bool want32 = gpu_checksums_ && target.WantsValueChecksum();
+        const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
         std::vector<uint32_t> r16(gpu_checksums_ ? nb * size_t(n) : 0), r32(want32 ? nb * size_t(n) : 0);
         rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, nb, present.data(),
                                                                     required.data(), r16.data(),

@@ -107,6 +107,12 @@ public:
     // instead of leaving the byte-serial CRC to the datanode.  On by
     // default; the stored entries are byte-identical either way.
     void SetGpuChecksums(bool v) { gpu_checksums_ = v; }
+    // With SetGpuChecksums, also compute the mutcask value CRC-32 (cask.go:73-79) on the GPU
+    // (a separate rows pass after the encode).  Off by default: the datanode's own
+    // carry-less-multiply fold (crc_clmul.hpp, ~30 GiB/s per core, run in the datanode calls'
+    // fan-out) measured faster than the extra GPU pass.  Stored values are
+    // byte-identical either way.
+    void SetGpuValueChecksums(bool v) { gpu_value_checksums_ = v; }
     // Get / GetMany read shards with DataNodeClient::GetForVerify and check the stored entry
     // (and mutcask value) checksums on the GPU, one call per fetch wave, instead of each
     // datanode checking its own (server.go:93-97, cask.go:250).  A shard that fails is
@@ -158,6 +164,7 @@ private:
     int num_slots_ = 0;
     int device_ = 0;
     bool gpu_checksums_ = true;
+    bool gpu_value_checksums_ = false;
     bool gpu_verified_reads_ = false;
     // GPU check of the unverified shards of one fetch wave; failures become errors in got[]
     void verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas, const std::vector<Bytes>& data,

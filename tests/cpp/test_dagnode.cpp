@@ -552,9 +552,13 @@ static void test_gpu_entry_checksums() {
 // themselves, and both checksums equal the oracle's.  Single Puts get both from the
 // coalesced encode (rsmi_encode_block_coalesced_crcs).  Reads verify both.
 static void test_gpu_value_checksums() {
+    // the value CRC-32 from the GPU pass (SetGpuValueChecksums) and from each datanode's own
+    // fold (the default): stored values byte-identical to the host-checksummed cluster's
+    for (bool gpu32 : {true, false})
     for (auto km : {std::make_pair(2, 1), std::make_pair(10, 4), std::make_pair(16, 4)}) {
         const int k = km.first, m = km.second, n = k + m;
         Cluster gpu(k, m, KvEngine::Mutcask), host(k, m, KvEngine::Mutcask);
+        gpu.node->SetGpuValueChecksums(gpu32);
         host.node->SetGpuChecksums(false);
         std::mt19937_64 r(91 + k);
         std::vector<std::string> keys;

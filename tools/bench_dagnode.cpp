@@ -152,9 +152,10 @@ int main(int argc, char** argv) {
     d->RepairDataNodeBatched(0, 3, 256, &rep);
     const double repb = secs(t0);
     // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
-    // entry (cask.go:73-79).  PutMany with both checksums from the GPU pass, against the
-    // datanodes computing both themselves.
-    double putm = 0, putmh = 0, put1m = 0, put1mh = 0, c32 = 0;
+    // entry (cask.go:73-79).  Put / PutMany with the entry CRC-16 from the GPU pass and the
+    // value CRC-32 from each datanode (the default), against the datanodes computing both, and
+    // against both from the GPU.
+    double putm = 0, putmh = 0, put1m = 0, put1mh = 0, putm32 = 0, put1m32 = 0, c32 = 0;
     {
         DagNodeConfig mc = cfg;
         std::vector<std::shared_ptr<DataNodeClient>> mcl;
@@ -178,6 +179,13 @@ int main(int argc, char** argv) {
         t0 = clk::now();
         md->PutMany(keys, blocks);
         putm = secs(t0);
+        md->SetGpuValueChecksums(true);  // the CRC-32 from the GPU pass as well
+        t0 = clk::now();
+        for (int i = 0; i < N; i++) md->Put(keys[i], blocks[i]);
+        put1m32 = secs(t0);
+        t0 = clk::now();
+        md->PutMany(keys, blocks);
+        putm32 = secs(t0);
         t0 = clk::now();
         volatile uint32_t s32 = 0;
         for (int i = 0; i < N; i++) s32 ^= crc32_ieee(blocks[i].data(), blocks[i].size());
@@ -195,8 +203,10 @@ int main(int argc, char** argv) {
                 gcalls, gbatches);
     std::printf("RepairDataNode     %8.2f GiB/s (of block payload)\nRepair batched     %8.2f GiB/s (%zu keys)\n",
                 gib / rep1, gib / repb, rep);
-    std::printf("Put, mutcask       %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / put1m, gib / put1mh);
-    std::printf("PutMany, mutcask   %8.2f GiB/s (datanode CRCs: %.2f)\n", gib / putm, gib / putmh);
+    std::printf("Put, mutcask       %8.2f GiB/s (datanode CRCs: %.2f; CRC-32 on the GPU too: %.2f)\n", gib / put1m,
+                gib / put1mh, gib / put1m32);
+    std::printf("PutMany, mutcask   %8.2f GiB/s (datanode CRCs: %.2f; CRC-32 on the GPU too: %.2f)\n", gib / putm,
+                gib / putmh, gib / putm32);
     std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / crc);
     std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / c32);
     return 0;
