@@ -8,6 +8,7 @@
 #include "../../include/rsmi.h"
 #include "crc16.hpp"
 #include "crc32.hpp"
+#include "host/datanode.hpp"
 
 using namespace rsmi;
 
@@ -73,9 +74,10 @@ int rsmi_check_shards(int n, const size_t* lens, int nil_ok, size_t* S_out) {
     return RSMI_OK;
 }
 
-uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return crc16_checksum(p, n); }
+// the datanode's host CRCs: carry-less-multiply folding from 256 bytes (host/crc_clmul.hpp)
+uint16_t rsmi_crc16_ibm(const uint8_t* p, size_t n) { return host::crc16_ibm(p, n); }
 
-uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n) { return crc32_checksum(p, n); }
+uint32_t rsmi_crc32_ieee(const uint8_t* p, size_t n) { return host::crc32_ieee(p, n); }
 
 uint32_t rsmi_crc32_entry(const uint8_t* head, size_t head_len, uint32_t raw, size_t data_len) {
     return crc32_entry(head, head_len, raw, data_len);

@@ -46,7 +46,7 @@ def test_oracle_check_value():
 
 def test_library_checksum_matches_oracle():
     r = random.Random(11)
-    for n in [0, 1, 2, 15, 16, 17, 255, 1024, 4099, 26215]:
+    for n in [0, 1, 2, 15, 16, 17, 255, 256, 257, 272, 1024, 4099, 26215, 26227, 104858]:
         b = bytes(r.randrange(256) for _ in range(n))
         assert rsmi.crc16_ibm(b) == orc.crc16_ibm(b), n
 

@@ -34,7 +34,7 @@ def test_oracle_check_value_and_zlib():
 
 def test_library_checksum_matches_zlib():
     r = np.random.default_rng(12)
-    for n in [0, 1, 7, 16, 1023, 1024, 1025, 26215, 262144]:
+    for n in [0, 1, 7, 16, 255, 256, 257, 1023, 1024, 1025, 26215, 262144, 262147]:
         b = r.integers(0, 256, size=n, dtype=np.uint8).tobytes()
         assert rsmi.crc32_ieee(b) == zlib.crc32(b), n
 
