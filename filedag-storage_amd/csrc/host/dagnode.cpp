@@ -519,10 +519,17 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
     s = enc.DecodeDataBlocks(f.shards);
     if (!s.ok()) return s;
     const size_t S = size_t(enc.ShardSize());
-    block->assign(size_t(config_.data_blocks) * S, 0);
-    for (int i = 0; i < config_.data_blocks; i++)
-        std::memcpy(block->data() + size_t(i) * S, f.shards[i].data(), std::min(S, f.shards[i].size()));
-    block->resize(size_t(f.meta.block_size));
+    // the first k shards concatenated and truncated to BlockSize (node.go:311-319), copied
+    // once (no zero fill of the whole block first)
+    const size_t bs = size_t(f.meta.block_size);
+    block->clear();
+    block->reserve(bs);
+    for (int i = 0; i < config_.data_blocks && block->size() < bs; i++) {
+        const size_t take = std::min(bs - block->size(), std::min(S, f.shards[i].size()));
+        block->insert(block->end(), f.shards[i].begin(), f.shards[i].begin() + long(take));
+        if (take < S && block->size() < bs) block->resize(std::min(bs, block->size() + (S - take)), 0);
+    }
+    block->resize(bs);
     if (!f.repair.empty()) {  // the shards move into the task: `f` is spent after this
         const int32_t bs = f.meta.block_size;
         std::lock_guard<std::mutex> g(q_mu_);

@@ -1,6 +1,8 @@
 // erasure.cpp -- see erasure.hpp.
 #include "erasure.hpp"
 
+#include <memory>
+
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -62,6 +64,21 @@ PinnedBuf& thread_staging() {
 }
 
 namespace {
+// per-thread scratch for one block's (k+m)*S rows around a single-block encode or
+// reconstruct: neither zero-filled (the call writes every byte it returns) nor allocated per
+// call (a 364 KB vector per Put or Get was a fresh value-initialised allocation each time)
+uint8_t* block_scratch(size_t bytes) {
+    static thread_local std::unique_ptr<uint8_t[]> p;
+    static thread_local size_t cap = 0;
+    if (bytes > cap) {
+        p.reset(new (std::nothrow) uint8_t[bytes]);
+        cap = p ? bytes : 0;
+    }
+    return p.get();
+}
+}  // namespace
+
+namespace {
 std::mutex g_ctx_mu;
 std::map<std::tuple<int, int, int>, rsmi_ctx*> g_ctx_cache;  // lives for the process
 }  // namespace
@@ -106,10 +123,11 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
-    Bytes flat(size_t(n) * S);
-    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat.data(), nullptr);
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
+    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat, nullptr);
     if (rc) return rsmi_status(rc);
-    for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    for (int i = 0; i < n; i++) (*shards)[i].assign(flat + i * S, flat + (i + 1) * S);
     return Status::Ok();
 }
 
@@ -128,13 +146,14 @@ Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
-    Bytes flat(size_t(n) * S);
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
     raw->assign(size_t(n), 0);
     if (raw32) raw32->assign(size_t(n), 0);
-    rc = rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat.data(), raw->data(),
+    rc = rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat, raw->data(),
                                           raw32 ? raw32->data() : nullptr);
     if (rc) return rsmi_status(rc);
-    for (int i = 0; i < n; i++) (*shards)[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    for (int i = 0; i < n; i++) (*shards)[i].assign(flat + i * S, flat + (i + 1) * S);
     return Status::Ok();
 }
 
@@ -159,15 +178,16 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
     if (np == n || (data_only && dp == data_blocks_)) return Status::Ok();
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
-    Bytes flat(size_t(n) * S);  // [][]byte -> one contiguous buffer for the C-ABI
+    // [][]byte -> one contiguous buffer for the C-ABI (missing rows: don't-care bytes)
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
     for (int i = 0; i < n; i++)
-        if (present[i]) std::memcpy(flat.data() + size_t(i) * S, shards[i].data(), S);
+        if (present[i]) std::memcpy(flat + size_t(i) * S, shards[i].data(), S);
     // coalesced: concurrent degraded Gets usually miss the same node's shard, so they batch
-    rc = rsmi_reconstruct_coalesced(c, flat.data(), S, present.data(), data_only ? 1 : 0);
+    rc = rsmi_reconstruct_coalesced(c, flat, S, present.data(), data_only ? 1 : 0);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++)
-        if (!present[i] && (i < data_blocks_ || !data_only))
-            shards[i].assign(flat.begin() + size_t(i) * S, flat.begin() + size_t(i + 1) * S);
+        if (!present[i] && (i < data_blocks_ || !data_only)) shards[i].assign(flat + size_t(i) * S, flat + size_t(i + 1) * S);
     return Status::Ok();
 }
 
