@@ -45,6 +45,18 @@ Crc16Tables::Crc16Tables() {
     for (int k = 0; k < 8; k++)
         for (int p = 0; p < 32; p++)
             for (int v = 0; v < 16; v++) G[k][p][v] = shift(N[p][v], uint64_t(1024 * (7 - k)));
+    const uint32_t code4[4] = {4, 2, 1, 1};
+    for (int t = 0; t < 8; t++)
+        for (int s = 0; s < 4; s++)
+            for (int l = 0; l < 64; l++) {
+                const int j = l >> 4, n = l & 15;
+                for (int w = 0; w < 4; w++) MW[t][s][l][w] = 0;
+                for (int e = 0; e < 32; e++) {
+                    const uint16_t c = shift(U[15 - (e >> 1)][1 << (s + 4 * (e & 1))],
+                                             uint64_t(256 * (3 - j) + 1024 * (7 - t)));
+                    if ((c >> n) & 1) MW[t][s][l][e / 8] |= code4[s] << (4 * (e % 8));
+                }
+            }
     // the group order the negative shifts rely on: A^32767 = I on a basis
     for (int bit = 0; bit < 16; bit++)
         if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();

@@ -41,6 +41,13 @@ struct Crc16Tables {
     // nibble-sliced power tables of the rows pass: P4[i][h][v] = A^(2^i)(v << 4h) (16-entry
     // tables never conflict; 1.9 KiB where P takes 15 KiB)
     uint16_t P4[kCrcPowers][4][16];
+    // fp4 weight operands of the matrix-core rows pass (rs_crc16_rows_mfma_kernel), per tile t
+    // of an 8-tile group, bit group s (data bits s and s + 4 of every byte), lane l = 16 j + n:
+    // nibble e of the lane's 16 bytes weighs data bit s + 4 (e & 1) of byte e >> 1 of chunk
+    // 16 j + m for CRC bit n, relative to the end of chunk 48 + m of the group's tile 7; fp4
+    // codes 2.0 / 1.0 / 0.5 / 0.5 (s = 0..3) against data values 0.5 / 1 / 2 / 2, so every
+    // product of a set data bit and a set weight is 1.0
+    uint32_t MW[8][4][64][4];
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
     // A^n(s) for any n >= 0 (reduced mod 32767)

@@ -645,6 +645,114 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
     }
 }
 
+// The rows pass with the fold on the matrix cores, aligned rows.  R(chunk) is
+// GF(2)-linear in the chunk's 128 bits, so a tile's fold is a GF(2) matrix product; the fp4
+// MFMA v_mfma_scale_f32_16x16x128_f8f6f4 sums integer products exactly, and bit 0 of each count
+// is the product's bit.  B = the tile's data, one data bit per fp4 nibble (v & 0x11111111,
+// 0x22.., 0x44.., (v >> 1) & 0x44..; bit 3 is the e2m1 sign), column m = lane & 15, k block
+// j = lane >> 4 (chunk 16 j + m); A = the weights of tile t of an 8-tile group (MW, in LDS,
+// one ds_read_b128 per MFMA), row n = CRC bit; every product of a set data bit and a set weight
+// is 1.0.  The counts of a whole group accumulate in one f32 quad (at most 4096 per count), so
+// the parity is read once per group: four ballots, and lane m (< 16) gathers class m's value
+// (chunks m, m + 16, m + 32, m + 48 of the group's tiles, relative to the end of chunk 48 + m
+// of tile 7).  Groups step by A^8192 as in the nibble pass; at the item's end a 4-level scan
+// over lanes 0..15 (A^(16 * 2^j)) leaves the value relative to the group's end in lane 15, and
+// the shift to the row's end is the nibble pass's.  4 MFMAs and 20 VALU per tile fold what the
+// nibble tables fold with 32 lookups and ~70 VALU.
+typedef int mfma_v8i __attribute__((ext_vector_type(8)));
+typedef float mfma_v4f __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t* __restrict__ tbl,
+                                                                 const uint8_t* __restrict__ base, uint64_t bstride,
+                                                                 uint64_t rpitch, uint32_t nrows, uint64_t S,
+                                                                 uint32_t tpb, uint32_t nsup, uint64_t nitems,
+                                                                 uint32_t* __restrict__ out, uint64_t out_bs,
+                                                                 Crc16Shift sh) {
+    __shared__ uint32_t s_p4[kCrcP4Words];
+    __shared__ u32x4 s_w[kCrcMWWords / 4];
+    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = tbl[kCrcP4Off + i];
+    for (int i = threadIdx.x; i < kCrcMWWords / 4; i += kWG)
+        s_w[i] = reinterpret_cast<const u32x4*>(tbl + kCrcMWOff)[i];
+    __syncthreads();
+    const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_p4);
+    uint32_t col_e = 0;  // A^E, lane-distributed
+#pragma unroll
+    for (int b = 0; b < 16; b++) col_e = (threadIdx.x & 15u) == uint32_t(b) ? sh.col[b] : col_e;
+    const uint64_t last_end = (uint64_t(tpb) + kCrcSegTiles - 1) / kCrcSegTiles * kCrcSegTiles * (kWave * 16);
+    const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
+    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
+        const CrcItem x = crc_item(it, nsup, nrows, tpb);
+        const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
+        uint32_t acc = 0;  // lanes 0..15: class m's running value
+        for (uint32_t g0 = 0; g0 < x.nt; g0 += kCrcSegTiles) {
+            const uint32_t t0 = x.t0 + g0;
+            const uint32_t nt = x.nt - g0 < uint32_t(kCrcSegTiles) ? x.nt - g0 : uint32_t(kCrcSegTiles);
+            u32x4 v[kCrcSegTiles];
+#pragma unroll
+            for (int i = 0; i < kCrcSegTiles; i++) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
+                v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
+            }
+            mfma_v4f c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < kCrcSegTiles; i++) {
+                if (uint32_t(i) < nt) {
+                    u32x4 d = v[i];
+                    if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
+                        const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const int64_t n = valid - 4 * w;
+                            d[w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        mfma_v8i bd;
+#pragma unroll
+                        for (int w = 0; w < 4; w++)
+                            bd[w] = int(q < 3 ? d[w] & (0x11111111u << q) : (d[w] >> 1) & 0x44444444u);
+                        bd[4] = bd[5] = bd[6] = bd[7] = 0;
+                        const u32x4 wt = s_w[(i * 4 + q) * kWave + lane];
+                        const mfma_v8i aw = {int(wt[0]), int(wt[1]), int(wt[2]), int(wt[3]), 0, 0, 0, 0};
+                        c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bd, c, 4, 4, 0, 127, 0, 127);
+                    }
+                }
+            }
+            // parity bits -> class m's 16-bit value: bit n of class m is bit 16 (n >> 2) + m of
+            // ballot n & 3
+            uint32_t Y = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint64_t bl = __builtin_amdgcn_ballot_w64((int(c[i]) & 1) != 0);
+                const uint32_t lo = uint32_t(bl) >> m, hi = uint32_t(bl >> 32) >> m;
+                Y |= ((lo & 0x10001u) | ((hi & 0x10001u) << 8)) << i;  // n = i, 4 + i (bit 16), 8 + i, 12 + i (bit 24)
+            }
+            const uint32_t val = (Y & 0x0F0Fu) | ((Y >> 12) & 0xF0F0u);
+            acc = crc_pow4(sQ, 13, acc) ^ val;  // earlier groups move 8 KiB further from the end
+        }
+        // classes -> the group's end: lane 15 takes sum_m A^(16 (15 - m)) (class m)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (m >= (1u << j)) acc ^= t;
+        }
+        uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), 15));  // wave-uniform from here
+        const uint32_t dd = uint32_t((last_end - crc_item_end(x)) % kCrcOrder);
+#pragma unroll
+        for (int i = 0; i < kCrcPowers; i++)
+            if ((dd >> i) & 1) val = crc_pow4(sQ, i, val);
+        val = crc_apply_cols(col_e, val, lane & 15u);
+        if (lane == kWave - 1) atomicXor(out + x.b * out_bs + x.r, val);
+    }
+}
+
+void* crc16_rows_mfma_kernel() { return reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel); }
+
 // R(row) from the fused encode's tile records (rs_fast_kernel CRC): one wave per block (a
 // persistent grid strides over blocks).  Lane l takes quads i = 64 j + l of the block (quad i =
 // chunks 4i..4i+3, tile i / 16, record lane 4 (i % 16) + q), loads the quad values of every

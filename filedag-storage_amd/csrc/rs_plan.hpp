@@ -49,7 +49,9 @@ constexpr int kCrcGWords = 8 * 32 * 16 / 2;     // tile-set nibble tables (rows 
 constexpr int kCrcGOff = kCrcQOff + kCrcQWords;
 constexpr int kCrcP4Words = 15 * 4 * 16 / 2;     // nibble-sliced powers (rows pass)
 constexpr int kCrcP4Off = kCrcGOff + kCrcGWords;
-constexpr int kCrcTableWords = kCrcP4Off + kCrcP4Words;
+constexpr int kCrcMWWords = 8 * 4 * 64 * 4;       // fp4 weight operands (matrix-core rows pass)
+constexpr int kCrcMWOff = kCrcP4Off + kCrcP4Words;
+constexpr int kCrcTableWords = kCrcMWOff + kCrcMWWords;
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
@@ -67,6 +69,7 @@ struct Crc16Shift {
     uint32_t col[16];
 };
 void* crc16_rows_kernel(bool aligned);
+void* crc16_rows_mfma_kernel();  // aligned rows, the fold on the matrix cores
 void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
 void* crc32_rows_kernel(bool aligned);
 

@@ -368,6 +368,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "coalesce_max")) {
         if (value < 1 || value > 65536) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_max = value;
+    } else if (!std::strcmp(key, "crc16_fold")) {
+        if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_crc16_fold = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;

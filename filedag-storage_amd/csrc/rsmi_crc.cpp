@@ -14,13 +14,16 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) + sizeof(t.G) + sizeof(t.P4) == size_t(kCrcTableWords) * 4, "CRC table layout");
+    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) + sizeof(t.G) + sizeof(t.P4) + sizeof(t.MW) ==
+                      size_t(kCrcTableWords) * 4,
+                  "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
     std::memcpy(h.data(), t.P, sizeof(t.P));
     std::memcpy(h.data() + kCrcPWords * 2, t.N, sizeof(t.N));
     std::memcpy(h.data() + kCrcQOff * 2, t.Q, sizeof(t.Q));
     std::memcpy(h.data() + kCrcGOff * 2, t.G, sizeof(t.G));
     std::memcpy(h.data() + kCrcP4Off * 2, t.P4, sizeof(t.P4));
+    std::memcpy(h.data() + kCrcMWOff * 2, t.MW, sizeof(t.MW));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -35,7 +38,7 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     if (zero) HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
     if (S == 0) return RSMI_OK;  // R(empty) = 0
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = crc16_rows_kernel(aligned);
+    void* fn = aligned && c->opt_crc16_fold == 1 ? crc16_rows_mfma_kernel() : crc16_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16;
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;

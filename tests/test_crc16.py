@@ -93,12 +93,16 @@ def _device_rows(nb, nrows, S, pitch, offset, seed):
                                32769, 36865, 65536, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 @pytest.mark.parametrize("wpc", [0, 1])
-def test_rows_dev_matches_oracle(S, layout, wpc):
-    """Aligned rows take the pipelined pass, others the plain one; waves_per_cu=1 makes each
-    wave walk many items (the pipelined pass's two register sets alternate).  Row sizes cover
-    half-group, group (8 KiB) and item (32 KiB) boundaries on both sides."""
+@pytest.mark.parametrize("fold", [1, 0])
+def test_rows_dev_matches_oracle(S, layout, wpc, fold):
+    """Aligned rows take the matrix-core pass (fold 1, the default) or the pipelined nibble pass
+    (fold 0), others the plain nibble one; waves_per_cu=1 makes each wave walk many items (the
+    pipelined pass's two register sets alternate).  Row sizes cover half-group, group (8 KiB) and
+    item (32 KiB) boundaries on both sides."""
     import torch
 
+    if layout == "unaligned" and fold == 0:
+        pytest.skip("unaligned rows have one fold")
     nrows, nb = 3, 5
     if layout == "aligned":
         pitch, off = (S + 15) // 16 * 16 + 16, 0
@@ -108,6 +112,7 @@ def test_rows_dev_matches_oracle(S, layout, wpc):
     out = torch.full((nb, nrows + 1), 0xDEAD, dtype=torch.int32, device="cuda")
     with rsmi.Codec(4, 2) as c:
         c.set_option("waves_per_cu", wpc)
+        c.set_option("crc16_fold", fold)
         c.crc16_rows_dev(dev.data_ptr() + off, pitch, nrows * pitch, nrows, S, nb, out.data_ptr(), nrows + 1)
         torch.cuda.synchronize()
     got = out.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
@@ -121,7 +126,8 @@ def test_rows_dev_matches_oracle(S, layout, wpc):
 
 
 @pytest.mark.gpu
-def test_rows_dev_full_size_batch():
+@pytest.mark.parametrize("fold", [1, 0])
+def test_rows_dev_full_size_batch(fold):
     """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows: a checksum of checksums against the
     oracle on a sample of rows, plus every row nonzero-tested against its own recompute."""
     import torch
@@ -133,6 +139,7 @@ def test_rows_dev_full_size_batch():
     dev = torch.randint(0, 256, (nb, n, pitch), dtype=torch.uint8, device="cuda", generator=g)
     out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
     with rsmi.Codec(k, m) as c:
+        c.set_option("crc16_fold", fold)
         c.crc16_rows_dev(dev.data_ptr(), pitch, n * pitch, n, S, nb, out.data_ptr(), n)
         torch.cuda.synchronize()
         assert c.last_kernel() == "rs_crc16_rows_kernel"

@@ -15,7 +15,7 @@ import rsmi  # noqa: E402
 
 
 # env CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
-FOLDS = ["crc16", "crc32"]
+FOLDS = ["crc16", "crc16nib", "crc32"]  # crc16: the default fold (matrix cores); crc16nib: nibble tables
 WPC = int(os.environ.get("CRC_WPC", "0"))
 
 
@@ -31,6 +31,8 @@ def main():
             c = rsmi.Codec(k, m)
             if WPC:
                 c.set_option("waves_per_cu", WPC)
+            if fold == "crc16nib":
+                c.set_option("crc16_fold", 0)
             if fold == "crc32":
                 f = lambda: c.crc32_rows_dev(buf.data_ptr(), p, n * p, n, S, nb, out.data_ptr(), n, st.cuda_stream)
             else:
@@ -48,7 +50,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
-            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {'crc32 (mutcask)' if fold == 'crc32' else 'crc16 (datanode)'}: "
+            print(f"RS({k},{m}) B={B} nb={nb} rows={nb * n} S={S} {dict(crc32='crc32 (mutcask)', crc16='crc16 (datanode, matrix cores)', crc16nib='crc16 (datanode, nibble tables)')[fold]}: "
                   f"{med * 1e3:8.1f} us  {nb * n * S / med / 1e6:8.1f} GB/s", flush=True)
             c.close()
 

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kWG) void fold_i8(const uint8_t* __restrict__ buf, 
 // value of class m (chunks m, m+16, m+32, m+48 of a tile) relative to the end of chunk 48 + m
 static uint16_t class_value(const uint8_t* tile, int m) {
     uint16_t v = 0;
-    for (int j = 0; j < 4; j++) v ^= zshift(host_chunk(tile + 16 * (16 * j + m)), 16 * (3 - j));
+    for (int j = 0; j < 4; j++) v ^= zshift(host_chunk(tile + 16 * (16 * j + m)), 256 * (3 - j));  // 16 chunks apart
     return v;
 }
 static uint16_t quad_value(const uint8_t* tile, int q) {
@@ -211,7 +211,7 @@ int main(int argc, char** argv) {
         for (int l = 0; l < 64; l++) {
             const int j = l >> 4, n = l & 15;
             for (int e = 0; e < 32; e++) {
-                const uint16_t c = zshift(contrib(e >> 1, s + 4 * (e & 1)), 16 * (3 - j));
+                const uint16_t c = zshift(contrib(e >> 1, s + 4 * (e & 1)), 256 * (3 - j));
                 if ((c >> n) & 1) w4[(s * 64 + l) * 4 + e / 8] |= code4[s] << (4 * (e % 8));
             }
         }
@@ -219,7 +219,7 @@ int main(int argc, char** argv) {
         for (int l = 0; l < 64; l++) {
             const int j = l >> 4, n = l & 15;
             for (int e = 0; e < 16; e++) {
-                const uint16_t c = zshift(contrib(e, s), 16 * (3 - j));
+                const uint16_t c = zshift(contrib(e, s), 256 * (3 - j));
                 if ((c >> n) & 1) w8[(s * 64 + l) * 4 + e / 4] |= (s == 0 ? 0x80u : (1u << (7 - s))) << (8 * (e % 4));
             }
         }
