@@ -217,7 +217,8 @@ int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     rc = launch_crc(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
                     static_cast<hipStream_t>(stream));
     if (rc) return rc;
-    c->last_kernel = "rs_crc16_rows_kernel";
+    const bool aligned = reinterpret_cast<uintptr_t>(d_rows) % 16 == 0 && shard_stride % 16 == 0 && block_stride % 16 == 0;
+    c->last_kernel = aligned && c->opt_crc16_fold == 1 ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel";
     return hip_status(hipGetLastError());
 }
 

@@ -142,7 +142,7 @@ def test_rows_dev_full_size_batch(fold):
         c.set_option("crc16_fold", fold)
         c.crc16_rows_dev(dev.data_ptr(), pitch, n * pitch, n, S, nb, out.data_ptr(), n)
         torch.cuda.synchronize()
-        assert c.last_kernel() == "rs_crc16_rows_kernel"
+        assert c.last_kernel() == ("rs_crc16_rows_kernel,MFMA" if fold else "rs_crc16_rows_kernel")
     got = out.cpu().numpy()
     rng = random.Random(1)
     for _ in range(64):
