@@ -768,10 +768,11 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_kernel(const uint32_t* _
                                                                uint32_t nsh, uint64_t S, uint64_t nblocks,
                                                                uint32_t* __restrict__ out) {
     constexpr int R = 8 * NS2;  // rows carried per lane (padding rows stay zero)
-    __shared__ __attribute__((aligned(128))) uint32_t s_tbl[kCrcPWords];
-    for (int i = threadIdx.x; i < kCrcPWords; i += kWG) s_tbl[i] = tbl[i];
+    // nibble-sliced powers (P4, 1.9 KiB, 16-entry tables: conflict-free), 4 lookups per power
+    __shared__ uint32_t s_tbl[kCrcP4Words];
+    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_tbl[i] = tbl[kCrcP4Off + i];
     __syncthreads();
-    auto pw = [&](int i, uint32_t x) { return crc_pow(reinterpret_cast<const uint16_t*>(s_tbl), i, x); };
+    auto pw = [&](int i, uint32_t x) { return crc_pow4(reinterpret_cast<const uint16_t*>(s_tbl), i, x); };
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);

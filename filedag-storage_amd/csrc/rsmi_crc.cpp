@@ -155,8 +155,8 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
     uint32_t tpb32 = uint32_t(tpb), nsh32 = uint32_t(nsh);
     uint64_t S64 = S, nb64 = nblocks;
     void* args[] = {&tb, &rec, &tail, &tpb32, &nsh32, &S64, &nb64, &raw};
-    // one wave per block, a persistent grid of up to 8 workgroups per CU (the power tables take
-    // 15 KiB of LDS per workgroup, so 10 fit)
+    // one wave per block, a persistent grid of up to 8 workgroups per CU (the nibble-sliced
+    // power tables take 1.9 KiB of LDS per workgroup)
     const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
     void* fn = crc16_combine_kernel(int(ns2));
     if (!fn) return RSMI_ERR_INVALID_ARG;
