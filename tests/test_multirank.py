@@ -63,23 +63,25 @@ def test_two_rank_gloo_partition_and_timing(tmp_path):
     assert ok.all(), ok
 
 
-def test_bench_spawns_ranks_itself_mock():
-    """`bench.py --gpus 2` with no launcher starts its two ranks itself (before any GPU call)
-    and rank 0 prints one line with n_gpus 2.  --mock swaps the device step for a CPU stand-in
-    so the launcher, gloo, the reductions and the JSON line run here without a GPU."""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_spawns_ranks_itself_mock(n):
+    """`bench.py --gpus N` with no launcher starts its N ranks itself (before any GPU call) and
+    rank 0 prints one line with n_gpus N -- N = 8 is the driver's scaling run's shape.  --mock
+    swaps the device step for a CPU stand-in so the launcher, gloo, the reductions and the JSON
+    line run here without a GPU."""
     import json
     import subprocess
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mock", "--steps", "3"],
-                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--mock", "--steps", "3"],
+                         capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.strip()]
     assert len(lines) == 1 and lines[0].startswith("{"), out.stdout  # stdout holds the JSON line only
     j = json.loads(lines[0])
-    assert j["n_gpus"] == 2 and j["mock"] and j["steps"] == 3
-    assert sorted(r["rank"] for r in j["config"]["ranks"]) == [0, 1]
-    assert sum(r["blocks"] for r in j["config"]["ranks"]) == 16
+    assert j["n_gpus"] == n and j["mock"] and j["steps"] == 3
+    assert sorted(r["rank"] for r in j["config"]["ranks"]) == list(range(n))
+    assert sum(r["blocks"] for r in j["config"]["ranks"]) == 8 * n
 
 
 def test_bench_rejects_world_size_mismatch():
