@@ -17,6 +17,7 @@ import rsmi  # noqa: E402
 # env CRC_WPC (rows-kernel grid cap in waves per CU; 0 = default)
 FOLDS = ["crc16", "crc16nib", "crc32"]  # crc16: the default fold (matrix cores); crc16nib: nibble tables
 WPC = int(os.environ.get("CRC_WPC", "0"))
+SPLIT = os.environ.get("CRC_SPLIT", "0") == "1"  # rows back to back at pitch S (the unaligned passes)
 
 
 def main():
@@ -24,7 +25,7 @@ def main():
     for k, m, B, nb in ((10, 4, 262144, 4096), (10, 4, 1 << 20, 1024), (16, 4, 4 << 20, 256)):
         n = k + m
         S = (B + k - 1) // k
-        p = rsmi.recommended_pitch(S)
+        p = S if SPLIT else rsmi.recommended_pitch(S)
         buf = torch.randint(0, 256, (nb, n, p), dtype=torch.uint8, device="cuda")
         out = torch.empty((nb, n), dtype=torch.int32, device="cuda")
         for fold in FOLDS:
