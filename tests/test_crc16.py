@@ -126,6 +126,36 @@ def test_rows_dev_matches_oracle(S, layout, wpc, fold):
 
 
 @pytest.mark.gpu
+def test_rows_dev_random_shapes_both_folds():
+    """40 random aligned geometries (row length, rows per block, blocks, pitch and block stride
+    with random 16-byte padding): the matrix-core and the nibble folds give the oracle's R(row)
+    on every row."""
+    import torch
+
+    rng = random.Random(2026)
+    for _ in range(40):
+        S = rng.choice([rng.randrange(1, 2048), rng.randrange(2048, 70000), rng.randrange(70000, 300000)])
+        nrows, nb = rng.randrange(1, 6), rng.randrange(1, 7)
+        pitch = (S + 15) // 16 * 16 + 16 * rng.randrange(0, 4)
+        bstride = nrows * pitch + 16 * rng.randrange(0, 3)
+        g = torch.Generator().manual_seed(S)
+        host = torch.randint(0, 256, (nb * bstride + 64,), dtype=torch.uint8, generator=g)
+        dev = host.to("cuda")
+        h = host.numpy()
+        for fold in (1, 0):
+            out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+            with rsmi.Codec(4, 2) as c:
+                c.set_option("crc16_fold", fold)
+                c.crc16_rows_dev(dev.data_ptr(), pitch, bstride, nrows, S, nb, out.data_ptr(), nrows)
+                torch.cuda.synchronize()
+            got = out.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            for b in range(nb):
+                for r in range(nrows):
+                    row = h[b * bstride + r * pitch:][:S].tobytes()
+                    assert rsmi.crc16_entry(b"", int(got[b, r]), S) == orc.crc16_ibm(row), (S, nrows, nb, fold, b, r)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fold", [1, 0])
 def test_rows_dev_full_size_batch(fold):
     """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows: a checksum of checksums against the
