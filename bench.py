@@ -613,7 +613,7 @@ def main():
             "unit": "GB/s",
             "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
             "traffic": load_traffic(enc_kernel) if headline else None,
-            "kernel": enc_kernel + (" + rs_crc16_combine_kernel" if a.fused_crc else ""),
+            "kernel": enc_kernel + (" + its CRC-16 combine kernel" if a.fused_crc else ""),
             "algorithmic_bytes_per_launch": enc_bytes,
             "avg_launch_ms": round(enc_ms, 4),
             "median_launch_ms": round(enc_t[a.steps // 2], 4),

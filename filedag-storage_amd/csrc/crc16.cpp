@@ -57,6 +57,16 @@ Crc16Tables::Crc16Tables() {
                     if ((c >> n) & 1) MW[t][s][l][e / 8] |= code4[s] << (4 * (e % 8));
                 }
             }
+    const uint32_t fcode4[4] = {4, 2, 1, 4};
+    for (int t = 0; t < 4; t++)
+        for (int s = 0; s < 4; s++)
+            for (int l = 0; l < 64; l++)
+                for (int w = 0; w < 4; w++) {
+                    uint32_t x = MW[4 + t][s][l][w], y = 0;
+                    for (int e = 0; e < 8; e++)
+                        if ((x >> (4 * e)) & 0xF) y |= fcode4[s] << (4 * e);
+                    FW[t][s][l][w] = y;
+                }
     // the group order the negative shifts rely on: A^32767 = I on a basis
     for (int bit = 0; bit < 16; bit++)
         if (shift(uint16_t(1u << bit), kCrcOrder) != uint16_t(1u << bit)) std::abort();

@@ -48,6 +48,12 @@ struct Crc16Tables {
     // codes 2.0 / 1.0 / 0.5 / 0.5 (s = 0..3) against data values 0.5 / 1 / 2 / 2, so every
     // product of a set data bit and a set weight is 1.0
     uint32_t MW[8][4][64][4];
+    // fp4 weight operands of the fused encode + CRC kernel (rs_fused_mfma_kernel): a wave codes a
+    // unit of 4 consecutive tiles of one block, tile t of the unit weighs like MW[4 + t] (relative
+    // to the end of chunk 48 + m of the unit's tile 3), except that bit group 3 arrives as
+    // (x >> 3) & 0x11111111 (bit 3 of each nibble moved to bit 0, data value 0.5, so weight 2.0):
+    // the encode computes x >> 3 for its GF tables anyway
+    uint32_t FW[4][4][64][4];
     Crc16Tables();
     uint16_t pow2(int i, uint16_t s) const { return uint16_t(P[i][0][s & 0xFF] ^ P[i][1][s >> 8]); }
     // A^n(s) for any n >= 0 (reduced mod 32767)

@@ -317,6 +317,223 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     }
 }
 
+typedef int mfma_v8i __attribute__((ext_vector_type(8)));
+typedef float mfma_v4f __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ fused encode + CRC-16, matrix-core fold
+// DagNode.Put's device form (node.go:358-408 with server.go:57-80's checksum of every shard):
+// the encode of rs_fast_kernel (aligned layouts, encode plans: input row c is shard c, output row
+// j shard K + j) with R(shard) of every row it reads and writes folded on the matrix cores
+// instead of the nibble tables of the CRC variants above.  R(chunk) is GF(2)-linear in the
+// chunk's 128 bits, so a tile's fold is a GF(2) matrix product evaluated as exact fp4 counts
+// (v_mfma_scale_f32_16x16x128_f8f6f4, as in rs_crc16_rows_mfma_kernel): B = one data bit per
+// nibble (forms x & 0x11111111, & 0x22.., & 0x44.. and (x >> 3) & 0x11111111 -- the encode
+// computes x >> 3 for its GF tables anyway), A = the weights of the tile's position in its unit
+// (crc16.hpp FW, LDS, loaded once per tile and shared by every row).  Per row and tile: 4
+// bitwise ops per dword and 4 MFMAs, against 15 VALU and 8 LDS lookups per dword for the nibble
+// fold.
+//
+// A wave codes a unit of kFusedUnitTiles = 4 consecutive tiles of one block, and the counts of a
+// row accumulate over the unit's tiles, so the parity is read once per unit.  Two shards share
+// one f32 accumulator: the odd shard's MFMAs run with B scale 2^12, and a unit's counts stay
+// below 2^11 (4 tiles x 4 MFMAs x 128 products), so count0 + 2^12 count1 < 2^24 is exact in f32
+// and the parities are bits 0 and 12 of the integer.  Record of a unit: per accumulator and lane
+// l = 16 j + m, bits 0-3 / 12-15 = parity of element i of the even / odd shard (CRC bit 4 j + i
+// of class m: chunks m, m + 16, m + 32, m + 48 of the unit's tiles, relative to the end of chunk
+// 48 + m of its tile 3); two accumulators per dword, dword d of the unit at lane slot 4 m + j, so
+// a class's four dwords are contiguous for rs_crc16_combine_mfma_kernel.
+template <int K, int MT, int NT, int WPS>
+__global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
+                                                              const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                              uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
+                                                              uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
+                                                              uint32_t upb, uint32_t nunits,
+                                                              const uint32_t* __restrict__ crc_tbl,
+                                                              uint32_t* __restrict__ crc_rec) {
+    static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
+    constexpr int NSH = K + MT;
+    constexpr int NACC = (NSH + 1) / 2;  // two shards per accumulator
+    constexpr int NREC = (NACC + 1) / 2;  // record dwords per lane and unit
+    __shared__ u32x4 s_tbl[K * kColDwords / 4];
+    __shared__ u32x4 s_w[kCrcFWWords / 4];
+    {
+        const uint32_t* src = plan->tbl;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
+        for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+        const u32x4* w = reinterpret_cast<const u32x4*>(crc_tbl + kCrcFWOff);
+        for (int i = threadIdx.x; i < kCrcFWWords / 4; i += kWG) s_w[i] = w[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t u = blockIdx.x * (kWG / kWave) + wid;
+    if (u >= nunits) return;
+    const uint32_t blk = u / upb;
+    const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
+    const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
+    const uint8_t* ib = in + uint64_t(blk) * in_bs;
+    uint8_t* ob = out + uint64_t(blk) * out_bs;
+
+    constexpr int P = rows_in_flight<K, MT>();
+    uint64_t in_off[K], out_off[MT];
+#pragma unroll
+    for (int c = 0; c < K; c++) in_off[c] = uint64_t(plan->in_row[c]) * in_rs;
+#pragma unroll
+    for (int j = 0; j < MT; j++) out_off[j] = uint64_t(plan->out_row[j]) * out_rs;
+
+    mfma_v4f cacc[NACC];
+#pragma unroll
+    for (int a = 0; a < NACC; a++) cacc[a] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+    for (uint32_t i = 0; i < nt; i++) {
+        const uint32_t ch = (t0 + i) * kWave + lane;
+        const uint32_t chl = ch < cpb ? ch : cpb - 1;  // load chunk, clamped: loads stay unconditional
+        // bytes of the lane's chunk that count: those before S (lanes past the row's last chunk,
+        // which loaded a clamped chunk, count nothing); all-ones except in a row's last tile
+        uint32_t mk[4];
+        {
+            const int valid = int(S) - int(ch * 16u);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int nb = valid - 4 * w;
+                mk[w] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+            }
+        }
+        // this tile position's weights, one operand per bit form, shared by every row
+        u32x4 W[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) W[q] = s_w[(i * 4 + q) * kWave + lane];
+        auto crc_row = [&](const u32x4& x, int r) {
+            mfma_v4f& acc = cacc[r / 2];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t msk = q == 1 ? 0x22222222u : q == 2 ? 0x44444444u : 0x11111111u;
+                mfma_v8i bd;
+#pragma unroll
+                for (int w = 0; w < 4; w++)
+                    bd[w] = int(__builtin_amdgcn_bitop3_b32(q < 3 ? x[w] : x[w] >> 3, mk[w], msk, 0x80));  // a & b & c
+                bd[4] = bd[5] = bd[6] = bd[7] = 0;
+                const mfma_v8i aw = {int(W[q][0]), int(W[q][1]), int(W[q][2]), int(W[q][3]), 0, 0, 0, 0};
+                acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bd, acc, 4, 4, 0, 127, 0,
+                                                                       (r & 1) ? 127 + 12 : 127);
+            }
+            // keep the MFMAs here: the accumulators are only read after the tile loop, so without
+            // an anchor the MFMAs sink to the loop's end and every row's bit forms stay live
+            asm volatile("" : "+v"(acc));
+        };
+        auto load_col = [&](int c) { return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl); };
+
+        u32x4 v[P];
+#pragma unroll
+        for (int c = 0; c < P; c++) v[c] = load_col(c);
+        uint32_t acc[MT][4], pend[MT][4];
+        uint32_t tb = 0;
+        asm volatile("" : "+v"(tb));
+        const u32x4* tbl = s_tbl + tb;
+        u32x4 Tn[5];
+#pragma unroll
+        for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            const int slot = c % P;
+            u32x4 T[5];
+#pragma unroll
+            for (int f = 0; f < 5; f++) T[f] = Tn[f];
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t x = u4get(v[slot], w);
+                const uint32_t s1 = x & 0x07070707u;
+                const uint32_t s2 = (x >> 3) & 0x07070707u;
+                const uint32_t s3 = (x >> 6) & 0x03030303u;
+#pragma unroll
+                for (int j = 0; j < MT; j++) {
+                    const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
+                    const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
+                    const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
+                    uint32_t& a = acc[j][w];
+                    uint32_t& q = pend[j][w];
+                    if (c == 0 && K == 1) {
+                        a = xor3(p1, p2, p3);
+                    } else if (c == 0) {
+                        a = p1 ^ p2;
+                        q = p3;
+                    } else if (c & 1) {
+                        a = xor3(a, p1, p2);
+                        a = xor3(a, p3, q);
+                    } else if (c == K - 1) {
+                        a = xor3(a, p1, p2);
+                        a ^= p3;
+                    } else {
+                        a = xor3(a, p1, p2);
+                        q = p3;
+                    }
+                }
+            }
+            crc_row(v[slot], c);
+            if (c + P < K) v[slot] = load_col(c + P);
+            if (c + 1 < K) {
+#pragma unroll
+                for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < MT; j++)
+#pragma unroll
+            for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
+#pragma unroll
+        for (int j = 0; j < MT; j++) crc_row(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j);
+
+        if (ch < cpb) {
+            const uint32_t boff = ch * 16u;
+            if (boff + 16u <= S) {
+#pragma unroll
+                for (int j = 0; j < MT; j++) {
+                    const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                    if constexpr (NT == 1)
+                        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                    else
+                        *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                }
+            } else {
+                // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+#pragma unroll
+                for (int j = 0; j < MT; j++) {
+                    uint8_t* p = ob + out_off[j] + boff;
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const uint32_t val = acc[j][w];
+                        const uint32_t o = boff + 4u * w;
+                        if (o + 4u <= S) {
+                            *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                        } else if (o < S) {
+                            p[4 * w] = uint8_t(val);
+                            if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                            if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // parities -> the unit's record: bit i / 12 + i of accumulator a = element i's parity of
+    // shard 2 a / 2 a + 1
+    uint32_t y[NACC];
+#pragma unroll
+    for (int a = 0; a < NACC; a++) {
+        y[a] = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) y[a] |= (uint32_t(cacc[a][e]) & 0x1001u) << e;
+    }
+    uint32_t* rec = crc_rec + uint64_t(u) * (NREC * kWave) + (lane & 15u) * 4u + (lane >> 4);
+#pragma unroll
+    for (int d = 0; d < NREC; d++) rec[d * kWave] = y[2 * d] | (2 * d + 1 < NACC ? y[2 * d + 1] << 16 : 0u);
+}
+
+
 // Any K (<= 256), MT <= 4, any alignment: one byte-group of 4 per lane, bytewise memory
 // access.  Correctness path for layouts the fast kernel does not accept.
 __global__ __launch_bounds__(kWG) void rs_generic_kernel(const RsPlanDev* __restrict__ plan, const uint8_t* in,
@@ -659,9 +876,6 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 // over lanes 0..15 (A^(16 * 2^j)) leaves the value relative to the group's end in lane 15, and
 // the shift to the row's end is the nibble pass's.  4 MFMAs and 20 VALU per tile fold what the
 // nibble tables fold with 32 lookups and ~70 VALU.
-typedef int mfma_v8i __attribute__((ext_vector_type(8)));
-typedef float mfma_v4f __attribute__((ext_vector_type(4)));
-
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
@@ -752,6 +966,52 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
 }
 
 void* crc16_rows_mfma_kernel() { return reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel); }
+
+// R(row) from rs_fused_mfma_kernel's unit records: one wave per block (a persistent grid strides
+// over blocks), lanes l = 16 g + m take class m of rows r = g, g + 4, ... in turn.  For each unit
+// h a lane gathers its class's 16-bit value from the class's four record dwords (one 16-byte
+// load) and steps its running value by A^4096 (one unit) before adding it; a 4-level scan over
+// the 16 classes (A^(16 * 2^j)) then leaves the row's value relative to the end of the last unit
+// (upb * 4096 bytes) in lane 15 of the group, and A^e, e = (S - upb * 4096) mod 32767, moves it
+// to the row's end.  out[block * nsh + r] is written once (host memory allowed).
+__global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32_t* __restrict__ tbl,
+                                                                    const uint32_t* __restrict__ rec, uint32_t upb,
+                                                                    uint32_t nrec, uint32_t nsh, uint32_t e,
+                                                                    uint64_t nblocks, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_p4[kCrcP4Words];
+    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = tbl[kCrcP4Off + i];
+    __syncthreads();
+    const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_p4);
+    const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u, g = lane >> 4;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
+    for (uint64_t b = uint64_t(blockIdx.x) * (kWG / kWave) + wid; b < nblocks; b += nw) {
+        const uint32_t* rb = rec + b * upb * nrec * kWave + m * 4u;
+        for (uint32_t r0 = 0; r0 < nsh; r0 += 4) {
+            const uint32_t r = r0 + g;
+            const uint32_t rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row and store nothing
+            const uint32_t a = rr >> 1, d = a >> 1, sh = 16u * (a & 1u) + 12u * (rr & 1u);
+            uint32_t acc = 0;
+            for (uint32_t h = 0; h < upb; h++) {
+                const u32x4 x = *reinterpret_cast<const u32x4*>(rb + (uint64_t(h) * nrec + d) * kWave);
+                const uint32_t v = ((x[0] >> sh) & 15u) | (((x[1] >> sh) & 15u) << 4) | (((x[2] >> sh) & 15u) << 8) |
+                                   (((x[3] >> sh) & 15u) << 12);
+                acc = crc_pow4(sQ, 12, acc) ^ v;  // earlier units move 4 KiB further from the end
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
+                const uint32_t t = __shfl_up(w, 1u << j);
+                if (m >= (1u << j)) acc ^= t;
+            }
+            for (int k = 0; k < kCrcPowers; k++)
+                if ((e >> k) & 1) acc = crc_pow4(sQ, k, acc);
+            if (m == 15 && r < nsh) out[b * nsh + r] = acc;
+        }
+    }
+}
+
+void* crc16_combine_mfma_kernel() { return reinterpret_cast<void*>(&rs_crc16_combine_mfma_kernel); }
 
 // R(row) from the fused encode's tile records (rs_fast_kernel CRC): one wave per block (a
 // persistent grid strides over blocks).  Lane l takes quads i = 64 j + l of the block (quad i =
@@ -858,6 +1118,7 @@ static void fill_km(FastKernelTable& t) {
     t.ua[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true>);
     t.crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, true>);
     t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, true>);
+    t.fused[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd>);
 }
 
 template <int K>

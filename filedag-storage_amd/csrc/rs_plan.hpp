@@ -29,6 +29,7 @@ struct FastKernelTable {
     void* ua[17][kMaxMT + 1];
     void* crc[17][kMaxMT + 1];
     void* ua_crc[17][kMaxMT + 1];
+    void* fused[17][kMaxMT + 1];  // aligned, the CRC-16 folded on the matrix cores (rs_fused_mfma_kernel)
 };
 
 const FastKernelTable& fast_kernels();
@@ -51,7 +52,11 @@ constexpr int kCrcP4Words = 15 * 4 * 16 / 2;     // nibble-sliced powers (rows p
 constexpr int kCrcP4Off = kCrcGOff + kCrcGWords;
 constexpr int kCrcMWWords = 8 * 4 * 64 * 4;       // fp4 weight operands (matrix-core rows pass)
 constexpr int kCrcMWOff = kCrcP4Off + kCrcP4Words;
-constexpr int kCrcTableWords = kCrcMWOff + kCrcMWWords;
+constexpr int kCrcFWWords = 4 * 4 * 64 * 4;       // fp4 weights of the fused encode + CRC kernel
+constexpr int kCrcFWOff = kCrcMWOff + kCrcMWWords;
+constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
+constexpr int kFusedUnitTiles = 4;  // fused encode + CRC on the matrix cores: tiles per wave (one unit)
+constexpr int kFusedWavesPerSimd = 3;  // its register budget: 168 VGPRs + AGPRs (the row accumulators)
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
@@ -71,6 +76,7 @@ struct Crc16Shift {
 void* crc16_rows_kernel(bool aligned);
 void* crc16_rows_mfma_kernel();  // aligned rows, the fold on the matrix cores
 void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
+void* crc16_combine_mfma_kernel();    // records of rs_fused_mfma_kernel
 void* crc32_rows_kernel(bool aligned);
 
 }  // namespace rsmi

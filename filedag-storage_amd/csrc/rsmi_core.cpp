@@ -371,6 +371,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "crc16_fold")) {
         if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
         c->opt_crc16_fold = int(value);
+    } else if (!std::strcmp(key, "crc16_fused_fold")) {
+        if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_fused_fold = int(value);
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;

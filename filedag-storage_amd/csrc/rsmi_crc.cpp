@@ -14,7 +14,8 @@ namespace impl {
 int ensure_crc_tables(rsmi_ctx* c) {
     if (c->d_crc_tbl) return RSMI_OK;
     const Crc16Tables& t = crc16_tables();
-    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) + sizeof(t.G) + sizeof(t.P4) + sizeof(t.MW) ==
+    static_assert(sizeof(t.P) + sizeof(t.N) + sizeof(t.Q) + sizeof(t.G) + sizeof(t.P4) + sizeof(t.MW) +
+                          sizeof(t.FW) ==
                       size_t(kCrcTableWords) * 4,
                   "CRC table layout");
     std::vector<uint16_t> h(size_t(kCrcTableWords) * 2);
@@ -24,6 +25,7 @@ int ensure_crc_tables(rsmi_ctx* c) {
     std::memcpy(h.data() + kCrcGOff * 2, t.G, sizeof(t.G));
     std::memcpy(h.data() + kCrcP4Off * 2, t.P4, sizeof(t.P4));
     std::memcpy(h.data() + kCrcMWOff * 2, t.MW, sizeof(t.MW));
+    std::memcpy(h.data() + kCrcFWOff * 2, t.FW, sizeof(t.FW));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc_tbl), h.size() * 2));
     HIP_TRY(hipMemcpy(c->d_crc_tbl, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -134,15 +136,55 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                     size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
     if (plan.tiles.size() != 1 || plan.tiles[0].K > 16) return RSMI_ERR_INVALID_ARG;
-    const size_t nsh = size_t(plan.tiles[0].K + plan.tiles[0].MT);
+    const DevTile& tile = plan.tiles[0];
+    const size_t nsh = size_t(tile.K + tile.MT);
     const size_t cpb = (S + 15) / 16, tpb = (cpb + kWave - 1) / kWave;
-    const size_t ns2 = ((nsh + 3) / 4 + 1) / 2;
-    const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * nsh * 4;
     int rc;
     if ((rc = ensure_crc_tables(c))) return rc;
-    if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
-                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0;
+                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
+                         in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (size_t(1) << 31);
+    if (aligned && c->opt_fused_fold == 1 && fast_kernels().fused[tile.K][tile.MT]) {
+        // the fold on the matrix cores (rs_fused_mfma_kernel): one unit of 4 tiles per wave, then
+        // the records' combine
+        const size_t upb = (tpb + kFusedUnitTiles - 1) / kFusedUnitTiles;
+        const size_t nrec = ((nsh + 1) / 2 + 1) / 2;
+        const size_t rec_per_block = upb * nrec * kWave;
+        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * rec_per_block * 4))) return rc;
+        uint32_t* rec = reinterpret_cast<uint32_t*>(c->d_chunks);
+        void* fn = fast_kernels().fused[tile.K][tile.MT];
+        const RsPlanDev* pd = tile.dev;
+        uint32_t S32 = uint32_t(S), cpb32 = uint32_t(cpb), tpb32 = uint32_t(tpb), upb32 = uint32_t(upb);
+        const uint32_t* tb = c->d_crc_tbl;
+        uint64_t ibs = in_bs, irs = in_rs, obs = out_bs, ors = out_rs;
+        // launches of at most 2^31 units (32-bit unit index)
+        const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / upb);
+        for (uint64_t b0 = 0; b0 < nblocks; b0 += max_blocks) {
+            const uint64_t nb = std::min<uint64_t>(max_blocks, nblocks - b0);
+            uint32_t nunits = uint32_t(nb * upb);
+            const uint8_t* inb = in + b0 * in_bs;
+            uint8_t* outb = out + b0 * out_bs;
+            uint32_t* rb = rec + b0 * rec_per_block;
+            void* args[] = {&pd, &inb, &outb, &ibs, &irs, &obs, &ors, &S32, &cpb32, &tpb32, &upb32, &nunits, &tb, &rb};
+            const uint32_t wgs = (nunits + kWG / kWave - 1) / (kWG / kWave);
+            HIP_TRY(hipLaunchKernel(fn, dim3(wgs), dim3(kWG), args, 0, st));
+        }
+        uint32_t e = uint32_t(((int64_t(S) - int64_t(upb) * 4096) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
+        uint32_t nrec32 = uint32_t(nrec), nsh32 = uint32_t(nsh);
+        uint64_t nb64 = nblocks;
+        const uint32_t* crec = rec;
+        void* cargs[] = {&tb, &crec, &upb32, &nrec32, &nsh32, &e, &nb64, &raw};
+        const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
+        HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
+        char buf[96];
+        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>", tile.K, tile.MT,
+                      auto_cache_policy(tile.K, tile.MT));
+        c->last_kernel = buf;
+        return hip_status(hipGetLastError());
+    }
+    const size_t ns2 = ((nsh + 3) / 4 + 1) / 2;
+    const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * nsh * 4;
+    if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;
     if (!aligned && S < 16) return RSMI_ERR_INVALID_ARG;
     CrcFuse fz;
     fz.tbl = c->d_crc_tbl;

@@ -341,12 +341,15 @@ def test_coalesced_reconstruct_concurrent_callers():
                                              (2, 1, 16, 9, "split"), (5, 3, 1000, 7, "pitched"),
                                              (6, 6, 5000, 4, "split"), (12, 4, 1, 5, "pitched"),
                                              (1, 1, 33, 5, "split"), (8, 4, 65535, 3, "padded")])
-@pytest.mark.parametrize("opt", [("waves_per_cu", 0), ("waves_per_cu", 1)])
-def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opt):
+@pytest.mark.parametrize("opts", [[("crc16_fused_fold", 1)], [("crc16_fused_fold", 0)],
+                                  [("crc16_fused_fold", 0), ("waves_per_cu", 1)]])
+def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opts):
     """Device-resident encode with the CRC fused into the encode pass: parity and every row's
     R(row) equal the oracle's (k > 16, m > 4, and S < 16 in unaligned layouts take the separate
     CRC pass).  Row padding in pitched layouts holds garbage, which must not reach the CRC.
-    waves_per_cu=1 makes every wave code many tiles and every combine wave many blocks."""
+    crc16_fused_fold 1: aligned layouts fold on the matrix cores (rs_fused_mfma_kernel), 0: the
+    nibble-table variants; waves_per_cu=1 makes every nibble-fold wave code many tiles and every
+    combine wave many blocks."""
     import torch
 
     n = k + m
@@ -358,7 +361,8 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opt):
     raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
     base = d.data_ptr()
     with rsmi.Codec(k, m) as c:
-        c.set_option(*opt)
+        for opt in opts:
+            c.set_option(*opt)
         c.encode_batch_dev_crc(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, raw.data_ptr(),
                                torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
@@ -367,8 +371,11 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opt):
     want = orc.encode_fast(k, m, data)
     assert np.array_equal(got[:, k:, :S], want)
     if k <= 16 and m <= 4 and (S >= 16 or rs % 16 == 0):
-        assert ",CRC" in kern, kern
-        assert (",UA" in kern) == (rs % 16 != 0), kern
+        if rs % 16 == 0 and opts[0][1] == 1:
+            assert kern.startswith("rs_fused_mfma_kernel"), kern
+        else:
+            assert ",CRC" in kern, kern
+            assert (",UA" in kern) == (rs % 16 != 0), kern
     r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     for b in range(nb):
         rows = list(data[b]) + list(want[b])
@@ -415,3 +422,43 @@ def test_reconstruct_verify_survivor_crcs(k, m, S, nb, lost, pinned):
             if pinned:
                 del sh
                 rsmi.lib().rsmi_host_free(ptr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(10, 4), (16, 4), (1, 1), (2, 1), (3, 2), (4, 2), (12, 3), (5, 1)])
+@pytest.mark.parametrize("fill", ["ones", "zeros", "random"])
+def test_fused_mfma_counts_exact(k, m, fill):
+    """rs_fused_mfma_kernel packs two shards into one f32 accumulator (the odd one scaled by
+    2^12) and reads both parities once per 4-tile unit: all-0xFF rows drive every count to its
+    maximum, so any inexact accumulation shows.  Row sizes cross the unit boundary (4 tiles =
+    4 KiB per row), end inside and on a chunk, and leave the last unit 1..4 tiles long."""
+    import torch
+
+    n = k + m
+    for S in (1, 15, 16, 1023, 1024, 4096, 4097, 5000, 16384, 26215):
+        nb = 5
+        rs = rsmi.recommended_pitch(S)
+        if fill == "ones":
+            data = np.full((nb, k, S), 0xFF, dtype=np.uint8)
+        elif fill == "zeros":
+            data = np.zeros((nb, k, S), dtype=np.uint8)
+        else:
+            data = np.random.default_rng(S * 31 + k).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+        host = np.full((nb, n, rs), 0xA5, dtype=np.uint8)  # padding that must not reach the CRC
+        host[:, :k, :S] = data
+        d = torch.from_numpy(host.reshape(-1).copy()).cuda()
+        raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+        with rsmi.Codec(k, m) as c:
+            c.encode_batch_dev_crc(d.data_ptr(), rs, n * rs, d.data_ptr() + k * rs, rs, n * rs, S, nb,
+                                   raw.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert c.last_kernel().startswith("rs_fused_mfma_kernel"), c.last_kernel()
+        got = d.cpu().numpy().reshape(nb, n, rs)
+        want = orc.encode_fast(k, m, data)
+        assert np.array_equal(got[:, k:, :S], want), S
+        assert (got[:, k:, S:] == 0xA5).all(), S  # padding past S never written
+        r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        for b in range(nb):
+            rows = list(data[b]) + list(want[b])
+            for i in range(n):
+                assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (S, b, i)

@@ -68,6 +68,8 @@ def fused_vs_separate():
     raw = torch.empty((nb, n), dtype=torch.int32, device="cuda")
     b = buf.data_ptr()
     c = rsmi.Codec(k, m)
+    cn = rsmi.Codec(k, m)
+    cn.set_option("crc16_fused_fold", 0)  # the nibble-table fused variant, for A/B
     if WPC:
         c.set_option("waves_per_cu", WPC)
     sh = st.cuda_stream
@@ -77,6 +79,8 @@ def fused_vs_separate():
                                                c.crc16_rows_dev(b, p, n * p, n, S, nb, raw.data_ptr(), n, sh)),
         "encode with fused CRC": lambda: c.encode_batch_dev_crc(b, p, n * p, b + k * p, p, n * p, S, nb,
                                                                 raw.data_ptr(), sh),
+        "fused CRC, nibble fold": lambda: cn.encode_batch_dev_crc(b, p, n * p, b + k * p, p, n * p, S, nb,
+                                                                  raw.data_ptr(), sh),
     }
     s2 = torch.cuda.Stream()
 
@@ -94,8 +98,9 @@ def fused_vs_separate():
         e.record(s2)
         st.wait_event(e)
 
-    for parts in (2, 4, 8):
-        V[f"encode || CRC pass, {parts} parts"] = lambda parts=parts: staged(parts)
+    if "fused" not in sys.argv[1:]:
+        for parts in (2, 4, 8):
+            V[f"encode || CRC pass, {parts} parts"] = lambda parts=parts: staged(parts)
     t_end = time.perf_counter() + 0.2
     while time.perf_counter() < t_end:
         for f in V.values():
@@ -115,8 +120,10 @@ def fused_vs_separate():
         print(f"RS(10,4) 256 KiB x {nb}: {name:32s} {med * 1e3:8.1f} us  "
               f"{nb * n * S / med / 1e6:8.1f} GB/s of shard bytes", flush=True)
     c.close()
+    cn.close()
 
 
 if __name__ == "__main__":
     fused_vs_separate()
-    main()
+    if "fused" not in sys.argv[1:]:
+        main()
