@@ -178,6 +178,16 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def finish(world):
+    """Every rank waits for rank 0's CPU leg, then leaves the process group together (a rank
+    that exits while a peer still talks to gloo can abort in the group's destructor)."""
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def gather(obj, world):
     if world == 1:
         return [obj]
@@ -251,9 +261,11 @@ class Layout:
 
 
 # ---------------------------------------------------------------- CPU legs (rank 0 only)
-def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds):
+def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds, world=1):
     """The oracle's SIMD restatement of the reference CPU path (test infrastructure, used here
-    only as the reported baseline) on host cores, over the same blocks the GPU coded."""
+    only as the reported baseline) on host cores, over the same blocks the GPU coded.  Rank 0
+    times it after every rank's GPU legs, at any N (the same run's CPU figure beside each point
+    of the 1..8-GPU curve)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc
 
@@ -294,8 +306,11 @@ def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds):
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} passes x the bench's own {nb} blocks of {B // 1024} KiB RS({k},{m}) {what}, "
-                  f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s",
+                  f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s"
+                  + (f"; rank 0 of {world}, timed after every rank's GPU legs finished" if world > 1 else ""),
         "single_core_value": round(reps1 * nb * B / el1 / 2**30, 3),
+        "host_cpus": os.cpu_count(),
+        "ranks": world,
     }
 
 
@@ -452,11 +467,12 @@ def run_mock(a, world, rank):
     el = max_over_ranks(time.perf_counter() - t0, world)
     per = gather({"rank": rank, "blocks": count}, world)
     if rank == 0:
+        cpu = cpu_baseline(k, m, S, k * S, data, [], True, min(a.cpu_seconds, 0.2), world) if a.cpu_seconds > 0 else None
         emit(json.dumps({"metric": "mock", "mock": True, "value": round(nb * world * k * S * a.steps / el / 2**30, 4),
                           "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(el * 1e3 / a.steps, 4), "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "u8", "data": "mock (CPU stand-in, orchestration test only)",
-                          "config": {"ranks": per}}))
+                          "config": {"ranks": per}, "cpu_baseline": cpu}))
 
 
 def main():
@@ -468,6 +484,7 @@ def main():
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     if a.mock:
         run_mock(a, world, rank)
+        finish(world)
         return 0
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (no CPU fallback)")
@@ -640,16 +657,15 @@ def main():
                      else [int(x) for x in a.group.split(",")])
         out["copy_inclusive"] = copy_inclusive(codec, k, m, S, min(nb, max(1, (1 << 30) // B)), lost, data_only,
                                                world, group)
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+    if rank == 0 and a.cpu_seconds > 0:
+        # every rank's GPU legs are done (gather above), so the host cores are free; at N > 1 the
+        # other ranks exit while rank 0 times the CPU codec on its own share of the job's blocks
         data_host = lay.rows(buf, 0, k).cpu().numpy()  # the bench's own blocks
-        out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds, world)
     if rank == 0:
         emit(json.dumps(out))
     codec.close()
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+    finish(world)
     return 0
 
 

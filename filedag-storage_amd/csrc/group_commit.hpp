@@ -6,7 +6,10 @@
 // queued so far (optionally waiting up to wait_us for the queue to reach cap), runs them as one
 // batch through exec(batch) with the lock released, marks them done and wakes the others.
 // Requests that arrive while a batch runs form the next batch.  A lone caller never waits: its
-// batch is itself.  Req needs a `bool done` member, false on submission.
+// batch is itself.  Req needs a `bool done` member, false on submission, and an `int rc`.  If
+// exec throws (std::bad_alloc from its own vectors), every request of the batch completes with
+// rc = the fail code given at construction and the executor role is released, so no current or
+// later caller waits forever; the exception does not cross the C-ABI.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -21,6 +24,7 @@ namespace rsmi {
 template <class Req>
 class GroupCommit {
 public:
+    explicit GroupCommit(int fail_rc) : fail_rc_(fail_rc) {}
     template <class Exec>
     void submit(Req& req, size_t cap, long wait_us, Exec&& exec) {
         calls_++;
@@ -40,7 +44,11 @@ public:
             std::vector<Req*> batch(pending_.begin(), pending_.begin() + take);
             pending_.erase(pending_.begin(), pending_.begin() + take);
             lk.unlock();
-            exec(batch);
+            try {
+                exec(batch);
+            } catch (...) {
+                for (Req* r : batch) r->rc = fail_rc_;
+            }
             batches_++;
             lk.lock();
             for (Req* r : batch) r->done = true;
@@ -56,6 +64,7 @@ private:
     std::condition_variable cv_;
     std::vector<Req*> pending_;
     bool executing_ = false;
+    const int fail_rc_;
     std::atomic<uint64_t> calls_{0}, batches_{0};
 };
 

@@ -333,15 +333,16 @@ typedef float mfma_v4f __attribute__((ext_vector_type(4)));
 // bitwise ops per dword and 4 MFMAs, against 15 VALU and 8 LDS lookups per dword for the nibble
 // fold.
 //
-// A wave codes a unit of kFusedUnitTiles = 4 consecutive tiles of one block, and the counts of a
-// row accumulate over the unit's tiles, so the parity is read once per unit.  Two shards share
+// A unit is kFusedUnitTiles = 4 consecutive tiles of one block, coded by the 4 waves of one
+// workgroup (one tile each, RSMI_FUSED_COOP) or by one wave, and the counts of a row accumulate
+// over the unit's tiles, so the parity is read once per unit.  Two shards share
 // one f32 accumulator: the odd shard's MFMAs run with B scale 2^12, and a unit's counts stay
 // below 2^11 (4 tiles x 4 MFMAs x 128 products), so count0 + 2^12 count1 < 2^24 is exact in f32
 // and the parities are bits 0 and 12 of the integer.  Record of a unit: per accumulator and lane
-// l = 16 j + m, bits 0-3 / 12-15 = parity of element i of the even / odd shard (CRC bit 4 j + i
-// of class m: chunks m, m + 16, m + 32, m + 48 of the unit's tiles, relative to the end of chunk
-// 48 + m of its tile 3); two accumulators per dword, dword d of the unit at lane slot 4 m + j, so
-// a class's four dwords are contiguous for rs_crc16_combine_mfma_kernel.
+// l = 16 j + m, a byte whose bits 0-3 / 4-7 = parity of element i of the even / odd shard (CRC
+// bit 4 j + i of class m: chunks m, m + 16, m + 32, m + 48 of the unit's tiles, relative to the
+// end of chunk 48 + m of its last tile); four accumulators per dword, dword d of the unit at lane
+// slot 4 m + j, so a class's four dwords are contiguous for rs_crc16_combine_mfma_kernel.
 template <int K, int MT, int NT, int WPS>
 __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
                                                               const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
@@ -349,25 +350,34 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                                                               uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                               uint32_t upb, uint32_t nunits,
                                                               const uint32_t* __restrict__ crc_tbl,
-                                                              uint32_t* __restrict__ crc_rec) {
+                                                              uint8_t* __restrict__ crc_rec) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     constexpr int NSH = K + MT;
     constexpr int NACC = (NSH + 1) / 2;  // two shards per accumulator
-    constexpr int NREC = (NACC + 1) / 2;  // record dwords per lane and unit
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
+#ifdef RSMI_FUSED_WSTAGE  // diagnostic: the weights staged in LDS by every workgroup (16 KiB)
     __shared__ u32x4 s_w[kCrcFWWords / 4];
+#endif
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
         for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+#ifdef RSMI_FUSED_WSTAGE
         const u32x4* w = reinterpret_cast<const u32x4*>(crc_tbl + kCrcFWOff);
         for (int i = threadIdx.x; i < kCrcFWWords / 4; i += kWG) s_w[i] = w[i];
+#endif
     }
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+#if RSMI_FUSED_COOP
+    // a workgroup codes a unit, wave w its tile w: every wave codes one tile, as in the plain
+    // encode, and the waves' counts meet in LDS at the end (below)
+    const uint32_t u = blockIdx.x;
+#else
     const uint32_t u = blockIdx.x * (kWG / kWave) + wid;
+#endif
     if (u >= nunits) return;
     const uint32_t blk = u / upb;
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
@@ -375,7 +385,11 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint8_t* ib = in + uint64_t(blk) * in_bs;
     uint8_t* ob = out + uint64_t(blk) * out_bs;
 
+#ifdef RSMI_FUSED_RING  // diagnostic: rows in flight
+    constexpr int P = K < RSMI_FUSED_RING ? K : RSMI_FUSED_RING;
+#else
     constexpr int P = rows_in_flight<K, MT>();
+#endif
     uint64_t in_off[K], out_off[MT];
 #pragma unroll
     for (int c = 0; c < K; c++) in_off[c] = uint64_t(plan->in_row[c]) * in_rs;
@@ -386,14 +400,19 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #pragma unroll
     for (int a = 0; a < NACC; a++) cacc[a] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
 
+#if RSMI_FUSED_COOP
+    static_assert(kFusedUnitTiles == kWG / kWave, "one tile per wave of the unit's workgroup");
+    for (uint32_t i = wid; i < nt; i += kWG / kWave) {
+#else
 #pragma unroll 1
     for (uint32_t i = 0; i < nt; i++) {
+#endif
         const uint32_t ch = (t0 + i) * kWave + lane;
         const uint32_t chl = ch < cpb ? ch : cpb - 1;  // load chunk, clamped: loads stay unconditional
         // bytes of the lane's chunk that count: those before S (lanes past the row's last chunk,
         // which loaded a clamped chunk, count nothing); all-ones except in a row's last tile
-        uint32_t mk[4];
-        {
+        uint32_t mk[4] = {~0u, ~0u, ~0u, ~0u};
+        if ((t0 + i + 1) * uint32_t(kWave * 16) > S) {  // wave-uniform: the row's last tile
             const int valid = int(S) - int(ch * 16u);
 #pragma unroll
             for (int w = 0; w < 4; w++) {
@@ -402,27 +421,50 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             }
         }
         // this tile position's weights, one operand per bit form, shared by every row
+        // (from global memory: the 16 KiB table stays in the L2, and a workgroup that staged it
+        // in LDS first would hold its waves' HBM loads back by the staging's latency)
+#ifdef RSMI_FUSED_WSTAGE
+        const u32x4* wt = s_w + (4 - kFusedUnitTiles + i) * 4 * kWave + lane;
+#else
+        const u32x4* wt = reinterpret_cast<const u32x4*>(crc_tbl + kCrcFWOff) + (4 - kFusedUnitTiles + i) * 4 * kWave + lane;
+#endif
+#ifndef RSMI_FUSED_WLDS
         u32x4 W[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) W[q] = s_w[(i * 4 + q) * kWave + lane];
-        auto crc_row = [&](const u32x4& x, int r) {
+        for (int q = 0; q < 4; q++) W[q] = wt[q * kWave];
+#endif
+        // one MFMA: bit form q of row r's chunk x into the row's accumulator
+        auto crc_mfma = [&](const u32x4& x, int r, int q) {
             mfma_v4f& acc = cacc[r / 2];
+#if defined(RSMI_FUSED_DIAG) && RSMI_FUSED_DIAG == 3  // diagnostic: no CRC work at all
+            return;
+#endif
+#if defined(RSMI_FUSED_DIAG) && RSMI_FUSED_DIAG == 1  // diagnostic: the output rows' CRC skipped
+            if (r >= K) return;
+#endif
+            const uint32_t msk = q == 1 ? 0x22222222u : q == 2 ? 0x44444444u : 0x11111111u;
+            mfma_v8i bd;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t msk = q == 1 ? 0x22222222u : q == 2 ? 0x44444444u : 0x11111111u;
-                mfma_v8i bd;
-#pragma unroll
-                for (int w = 0; w < 4; w++)
-                    bd[w] = int(__builtin_amdgcn_bitop3_b32(q < 3 ? x[w] : x[w] >> 3, mk[w], msk, 0x80));  // a & b & c
-                bd[4] = bd[5] = bd[6] = bd[7] = 0;
-                const mfma_v8i aw = {int(W[q][0]), int(W[q][1]), int(W[q][2]), int(W[q][3]), 0, 0, 0, 0};
-                acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bd, acc, 4, 4, 0, 127, 0,
-                                                                       (r & 1) ? 127 + 12 : 127);
-            }
-            // keep the MFMAs here: the accumulators are only read after the tile loop, so without
-            // an anchor the MFMAs sink to the loop's end and every row's bit forms stay live
-            asm volatile("" : "+v"(acc));
+            for (int w = 0; w < 4; w++)
+                bd[w] = int(__builtin_amdgcn_bitop3_b32(q < 3 ? x[w] : x[w] >> 3, mk[w], msk, 0x80));  // a & b & c
+            bd[4] = bd[5] = bd[6] = bd[7] = 0;
+#if defined(RSMI_FUSED_DIAG) && RSMI_FUSED_DIAG == 2  // diagnostic: the bit forms without the MFMAs
+            acc[0] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, acc[0]) ^ uint32_t(bd[0] ^ bd[1] ^ bd[2] ^ bd[3]));
+            return;
+#endif
+#ifdef RSMI_FUSED_WLDS  // diagnostic: the weights read from LDS for every MFMA instead of held per tile
+            const u32x4 Wq = wt[q * kWave];
+#else
+            const u32x4 Wq = W[q];
+#endif
+            const mfma_v8i aw = {int(Wq[0]), int(Wq[1]), int(Wq[2]), int(Wq[3]), 0, 0, 0, 0};
+            acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bd, acc, 4, 4, 0, 127, 0,
+                                                                   (r & 1) ? 127 + 12 : 127);
         };
+        // keep the MFMAs where they are issued: the accumulators are only read after the tile
+        // loop, so without an anchor the MFMAs sink to the loop's end and every row's bit forms
+        // stay live
+        auto anchor = [&](int r) { asm volatile("" : "+v"(cacc[r / 2])); };
         auto load_col = [&](int c) { return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl); };
 
         u32x4 v[P];
@@ -470,8 +512,18 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                         q = p3;
                     }
                 }
+#ifndef RSMI_FUSED_NOIL
+                // form w's MFMA between the GF work of dword w and w + 1: its latency (and the
+                // chain of the row's four MFMAs) hides under this wave's own VALU stream
+                crc_mfma(v[slot], c, w);
+                __builtin_amdgcn_sched_barrier(0);
+#endif
             }
-            crc_row(v[slot], c);
+#ifdef RSMI_FUSED_NOIL  // diagnostic: the row's four MFMAs back to back after its GF work
+#pragma unroll
+            for (int q = 0; q < 4; q++) crc_mfma(v[slot], c, q);
+#endif
+            anchor(c);
             if (c + P < K) v[slot] = load_col(c + P);
             if (c + 1 < K) {
 #pragma unroll
@@ -483,8 +535,16 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         for (int j = 0; j < MT; j++)
 #pragma unroll
             for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
+        // the output rows: bit form by bit form, even rows before odd ones, so consecutive MFMAs
+        // go to different accumulators wherever two output rows do not share one
 #pragma unroll
-        for (int j = 0; j < MT; j++) crc_row(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j);
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int j = h; j < MT; j += 2) crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
+#pragma unroll
+        for (int j = 0; j < MT; j++) anchor(K + j);
 
         if (ch < cpb) {
             const uint32_t boff = ch * 16u;
@@ -519,18 +579,27 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         }
     }
 
-    // parities -> the unit's record: bit i / 12 + i of accumulator a = element i's parity of
-    // shard 2 a / 2 a + 1
-    uint32_t y[NACC];
+    // parities -> the unit's record: byte (accumulator a, lane slot), bits i / 4 + i = element i's
+    // parity of shard 2 a / 2 a + 1 (bits 0 and 12 of the exact count)
+    auto record = [&](int a, const mfma_v4f& c) {
+        uint32_t y = 0;
 #pragma unroll
-    for (int a = 0; a < NACC; a++) {
-        y[a] = 0;
+        for (int e = 0; e < 4; e++) y |= (uint32_t(c[e]) & 0x1001u) << e;
+        crc_rec[(uint64_t(u) * NACC + a) * kWave + (lane & 15u) * 4u + (lane >> 4)] = uint8_t(y | (y >> 8));
+    };
+#if RSMI_FUSED_COOP
+    // the unit's four tiles meet in LDS (count sums stay below 2^24: exact), and wave w reads out
+    // accumulators w, w + 4, ..., so no wave is left with the whole unit's tail
+    __shared__ mfma_v4f s_red[kWG / kWave][NACC][kWave];
 #pragma unroll
-        for (int e = 0; e < 4; e++) y[a] |= (uint32_t(cacc[a][e]) & 0x1001u) << e;
-    }
-    uint32_t* rec = crc_rec + uint64_t(u) * (NREC * kWave) + (lane & 15u) * 4u + (lane >> 4);
+    for (int a = 0; a < NACC; a++) s_red[wid][a][lane] = cacc[a];
+    __syncthreads();
+    for (int a = int(wid); a < NACC; a += kWG / kWave)
+        record(a, s_red[0][a][lane] + s_red[1][a][lane] + s_red[2][a][lane] + s_red[3][a][lane]);
+#else
 #pragma unroll
-    for (int d = 0; d < NREC; d++) rec[d * kWave] = y[2 * d] | (2 * d + 1 < NACC ? y[2 * d + 1] << 16 : 0u);
+    for (int a = 0; a < NACC; a++) record(a, cacc[a]);
+#endif
 }
 
 
@@ -876,6 +945,14 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 // over lanes 0..15 (A^(16 * 2^j)) leaves the value relative to the group's end in lane 15, and
 // the shift to the row's end is the nibble pass's.  4 MFMAs and 20 VALU per tile fold what the
 // nibble tables fold with 32 lookups and ~70 VALU.
+//
+// UA: rows at any byte alignment (the Split layout: rows back to back at pitch S).  The loads
+// stay 16-byte aligned: lane l loads the aligned chunk holding row byte 16 ch (ch = the lane's
+// chunk), takes its neighbour's aligned chunk by DPP (wave_shl:1; lane 63 loads its own), and
+// funnel-shifts the pair by the row's misalignment (v_alignbyte_b32, wave-uniform), so the fold
+// sees the row's chunk exactly as on an aligned row.  Loads are clamped to the aligned chunk that
+// holds the row's last byte, so nothing past it is read.
+template <bool UA>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
@@ -900,15 +977,63 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
     for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
         const CrcItem x = crc_item(it, nsup, nrows, tpb);
         const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
+        // UA: the row's misalignment (wave-uniform), its aligned base and the aligned chunk that
+        // holds its last byte
+        const uint32_t mis = UA ? uint32_t(__builtin_amdgcn_readfirstlane(int(reinterpret_cast<uintptr_t>(row) & 15u))) : 0u;
+        const uint8_t* rowa = row - mis;
+        const uint64_t lasta = (mis + S - 1) / 16 * 16;
         uint32_t acc = 0;  // lanes 0..15: class m's running value
         for (uint32_t g0 = 0; g0 < x.nt; g0 += kCrcSegTiles) {
             const uint32_t t0 = x.t0 + g0;
             const uint32_t nt = x.nt - g0 < uint32_t(kCrcSegTiles) ? x.nt - g0 : uint32_t(kCrcSegTiles);
             u32x4 v[kCrcSegTiles];
+            if constexpr (!UA) {
 #pragma unroll
-            for (int i = 0; i < kCrcSegTiles; i++) {
-                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
-                v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
+                for (int i = 0; i < kCrcSegTiles; i++) {
+                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
+                }
+            } else {
+                u32x4 nx = {0, 0, 0, 0};
+#pragma unroll
+                for (int i = 0; i < kCrcSegTiles; i++) {
+                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // aligned, unconditional, clamped
+                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < lasta ? off : lasta)));
+                }
+                if (lane == kWave - 1) {  // the aligned chunk after the group's last one
+                    const uint64_t o2 = (uint64_t(t0 + kCrcSegTiles) * kWave) * 16;
+                    nx = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (o2 < lasta ? o2 : lasta)));
+                }
+#pragma unroll
+                for (int i = 0; i < kCrcSegTiles; i++) {
+                    // the next lane's aligned chunk (wave_shl:1); lane 63's is lane 0's of the next
+                    // tile (still unshifted), or the extra load after the group
+                    u32x4 hi;
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const uint32_t t = uint32_t(__builtin_amdgcn_update_dpp(0, int(v[i][w]), 0x130, 0xF, 0xF, false));
+                        const uint32_t n0 = i + 1 < kCrcSegTiles ? uint32_t(__builtin_amdgcn_readlane(int(v[i + 1][w]), 0)) : nx[w];
+                        hi[w] = lane == kWave - 1 ? n0 : t;
+                    }
+                    const uint32_t D[8] = {v[i][0], v[i][1], v[i][2], v[i][3], hi[0], hi[1], hi[2], hi[3]};
+                    const uint32_t q = mis >> 2, r = mis & 3u;
+                    u32x4 o;
+                    switch (q) {  // wave-uniform
+                        case 0:
+                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 1], D[w], r);
+                            break;
+                        case 1:
+                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 2], D[w + 1], r);
+                            break;
+                        case 2:
+                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 3], D[w + 2], r);
+                            break;
+                        default:
+                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 4], D[w + 3], r);
+                            break;
+                    }
+                    v[i] = o;
+                }
             }
             mfma_v4f c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -965,18 +1090,23 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
     }
 }
 
-void* crc16_rows_mfma_kernel() { return reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel); }
+void* crc16_rows_mfma_kernel(bool aligned) {
+    return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel<false>)
+                   : reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel<true>);
+}
 
-// R(row) from rs_fused_mfma_kernel's unit records: one wave per block (a persistent grid strides
-// over blocks), lanes l = 16 g + m take class m of rows r = g, g + 4, ... in turn.  For each unit
-// h a lane gathers its class's 16-bit value from the class's four record dwords (one 16-byte
-// load) and steps its running value by A^4096 (one unit) before adding it; a 4-level scan over
-// the 16 classes (A^(16 * 2^j)) then leaves the row's value relative to the end of the last unit
-// (upb * 4096 bytes) in lane 15 of the group, and A^e, e = (S - upb * 4096) mod 32767, moves it
-// to the row's end.  out[block * nsh + r] is written once (host memory allowed).
+// R(row) from rs_fused_mfma_kernel's unit records: a persistent grid whose waves take items
+// (block b, row group p) in turn, lane l = 16 g + m class m of row 4 p + g (the workgroup stages
+// the power tables once).  For each unit h
+// a lane gathers its class's 16-bit value from the class's four record dwords (one 16-byte load;
+// the loads of 8 units are issued before their power steps) and steps its running value by one
+// unit (A^4096 for 4-tile units) before adding it; a 4-level scan over the 16 classes (A^(16 * 2^j)) then leaves the
+// row's value relative to the end of the last unit (upb units of 1 KiB tiles) in lane 15 of the
+// group, and A^e, e = (S - that end) mod 32767 (column form, by value), moves it to the row's end.
+// out[block * nsh + r] is written once (host memory allowed).
 __global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32_t* __restrict__ tbl,
-                                                                    const uint32_t* __restrict__ rec, uint32_t upb,
-                                                                    uint32_t nrec, uint32_t nsh, uint32_t e,
+                                                                    const uint8_t* __restrict__ rec, uint32_t upb,
+                                                                    uint32_t nacc, uint32_t nsh, Crc16Shift sh,
                                                                     uint64_t nblocks, uint32_t* __restrict__ out) {
     __shared__ uint32_t s_p4[kCrcP4Words];
     for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = tbl[kCrcP4Off + i];
@@ -984,19 +1114,31 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32
     const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_p4);
     const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u, g = lane >> 4;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    for (uint64_t b = uint64_t(blockIdx.x) * (kWG / kWave) + wid; b < nblocks; b += nw) {
-        const uint32_t* rb = rec + b * upb * nrec * kWave + m * 4u;
-        for (uint32_t r0 = 0; r0 < nsh; r0 += 4) {
-            const uint32_t r = r0 + g;
-            const uint32_t rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row and store nothing
-            const uint32_t a = rr >> 1, d = a >> 1, sh = 16u * (a & 1u) + 12u * (rr & 1u);
+    const uint32_t npass = (nsh + 3) / 4;  // wave-uniform
+    const uint64_t nitems = nblocks * npass, nw = uint64_t(gridDim.x) * (kWG / kWave);
+    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
+        const uint64_t b = it / npass;
+        const uint32_t p = uint32_t(it - b * npass);
+        {
+            const uint32_t r = g + 4u * p, rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row, store nothing
+            const uint32_t sp = 4u * (rr & 1u);
+            // the class's four bytes (j = 0..3) of accumulator rr / 2 in unit h
+            const uint8_t* rb = rec + (b * upb * nacc + (rr >> 1)) * kWave + m * 4u;
             uint32_t acc = 0;
-            for (uint32_t h = 0; h < upb; h++) {
-                const u32x4 x = *reinterpret_cast<const u32x4*>(rb + (uint64_t(h) * nrec + d) * kWave);
-                const uint32_t v = ((x[0] >> sh) & 15u) | (((x[1] >> sh) & 15u) << 4) | (((x[2] >> sh) & 15u) << 8) |
-                                   (((x[3] >> sh) & 15u) << 12);
-                acc = crc_pow4(sQ, 12, acc) ^ v;  // earlier units move 4 KiB further from the end
+            for (uint32_t h0 = 0; h0 < upb; h0 += 8) {
+                uint32_t x[8];
+#pragma unroll
+                for (int hh = 0; hh < 8; hh++) {
+                    const uint32_t h = h0 + hh < upb ? h0 + hh : upb - 1;
+                    x[hh] = *reinterpret_cast<const uint32_t*>(rb + uint64_t(h) * nacc * kWave);
+                }
+#pragma unroll
+                for (int hh = 0; hh < 8; hh++) {
+                    if (h0 + hh >= upb) break;
+                    const uint32_t y = x[hh] >> sp;
+                    const uint32_t v = (y & 15u) | ((y >> 4) & 0xF0u) | ((y >> 8) & 0xF00u) | ((y >> 12) & 0xF000u);
+                    acc = crc_pow4(sQ, 10 + kFusedUnitLog, acc) ^ v;  // earlier units move one unit further
+                }
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -1004,9 +1146,10 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32
                 const uint32_t t = __shfl_up(w, 1u << j);
                 if (m >= (1u << j)) acc ^= t;
             }
-            for (int k = 0; k < kCrcPowers; k++)
-                if ((e >> k) & 1) acc = crc_pow4(sQ, k, acc);
-            if (m == 15 && r < nsh) out[b * nsh + r] = acc;
+            uint32_t y = 0;  // A^e(acc), column form
+#pragma unroll
+            for (int bit = 0; bit < 16; bit++) y ^= ((acc >> bit) & 1u) ? sh.col[bit] : 0u;
+            if (m == 15 && r < nsh) out[b * nsh + r] = y;
         }
     }
 }

@@ -55,8 +55,21 @@ constexpr int kCrcMWOff = kCrcP4Off + kCrcP4Words;
 constexpr int kCrcFWWords = 4 * 4 * 64 * 4;       // fp4 weights of the fused encode + CRC kernel
 constexpr int kCrcFWOff = kCrcMWOff + kCrcMWWords;
 constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
-constexpr int kFusedUnitTiles = 4;  // fused encode + CRC on the matrix cores: tiles per wave (one unit)
-constexpr int kFusedWavesPerSimd = 3;  // its register budget: 168 VGPRs + AGPRs (the row accumulators)
+#ifndef RSMI_FUSED_UNIT
+#define RSMI_FUSED_UNIT 4
+#endif
+#ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
+#define RSMI_FUSED_COOP 1
+#endif
+// fused encode + CRC on the matrix cores: tiles per wave (one unit), 1, 2 or 4 (the two-shard
+// accumulators stay exact up to 4 tiles)
+constexpr int kFusedUnitTiles = RSMI_FUSED_UNIT;
+constexpr int kFusedUnitLog = kFusedUnitTiles == 4 ? 2 : kFusedUnitTiles == 2 ? 1 : 0;
+static_assert(kFusedUnitTiles == 1 << kFusedUnitLog, "unit of 1, 2 or 4 tiles");
+#ifndef RSMI_FUSED_WPS
+#define RSMI_FUSED_WPS 3
+#endif
+constexpr int kFusedWavesPerSimd = RSMI_FUSED_WPS;  // its register budget: 168 VGPRs (the row accumulators)
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
 // LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
@@ -74,7 +87,7 @@ struct Crc16Shift {
     uint32_t col[16];
 };
 void* crc16_rows_kernel(bool aligned);
-void* crc16_rows_mfma_kernel();  // aligned rows, the fold on the matrix cores
+void* crc16_rows_mfma_kernel(bool aligned);  // the fold on the matrix cores (unaligned rows: funnel-shifted aligned loads)
 void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
 void* crc16_combine_mfma_kernel();    // records of rs_fused_mfma_kernel
 void* crc32_rows_kernel(bool aligned);

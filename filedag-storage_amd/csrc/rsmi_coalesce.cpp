@@ -17,7 +17,7 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
     if (c->h_coal) (void)hipHostFree(c->h_coal);
     c->h_coal = nullptr;
     c->h_coal_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_coal), need, hipHostMallocDefault) != hipSuccess) {
+    if (pinned_alloc(reinterpret_cast<void**>(&c->h_coal), need) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }

@@ -10,6 +10,21 @@ using namespace rsmi::impl;
 namespace rsmi {
 namespace impl {
 
+// Page-locked host memory for the caller (rsmi_host_alloc) and for every context's staging:
+// portable (mapped for every device, so a device group's members read and write one caller
+// buffer in place) and placed by the calling thread's NUMA policy (hipHostMallocNumaUser): a
+// device group's member threads run bound to their GPU's NUMA node (rsmi_group.cpp), so their
+// staging lands in that socket's memory; other threads get the default local placement.
+hipError_t pinned_alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable | hipHostMallocNumaUser);
+    if (e != hipSuccess) {  // a runtime without NUMA-user placement: portable only
+        (void)hipGetLastError();
+        e = hipHostMalloc(p, bytes, hipHostMallocPortable);
+    }
+    return e;
+}
+
 int hip_status(hipError_t e) {
     if (e == hipSuccess) return RSMI_OK;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorNoBinaryForGpu ||
@@ -387,7 +402,7 @@ const char* rsmi_last_kernel(const rsmi_ctx* c) { return c ? c->last_kernel.c_st
 
 void* rsmi_host_alloc(size_t bytes) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (pinned_alloc(&p, bytes) != hipSuccess) return nullptr;
     return p;
 }
 

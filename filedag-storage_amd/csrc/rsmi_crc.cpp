@@ -40,7 +40,9 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     if (zero) HIP_TRY(hipMemset2DAsync(out, out_bs * 4, 0, size_t(nrows) * 4, nblocks, stream));
     if (S == 0) return RSMI_OK;  // R(empty) = 0
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = aligned && c->opt_crc16_fold == 1 ? crc16_rows_mfma_kernel() : crc16_rows_kernel(aligned);
+    // the fold on the matrix cores for any layout (unaligned rows: aligned loads funnel-shifted),
+    // option crc16_fold 0: the nibble-table passes
+    void* fn = c->opt_crc16_fold == 1 ? crc16_rows_mfma_kernel(aligned) : crc16_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16;
     uint32_t tpb = uint32_t((S + tile - 1) / tile);
     constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;
@@ -148,10 +150,10 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
         // the fold on the matrix cores (rs_fused_mfma_kernel): one unit of 4 tiles per wave, then
         // the records' combine
         const size_t upb = (tpb + kFusedUnitTiles - 1) / kFusedUnitTiles;
-        const size_t nrec = ((nsh + 1) / 2 + 1) / 2;
-        const size_t rec_per_block = upb * nrec * kWave;
-        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * rec_per_block * 4))) return rc;
-        uint32_t* rec = reinterpret_cast<uint32_t*>(c->d_chunks);
+        const size_t nacc = (nsh + 1) / 2;  // two-shard accumulators: a record byte per lane each
+        const size_t rec_per_block = upb * nacc * kWave;
+        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * rec_per_block))) return rc;
+        uint8_t* rec = c->d_chunks;
         void* fn = fast_kernels().fused[tile.K][tile.MT];
         const RsPlanDev* pd = tile.dev;
         uint32_t S32 = uint32_t(S), cpb32 = uint32_t(cpb), tpb32 = uint32_t(tpb), upb32 = uint32_t(upb);
@@ -164,17 +166,22 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             uint32_t nunits = uint32_t(nb * upb);
             const uint8_t* inb = in + b0 * in_bs;
             uint8_t* outb = out + b0 * out_bs;
-            uint32_t* rb = rec + b0 * rec_per_block;
+            uint8_t* rb = rec + b0 * rec_per_block;
             void* args[] = {&pd, &inb, &outb, &ibs, &irs, &obs, &ors, &S32, &cpb32, &tpb32, &upb32, &nunits, &tb, &rb};
-            const uint32_t wgs = (nunits + kWG / kWave - 1) / (kWG / kWave);
+            const uint32_t wgs = RSMI_FUSED_COOP ? nunits : (nunits + kWG / kWave - 1) / (kWG / kWave);
             HIP_TRY(hipLaunchKernel(fn, dim3(wgs), dim3(kWG), args, 0, st));
         }
-        uint32_t e = uint32_t(((int64_t(S) - int64_t(upb) * 4096) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
-        uint32_t nrec32 = uint32_t(nrec), nsh32 = uint32_t(nsh);
+        const int64_t unit_bytes = int64_t(kFusedUnitTiles) * kWave * 16;
+        const uint64_t e = uint64_t(((int64_t(S) - int64_t(upb) * unit_bytes) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
+        Crc16Shift sh;
+        for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), e);
+        uint32_t nacc32 = uint32_t(nacc), nsh32 = uint32_t(nsh);
         uint64_t nb64 = nblocks;
-        const uint32_t* crec = rec;
-        void* cargs[] = {&tb, &crec, &upb32, &nrec32, &nsh32, &e, &nb64, &raw};
-        const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
+        const uint8_t* crec = rec;
+        void* cargs[] = {&tb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
+        // a persistent grid of up to 8 workgroups per CU, 4 waves each, over (block, 4-row group) items
+        const uint64_t items = nblocks * ((nsh + 3) / 4);
+        const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(c->num_cu) * 8)));
         HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         char buf[96];
         std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>", tile.K, tile.MT,
@@ -260,7 +267,8 @@ int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
                     static_cast<hipStream_t>(stream));
     if (rc) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(d_rows) % 16 == 0 && shard_stride % 16 == 0 && block_stride % 16 == 0;
-    c->last_kernel = aligned && c->opt_crc16_fold == 1 ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel";
+    c->last_kernel = c->opt_crc16_fold == 1 ? (aligned ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel,MFMA,UA")
+                                            : "rs_crc16_rows_kernel";
     return hip_status(hipGetLastError());
 }
 

@@ -67,8 +67,7 @@ uint8_t* small_stage(rsmi_ctx* c, size_t need) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     c->h_small = nullptr;
     c->h_small_cap = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_small), std::max<size_t>(need, 1 << 20), hipHostMallocDefault) !=
-        hipSuccess) {
+    if (pinned_alloc(reinterpret_cast<void**>(&c->h_small), std::max<size_t>(need, 1 << 20)) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
@@ -345,7 +344,7 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
             if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
             c->h_stage = nullptr;
             c->h_stage_cap = 0;
-            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), need, hipHostMallocDefault));
+            HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&c->h_stage), need));
             c->h_stage_cap = need;
         }
     }

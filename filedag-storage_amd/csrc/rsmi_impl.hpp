@@ -116,7 +116,7 @@ struct rsmi_ctx {
         int rc;
         bool done;
     };
-    rsmi::GroupCommit<CoalReq> coal;
+    rsmi::GroupCommit<CoalReq> coal{RSMI_ERR_DEVICE};
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;
 };
@@ -131,6 +131,7 @@ namespace impl {
     } while (0)
 
 int hip_status(hipError_t e);
+hipError_t pinned_alloc(void** p, size_t bytes);
 int ensure_device(rsmi_ctx* c);
 int make_plan(rsmi_ctx* c, const Matrix& coef, const std::vector<int>& in_rows, const std::vector<int>& out_rows,
               std::shared_ptr<Plan>& out);

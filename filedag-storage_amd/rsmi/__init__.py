@@ -114,6 +114,14 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(c_size)]),
         "rsmi_key_slot": (ctypes.c_int, [u8p, c_size]),
         "rsmi_group_member_of_key": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size]),
+        "rsmi_group_member_numa_node": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "rsmi_group_host_alloc": (ctypes.c_void_p, [ctypes.c_void_p, c_size, c_size]),
+        "rsmi_group_host_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_device_numa_node": (ctypes.c_int, [ctypes.c_int]),
+        "rsmi_sysfs_numa_node": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+        "rsmi_sysfs_node_cpus": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.c_int]),
+        "rsmi_bind_thread_to_numa_node": (ctypes.c_int, [ctypes.c_int]),
         "rsmi_group_encode_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size]),
         "rsmi_group_encode_batch_host_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, c_size, c_size, c_size,
                                                            ctypes.c_void_p, ctypes.c_void_p]),
@@ -372,6 +380,19 @@ class DeviceGroup:
         b = bytearray(key)
         return lib().rsmi_group_member_of_key(self._h, ctypes.addressof(_buf(b)) if b else None, len(b))
 
+    def member_numa_node(self, i: int) -> int:
+        return lib().rsmi_group_member_numa_node(self._h, i)
+
+    def host_alloc(self, block_bytes: int, nblocks: int) -> int:
+        """Page-locked buffer whose member block ranges sit on the members' NUMA nodes."""
+        p = lib().rsmi_group_host_alloc(self._h, block_bytes, nblocks)
+        if not p:
+            raise RsmiError(ErrDevice, "rsmi_group_host_alloc failed")
+        return p
+
+    def host_free(self, p: int) -> None:
+        lib().rsmi_group_host_free(self._h, p)
+
     def encode_batch_host_ptr(self, data_ptr: int, data_bs: int, parity_ptr: int, parity_bs: int, S: int,
                               nblocks: int) -> None:
         _check(lib().rsmi_group_encode_batch_host(self._h, data_ptr, data_bs, parity_ptr, parity_bs, S, nblocks))
@@ -393,6 +414,25 @@ class DeviceGroup:
         q = bytearray(1 if x else 0 for x in required)
         _check(lib().rsmi_group_reconstruct_rows_batch_host(self._h, ptr, bs, S, nblocks, ctypes.addressof(_buf(p)),
                                                           ctypes.addressof(_buf(q))))
+
+
+def device_numa_node(device: int) -> int:
+    return lib().rsmi_device_numa_node(device)
+
+
+def sysfs_numa_node(sysfs_root: str, pci_bus_id: str) -> int:
+    return lib().rsmi_sysfs_numa_node(sysfs_root.encode(), pci_bus_id.encode())
+
+
+def sysfs_node_cpus(sysfs_root: str, node: int) -> Optional[list]:
+    """CPU ids of a NUMA node from <sysfs_root>/devices/system/node/node<N>/cpulist (None if absent)."""
+    L = lib()
+    n = L.rsmi_sysfs_node_cpus(sysfs_root.encode(), node, None, 0)
+    if n < 0:
+        return None
+    arr = (ctypes.c_int * max(n, 1))()
+    L.rsmi_sysfs_node_cpus(sysfs_root.encode(), node, arr, n)
+    return list(arr[:n])
 
 
 def partition(nblocks: int, parts: int, i: int):

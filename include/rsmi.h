@@ -26,7 +26,10 @@
 extern "C" {
 #endif
 
-#define RSMI_ABI_VERSION 1
+/* 2: rsmi_set_option lost the keys of kernel variants measured slower than the defaults (they
+ * return RSMI_ERR_INVALID_ARG); device groups, NUMA placement, the key slot hash and
+ * rsmi_reconstruct_batch_host_verify were added; "crc16_fused_fold" is new. */
+#define RSMI_ABI_VERSION 2
 
 typedef struct rsmi_ctx rsmi_ctx;
 
@@ -116,6 +119,8 @@ int rsmi_reconstruct_batch_host(rsmi_ctx* ctx, uint8_t* shards, size_t block_str
 int rsmi_reconstruct_rows_batch_host(rsmi_ctx* ctx, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
                                      const uint8_t* present, const uint8_t* required);
 
+/* Page-locked host memory: portable (mapped for every device, so device-group members read and
+ * write one buffer in place) and placed by the calling thread's NUMA memory policy. */
 void* rsmi_host_alloc(size_t bytes);
 void rsmi_host_free(void* p);
 
@@ -275,7 +280,10 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* ctx, uint8_t* shards, size_t
  * into contiguous ranges, one per member, sizes differing by at most one block (rsmi_partition),
  * and run every range on its member's context from its own host thread -- no data crosses
  * devices, no collective runs -- then return the first failing member's status in member
- * order.  Same arguments, layouts, results and errors as the single-context calls. */
+ * order.  Same arguments, layouts, results and errors as the single-context calls (nblocks == 0
+ * validates the arguments on member 0 and returns).  Each member's thread is persistent and
+ * bound to its GPU's NUMA node (CPUs and preferred memory), so the page-locked staging its
+ * context allocates sits on that socket; one batch call runs at a time per group. */
 typedef struct rsmi_group rsmi_group;
 int rsmi_group_open(int k, int m, const int* devices, int ndev, rsmi_group** out);
 void rsmi_group_close(rsmi_group* group);
@@ -289,6 +297,26 @@ int rsmi_key_slot(const uint8_t* key, size_t len);
 /* The member that owns a key: contiguous slot ranges of 16384 / size slots per member, as
  * DagNodes own SlotPairs -- a stable key -> GPU map for per-block callers. */
 int rsmi_group_member_of_key(const rsmi_group* group, const uint8_t* key, size_t len);
+/* Member i's NUMA node (rsmi_device_numa_node of its device), -1 if unknown. */
+int rsmi_group_member_numa_node(const rsmi_group* group, int i);
+/* Page-locked (portable, mapped) host memory for nblocks blocks of block_bytes whose member
+ * ranges (rsmi_partition over the group's size) sit on the members' NUMA nodes, so on the
+ * zero-copy path each member's DMA reads and writes only its own socket's memory.  Zeroed.
+ * Freed by rsmi_group_host_free or rsmi_group_close.  NULL on failure. */
+void* rsmi_group_host_alloc(rsmi_group* group, size_t block_bytes, size_t nblocks);
+void rsmi_group_host_free(rsmi_group* group, void* p);
+/* The host NUMA node closest to a device: hipDeviceAttributeHostNumaId, else sysfs
+ * bus/pci/devices/<pci bus id>/numa_node; -1 when unknown. */
+int rsmi_device_numa_node(int device);
+/* Host-only helpers behind it, with the sysfs root injectable ("/sys" in production): the
+ * numa_node of a PCI bus id ("0000:75:00.0", any case; -1 if absent), and a node's CPU list
+ * (devices/system/node/node<N>/cpulist: returns the number of CPUs, writes at most max_cpus;
+ * -1 if absent or malformed). */
+int rsmi_sysfs_numa_node(const char* sysfs_root, const char* pci_bus_id);
+int rsmi_sysfs_node_cpus(const char* sysfs_root, int node, int* cpus, int max_cpus);
+/* Bind the calling thread to a NUMA node: the node's CPUs the process may use, and a
+ * preferred-node memory policy (allocations fall back to other nodes, never fail). */
+int rsmi_bind_thread_to_numa_node(int node);
 int rsmi_group_encode_batch_host(rsmi_group* group, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                size_t parity_block_stride, size_t S, size_t nblocks);
 int rsmi_group_encode_batch_host_crcs(rsmi_group* group, const uint8_t* data, size_t data_block_stride, uint8_t* parity,

@@ -55,8 +55,9 @@ static void coder_setup(coder_t* cd, const uint8_t* coef, int rows, int cols) {
     cd->rows = rows;
     cd->cols = cols;
     memcpy(cd->coef, coef, (size_t)rows * cols);
-    cd->nib = (uint8_t*)aligned_alloc(64, (size_t)rows * cols * 32 + 64);
-    cd->aff = (uint64_t*)aligned_alloc(64, (size_t)rows * cols * 8 + 64);
+    /* C11 aligned_alloc: the size must be a multiple of the alignment */
+    cd->nib = (uint8_t*)aligned_alloc(64, ((size_t)rows * cols * 32 + 127) / 64 * 64);
+    cd->aff = (uint64_t*)aligned_alloc(64, ((size_t)rows * cols * 8 + 127) / 64 * 64);
     for (int i = 0; i < rows * cols; i++) {
         uint8_t a = coef[i];
         for (int v = 0; v < 16; v++) {

@@ -9,11 +9,22 @@
 // device-free entry points (status strings, shard checks, checksum host halves) are the
 // product's own csrc/rsmi_common.cpp.  Outputs are checked against the oracle by the tests as
 // usual; what the sanitizers check is the host code around the calls.
+//
+// FAKE_RSMI_FAST (tools/Makefile bench_dagnode_cpu): the same layer with the multi-threaded SIMD
+// twin of the oracle (oracle/rs_cpu_fast.c, AVX-512 GFNI) and carry-less CRC folding, so the Dag
+// Node mirror runs end to end on a CPU codec -- the reference's own shape (klauspost encode on
+// host cores, erasure.go:37) -- and tools/bench_dagnode can time it beside the GPU build.
+// Batches split their blocks over FAKE_RSMI_THREADS (default OMP_NUM_THREADS, else every core)
+// threads; a single block codes on the calling thread.
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+#ifdef FAKE_RSMI_FAST
+#include "../../filedag-storage_amd/csrc/host/crc_clmul.hpp"
+#endif
 
 #include "../../filedag-storage_amd/csrc/crc16.hpp"
 #include "../../filedag-storage_amd/csrc/crc32.hpp"
@@ -37,19 +48,62 @@ struct Req {
     bool done;
 };
 
+#ifdef FAKE_RSMI_FAST
+uint32_t r16(const uint8_t* p, size_t n) {
+    bool done = false;
+    const uint32_t s = rsmi::host::clmul_crc16(0, p, n, &done);
+    return done ? s : rsmi::crc16_tables().fold(0, p, n);
+}
+uint32_t r32(const uint8_t* p, size_t n) {
+    bool done = false;
+    const uint32_t s = rsmi::host::clmul_crc32(0, p, n, &done);
+    return done ? s : rsmi::crc32_tables().fold(0, p, n);
+}
+int cpu_threads() {
+    for (const char* v : {"FAKE_RSMI_THREADS", "OMP_NUM_THREADS"}) {
+        const char* e = std::getenv(v);
+        if (e && std::atoi(e) > 0) return std::atoi(e);
+    }
+    return int(std::max(1u, std::thread::hardware_concurrency()));
+}
+// f(b0, b1) over [0, nblocks) split into contiguous ranges on up to cpu_threads() threads; the
+// first nonzero status
+template <class F>
+int par_blocks(size_t nblocks, F f) {
+    const size_t T = std::min<size_t>(size_t(cpu_threads()), nblocks);
+    if (T <= 1) return f(size_t(0), nblocks);
+    std::vector<int> rc(T, 0);
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < T; t++) th.emplace_back([&, t] { rc[t] = f(nblocks * t / T, nblocks * (t + 1) / T); });
+    rc[0] = f(0, nblocks / T);
+    for (auto& x : th) x.join();
+    for (int r : rc)
+        if (r) return r;
+    return 0;
+}
+#else
 uint32_t r16(const uint8_t* p, size_t n) { return rsmi::crc16_tables().fold(0, p, n); }
 uint32_t r32(const uint8_t* p, size_t n) { return rsmi::crc32_tables().fold(0, p, n); }
+template <class F>
+int par_blocks(size_t nblocks, F f) {
+    return f(size_t(0), nblocks);
+}
+#endif
 
 }  // namespace
 
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0;
-    rsmi::GroupCommit<Req> coal;
+    rsmi::GroupCommit<Req> coal{RSMI_ERR_DEVICE};
 };
 
 namespace {
 
 int encode_one(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
+#ifdef FAKE_RSMI_FAST
+    return rs_cpu_encode_batch(c->k, c->m, data, size_t(c->k) * S, parity, size_t(c->m) * S, S, 1, 1) ? RSMI_ERR_INVALID_ARG
+                                                                                                      : RSMI_OK;
+#endif
     std::vector<uint8_t> sh(size_t(c->n) * S);
     std::memcpy(sh.data(), data, size_t(c->k) * S);
     if (rs_oracle_encode(c->k, c->m, sh.data(), S)) return RSMI_ERR_INVALID_ARG;
@@ -59,6 +113,18 @@ int encode_one(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
 
 // rebuild the rows flagged in want (and missing) of one block of n rows at p
 int reconstruct_one(rsmi_ctx* c, uint8_t* p, size_t S, const uint8_t* present, const uint8_t* want) {
+#ifdef FAKE_RSMI_FAST
+    // in place when the wanted rows are what ReconstructData / Reconstruct rebuild
+    bool all = true, data = true;
+    for (int i = 0; i < c->n; i++) {
+        all &= bool(want[i]) == !present[i];
+        data &= bool(want[i]) == (!present[i] && i < c->k);
+    }
+    if (all || data)
+        return rs_cpu_reconstruct_batch(c->k, c->m, p, size_t(c->n) * S, S, 1, present, data ? 1 : 0, 1)
+                   ? RSMI_ERR_TOO_FEW_SHARDS
+                   : RSMI_OK;
+#endif
     std::vector<uint8_t> sh(p, p + size_t(c->n) * S);
     if (rs_oracle_reconstruct(c->k, c->m, sh.data(), S, present, 0)) return RSMI_ERR_TOO_FEW_SHARDS;
     for (int i = 0; i < c->n; i++)
@@ -113,17 +179,19 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t dbs, ui
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
-    for (size_t b = 0; b < nblocks; b++) {
-        const int rc = encode_one(c, data + b * dbs, parity + b * pbs, S);
-        if (rc) return rc;
-        for (size_t i = 0; i < n; i++) {
-            const uint8_t* row = i < k ? data + b * dbs + i * S : parity + b * pbs + (i - k) * S;
-            if (raw16) raw16[b * n + i] = r16(row, S);
-            if (raw32) raw32[b * n + i] = r32(row, S);
-        }
-    }
     (void)m;
-    return RSMI_OK;
+    return par_blocks(nblocks, [&](size_t b0, size_t b1) {
+        for (size_t b = b0; b < b1; b++) {
+            const int rc = encode_one(c, data + b * dbs, parity + b * pbs, S);
+            if (rc) return rc;
+            for (size_t i = 0; i < n; i++) {
+                const uint8_t* row = i < k ? data + b * dbs + i * S : parity + b * pbs + (i - k) * S;
+                if (raw16) raw16[b * n + i] = r16(row, S);
+                if (raw32) raw32[b * n + i] = r32(row, S);
+            }
+        }
+        return int(RSMI_OK);
+    });
 }
 
 int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs, size_t S,
@@ -137,16 +205,18 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t b
     if (!c || !shards || !present || !required) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     const size_t n = size_t(c->n);
-    for (size_t b = 0; b < nblocks; b++) {
-        const int rc = reconstruct_one(c, shards + b * bs, S, present, required);
-        if (rc) return rc;
-        for (size_t i = 0; i < n; i++) {
-            const bool rebuilt = !present[i] && required[i];
-            if (raw16) raw16[b * n + i] = rebuilt ? r16(shards + b * bs + i * S, S) : 0;
-            if (raw32) raw32[b * n + i] = rebuilt ? r32(shards + b * bs + i * S, S) : 0;
+    return par_blocks(nblocks, [&](size_t b0, size_t b1) {
+        for (size_t b = b0; b < b1; b++) {
+            const int rc = reconstruct_one(c, shards + b * bs, S, present, required);
+            if (rc) return rc;
+            for (size_t i = 0; i < n; i++) {
+                const bool rebuilt = !present[i] && required[i];
+                if (raw16) raw16[b * n + i] = rebuilt ? r16(shards + b * bs + i * S, S) : 0;
+                if (raw32) raw32[b * n + i] = rebuilt ? r32(shards + b * bs + i * S, S) : 0;
+            }
         }
-    }
-    return RSMI_OK;
+        return int(RSMI_OK);
+    });
 }
 
 int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t bs, size_t S, size_t nblocks,

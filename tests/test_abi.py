@@ -39,11 +39,11 @@ def test_library_exports_every_declared_symbol():
 def test_python_binding_covers_header():
     L = rsmi.lib()
     for s in declared_symbols():
-        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free", "rsmi_group_close"), s
+        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free", "rsmi_group_close", "rsmi_group_host_free"), s
 
 
 def test_abi_version_and_status_strings():
-    assert rsmi.lib().rsmi_abi_version() == 1
+    assert rsmi.lib().rsmi_abi_version() == 2
     for code in (0, 1, 2, 3, 4, 5, 6, 7, 8, 100, 101):
         assert rsmi.status_string(code) not in ("", "unknown status")
 

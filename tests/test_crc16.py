@@ -95,14 +95,13 @@ def _device_rows(nb, nrows, S, pitch, offset, seed):
 @pytest.mark.parametrize("wpc", [0, 1])
 @pytest.mark.parametrize("fold", [1, 0])
 def test_rows_dev_matches_oracle(S, layout, wpc, fold):
-    """Aligned rows take the matrix-core pass (fold 1, the default) or the pipelined nibble pass
-    (fold 0), others the plain nibble one; waves_per_cu=1 makes each wave walk many items (the
-    pipelined pass's two register sets alternate).  Row sizes cover half-group, group (8 KiB) and
-    item (32 KiB) boundaries on both sides."""
+    """Fold 1 (the default) runs the matrix-core pass -- on unaligned rows with aligned loads
+    funnel-shifted by the row's misalignment --, fold 0 the nibble passes (pipelined on aligned
+    rows); waves_per_cu=1 makes each wave walk many items (the pipelined pass's two register sets
+    alternate).  Row sizes cover half-group, group (8 KiB) and item (32 KiB) boundaries on both
+    sides; unaligned rows sit at pitch S + 3 from offset 5, so their misalignments vary."""
     import torch
 
-    if layout == "unaligned" and fold == 0:
-        pytest.skip("unaligned rows have one fold")
     nrows, nb = 3, 5
     if layout == "aligned":
         pitch, off = (S + 15) // 16 * 16 + 16, 0
@@ -123,6 +122,31 @@ def test_rows_dev_matches_oracle(S, layout, wpc, fold):
             row = h[off + b * nrows * pitch + r * pitch:][:S].tobytes()
             assert got[b, r] < 0x10000
             assert rsmi.crc16_entry(b"", int(got[b, r]), S) == orc.crc16_ibm(row), (b, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 15, 16, 17, 1023, 1024, 1040, 8191, 8193, 26215, 104858])
+def test_rows_dev_split_layout_every_misalignment(S):
+    """The Split layout (rows back to back at pitch S) from each of the 16 byte offsets of an
+    aligned base: every row misalignment (0..15) and so every funnel-shift case of the
+    matrix-core pass's unaligned loads, against the oracle."""
+    import torch
+
+    nrows, nb = 4, 3
+    for off in range(16):
+        host, dev = _device_rows(nb, nrows, S, S, off, S * 7 + off)
+        out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+        with rsmi.Codec(4, 2) as c:
+            c.crc16_rows_dev(dev.data_ptr() + off, S, nrows * S, nrows, S, nb, out.data_ptr(), nrows)
+            torch.cuda.synchronize()
+            assert c.last_kernel() == ("rs_crc16_rows_kernel,MFMA" if (off % 16 == 0 and S % 16 == 0) else
+                                       "rs_crc16_rows_kernel,MFMA,UA"), c.last_kernel()
+        got = out.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        h = host.numpy()
+        for b in range(nb):
+            for r in range(nrows):
+                row = h[off + (b * nrows + r) * S:][:S].tobytes()
+                assert rsmi.crc16_entry(b"", int(got[b, r]), S) == orc.crc16_ibm(row), (off, b, r)
 
 
 @pytest.mark.gpu

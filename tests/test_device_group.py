@@ -118,3 +118,93 @@ def test_group_batches_match_oracle(members, k, m, B, nb):
         erased = np.ascontiguousarray(erased.reshape(nb, n * S))
         s.reconstruct_batch_host_ptr(erased.ctypes.data, n * S, S, nb, [i not in lost for i in range(n)], False)
         assert np.array_equal(erased, shards)
+
+
+def _fake_sysfs(root):
+    """A sysfs tree with two GPUs on two sockets (the MI355X node shape) and a device whose
+    firmware reports no node."""
+    import os
+
+    for bus, node in (("0000:05:00.0", "0\n"), ("0000:75:00.0", "1\n"), ("0000:f5:00.0", "-1\n")):
+        d = os.path.join(root, "bus", "pci", "devices", bus)
+        os.makedirs(d)
+        with open(os.path.join(d, "numa_node"), "w") as f:
+            f.write(node)
+    for node, cpus in ((0, "0-3,8-11\n"), (1, "4-7,12-15\n"), (2, "16\n"), (3, "9-5\n")):
+        d = os.path.join(root, "devices", "system", "node", f"node{node}")
+        os.makedirs(d)
+        with open(os.path.join(d, "cpulist"), "w") as f:
+            f.write(cpus)
+    return str(root)
+
+
+def test_sysfs_device_to_numa_map(tmp_path):
+    """rsmi_device_numa_node's sysfs half (bus/pci/devices/<id>/numa_node, the id in any case)
+    and the node CPU lists the member threads bind to, against an injected sysfs root."""
+    root = _fake_sysfs(tmp_path)
+    assert rsmi.sysfs_numa_node(root, "0000:05:00.0") == 0
+    assert rsmi.sysfs_numa_node(root, "0000:75:00.0") == 1
+    assert rsmi.sysfs_numa_node(root, "0000:F5:00.0") == -1  # firmware without affinity
+    assert rsmi.sysfs_numa_node(root, "0000:99:00.0") == -1  # no such device
+    assert rsmi.sysfs_node_cpus(root, 0) == [0, 1, 2, 3, 8, 9, 10, 11]
+    assert rsmi.sysfs_node_cpus(root, 1) == [4, 5, 6, 7, 12, 13, 14, 15]
+    assert rsmi.sysfs_node_cpus(root, 2) == [16]
+    assert rsmi.sysfs_node_cpus(root, 3) is None  # malformed range
+    assert rsmi.sysfs_node_cpus(root, 7) is None  # no such node
+
+
+def test_bind_thread_to_numa_node():
+    """A member thread binds itself to its node: CPUs of the node the process may use, and a
+    preferred-node memory policy.  Run on a thread of its own (the binding is per thread)."""
+    import os
+    import threading
+
+    L = rsmi.lib()
+    assert L.rsmi_bind_thread_to_numa_node(-1) == rsmi.ErrInvalidArg
+    cpus0 = rsmi.sysfs_node_cpus("/sys", 0)
+    if not cpus0:
+        pytest.skip("no NUMA information in this container's sysfs")
+    out = {}
+
+    def run():
+        out["rc"] = L.rsmi_bind_thread_to_numa_node(0)
+        out["aff"] = os.sched_getaffinity(0)
+
+    allowed = os.sched_getaffinity(0)
+    t = threading.Thread(target=run)
+    t.start()
+    t.join()
+    assert out["rc"] == rsmi.OK
+    want = set(cpus0) & allowed
+    assert out["aff"] == (want or allowed)
+    assert os.sched_getaffinity(0) == allowed  # the calling thread is untouched
+
+
+def test_group_zero_blocks_validates_like_member():
+    """nblocks == 0 still validates the arguments: the group returns exactly what
+    member 0's single-context call returns for the same arguments, and every member reports
+    its NUMA node (-1 without a GPU)."""
+    L = rsmi.lib()
+    k, m, S = 4, 2, 1000
+    n = k + m
+    buf = np.zeros(n * S * 2, dtype=np.uint8)
+    none_present = bytearray(n)
+    all_present = bytearray([1] * n)
+    req = bytearray([1] + [0] * (n - 1))
+    with rsmi.DeviceGroup(k, m, [0, 0]) as s:
+        ctx = L.rsmi_group_context(s._h, 0)
+        assert s.member_numa_node(0) == s.member_numa_node(1)
+        assert s.member_numa_node(2) == -1
+        cases = [
+            (lambda h, f: f(h, buf.ctypes.data, n * S, S, 0, (ctypes.c_uint8 * n).from_buffer(none_present), 1),
+             L.rsmi_group_reconstruct_batch_host, L.rsmi_reconstruct_batch_host),
+            (lambda h, f: f(h, buf.ctypes.data, S, S, 0, (ctypes.c_uint8 * n).from_buffer(all_present), 0),
+             L.rsmi_group_reconstruct_batch_host, L.rsmi_reconstruct_batch_host),
+            (lambda h, f: f(h, buf.ctypes.data, n * S, S, 0, (ctypes.c_uint8 * n).from_buffer(none_present),
+                            (ctypes.c_uint8 * n).from_buffer(req)),
+             L.rsmi_group_reconstruct_rows_batch_host, L.rsmi_reconstruct_rows_batch_host),
+            (lambda h, f: f(h, buf.ctypes.data, 1, buf.ctypes.data, m * S, S, 0),
+             L.rsmi_group_encode_batch_host, L.rsmi_encode_batch_host),
+        ]
+        for call, gfn, cfn in cases:
+            assert call(s._h, gfn) == call(ctx, cfn)

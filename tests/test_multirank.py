@@ -82,6 +82,8 @@ def test_bench_spawns_ranks_itself_mock(n):
     assert j["n_gpus"] == n and j["mock"] and j["steps"] == 3
     assert sorted(r["rank"] for r in j["config"]["ranks"]) == list(range(n))
     assert sum(r["blocks"] for r in j["config"]["ranks"]) == 8 * n
+    cb = j["cpu_baseline"]  # rank 0 times the CPU codec at every N, after the ranks' legs
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["ranks"] == n and cb["kind"] == "port"
 
 
 def test_bench_rejects_world_size_mismatch():
@@ -138,7 +140,7 @@ def test_bench_two_ranks_torchrun_on_one_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "5", "--warmup", "1", "--blocks", "256", "--settle-ms", "0",
-           "--sustained-steps", "0", "--share-device"]
+           "--sustained-steps", "0", "--share-device", "--cpu-seconds", "1"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.strip()]
@@ -147,4 +149,24 @@ def test_bench_two_ranks_torchrun_on_one_gpu():
     assert j["n_gpus"] == 2 and j["steps"] == 5 and j["scaling"] == "weak"
     payload = 2 * 256 * 262144 * 5
     assert abs(j["value"] - payload / (j["ms_per_step"] * 5e-3) / 2**30) / j["value"] < 0.01
-    assert j["cpu_baseline"] is None  # only rank 0 at N=1 times the CPU
+    cb = j["cpu_baseline"]  # rank 0 times the CPU codec at N = 2 as well, after both ranks' legs
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["ranks"] == 2 and "rank 0 of 2" in cb["sample"]
+
+
+@pytest.mark.gpu
+def test_bench_gpus_guard_refuses_missing_devices():
+    """`bench.py --gpus N` with no launcher and no --share-device on a box with fewer than N
+    GPUs exits non-zero before it starts any rank (torch.cuda.device_count() does not
+    initialise the GPU): the message names the visible count, stdout stays empty."""
+    import subprocess
+
+    have = torch.cuda.device_count()
+    if have < 1:
+        pytest.skip("needs a GPU box")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(have + 1), "--steps", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode != 0
+    assert f"only {have} GPU(s) visible" in out.stderr, out.stderr[-2000:]
+    assert out.stdout.strip() == ""  # no rank ran, so no JSON line
+    assert "RANK" not in out.stderr and "Traceback" not in out.stderr  # refused in the launcher itself

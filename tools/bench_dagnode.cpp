@@ -6,10 +6,14 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <thread>
 
 #include "../filedag-storage_amd/csrc/host/dagnode.hpp"
+#ifdef FAKE_RSMI_FAST
+#include "../oracle/rs_oracle.h"  // rs_cpu_isa: the CPU codec build (tools/Makefile bench_dagnode_cpu)
+#endif
 
 using namespace rsmi::host;
 using clk = std::chrono::steady_clock;
@@ -142,14 +146,15 @@ int main(int argc, char** argv) {
     d->SetGpuVerifiedReads(false);
     dn[0]->SetOffline(false);
     d->RunRepairTasks();
-    dn[3]->server().Wipe();
+    const int rj = std::min(3, k - 1);  // the repaired node: data shard 3 (RS(2,1): shard 1)
+    dn[size_t(rj)]->server().Wipe();
     t0 = clk::now();
-    d->RepairDataNode(0, 3);
+    d->RepairDataNode(0, rj);
     const double rep1 = secs(t0);
-    dn[3]->server().Wipe();
+    dn[size_t(rj)]->server().Wipe();
     size_t rep = 0;
     t0 = clk::now();
-    d->RepairDataNodeBatched(0, 3, 256, &rep);
+    d->RepairDataNodeBatched(0, rj, 256, &rep);
     const double repb = secs(t0);
     // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
     // entry (cask.go:73-79).  Put / PutMany with the entry CRC-16 from the GPU pass and the
@@ -209,5 +214,14 @@ int main(int argc, char** argv) {
                 gib / putmh, gib / putm32);
     std::printf("CRC-16 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / crc);
     std::printf("CRC-32 alone       %8.2f GiB/s (one core, block bytes, carry-less folding)\n", gib / c32);
+#ifdef FAKE_RSMI_FAST
+    const char* threads = std::getenv("FAKE_RSMI_THREADS") ? std::getenv("FAKE_RSMI_THREADS") : std::getenv("OMP_NUM_THREADS");
+    std::printf("RESULT {\"codec\": \"cpu\", \"isa\": \"%s\", \"threads\": \"%s\", ", rs_cpu_isa(), threads ? threads : "all");
+#else
+    std::printf("RESULT {\"codec\": \"gpu\", ");
+#endif
+    std::printf("\"k\": %d, \"m\": %d, \"B\": %zu, \"N\": %d, \"put\": %.3f, \"putmany\": %.3f, \"put_threads\": %.3f, "
+                "\"get\": %.3f, \"getmany\": %.3f, \"get_threads\": %.3f, \"repair\": %.3f, \"repair_batched\": %.3f}\n",
+                k, m, B, N, gib / put1, gib / putb, gib / putT, gib / get1, gib / getb, gib / getT, gib / rep1, gib / repb);
     return 0;
 }
