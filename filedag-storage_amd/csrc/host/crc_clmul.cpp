@@ -4,6 +4,8 @@
 // constants, whole 16-byte blocks follow one at a time, and the byte table finishes.
 #include "crc_clmul.hpp"
 
+#include <atomic>
+
 #include <immintrin.h>
 
 #include <cstring>
@@ -108,15 +110,23 @@ const Engine& crc32_engine() {
 
 }  // namespace
 
+// Test switch (tests/test_erasure_host.py): force every length onto the callers' table loops,
+// so hosts with VPCLMULQDQ still test the path that CPUs without it take.
+std::atomic<int> g_force_tables{0};
+
 uint32_t clmul_crc16(uint32_t s, const uint8_t* p, size_t n, bool* done) {
-    *done = n >= 256 && cpu_ok();
+    *done = n >= 256 && !g_force_tables.load(std::memory_order_relaxed) && cpu_ok();
     return *done ? fold(crc16_engine(), s, p, n) : s;
 }
 
 uint32_t clmul_crc32(uint32_t s, const uint8_t* p, size_t n, bool* done) {
-    *done = n >= 256 && cpu_ok();
+    *done = n >= 256 && !g_force_tables.load(std::memory_order_relaxed) && cpu_ok();
     return *done ? fold(crc32_engine(), s, p, n) : s;
 }
 
 }  // namespace host
 }  // namespace rsmi
+
+// test-only (not in include/rsmi.h): 1 = the datanode CRCs take the slice-by-8 loops at every
+// length, 0 = carry-less folding from 256 bytes where the CPU has it (the default)
+extern "C" void rsmi_host_crc_force_tables(int on) { rsmi::host::g_force_tables.store(on ? 1 : 0); }

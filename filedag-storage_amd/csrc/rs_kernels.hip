@@ -320,6 +320,11 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 typedef int mfma_v8i __attribute__((ext_vector_type(8)));
 typedef float mfma_v4f __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ uint32_t crc_pow4(const uint16_t* sQ, int i, uint32_t s);
+__device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uint8_t* rec, uint32_t upb, uint32_t nacc,
+                                                   uint32_t nsh, const Crc16Shift& sh, uint32_t* out, uint32_t p,
+                                                   uint32_t lane);
+
 // ------------------------------------------------------------------ fused encode + CRC-16, matrix-core fold
 // DagNode.Put's device form (node.go:358-408 with server.go:57-80's checksum of every shard):
 // the encode of rs_fast_kernel (aligned layouts, encode plans: input row c is shard c, output row
@@ -350,7 +355,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                                                               uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                               uint32_t upb, uint32_t nunits,
                                                               const uint32_t* __restrict__ crc_tbl,
-                                                              uint8_t* __restrict__ crc_rec) {
+                                                              uint8_t* __restrict__ crc_rec, uint32_t* __restrict__ ctr,
+                                                              uint32_t* __restrict__ raw, Crc16Shift sh) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     constexpr int NSH = K + MT;
     constexpr int NACC = (NSH + 1) / 2;  // two shards per accumulator
@@ -596,6 +602,26 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     __syncthreads();
     for (int a = int(wid); a < NACC; a += kWG / kWave)
         record(a, s_red[0][a][lane] + s_red[1][a][lane] + s_red[2][a][lane] + s_red[3][a][lane]);
+#if RSMI_FUSED_INLINE_COMBINE
+    // The block's last unit to finish combines its records into R(row) (no second launch).  Each
+    // workgroup publishes its record (fence, then one atomic increment of the block's counter);
+    // atomicInc wraps the counter back to 0 at the block's last unit, so the counters are ready
+    // for the next launch without a memset.
+    __threadfence();
+    __syncthreads();
+    __shared__ uint32_t s_last;
+    if (threadIdx.x == 0) s_last = atomicInc(ctr + blk, upb - 1) == upb - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    __shared__ uint32_t s_p4[kCrcP4Words];
+    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
+    __syncthreads();
+    const uint8_t* rb = crc_rec + uint64_t(blk) * upb * NACC * kWave;
+    for (uint32_t p = wid; p < uint32_t(NSH + 3) / 4; p += kWG / kWave)
+        crc16_combine_rows(reinterpret_cast<const uint16_t*>(s_p4), rb, upb, NACC, NSH, sh, raw + uint64_t(blk) * NSH,
+                           p, lane);
+#endif
 #else
 #pragma unroll
     for (int a = 0; a < NACC; a++) record(a, cacc[a]);
@@ -1095,6 +1121,49 @@ void* crc16_rows_mfma_kernel(bool aligned) {
                    : reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel<true>);
 }
 
+// R(row) of rows 4 p + g (lane l = 16 g + m: class m) of one block from its unit records
+// (rs_fused_mfma_kernel): for each unit h a lane gathers its class's 16-bit value from the
+// class's four record bytes (one dword load; the loads of 8 units are issued before their power
+// steps) and steps its running value by one unit (A^4096 for 4-tile units) before adding it; a
+// 4-level scan over the 16 classes (A^(16 * 2^j)) then leaves the row's value relative to the end
+// of the last unit in lane 15 of the group, and A^e, e = (S - that end) mod 32767 (column form),
+// moves it to the row's end.  out[r] is written once (host memory allowed).
+__device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uint8_t* rec, uint32_t upb, uint32_t nacc,
+                                                   uint32_t nsh, const Crc16Shift& sh, uint32_t* out, uint32_t p,
+                                                   uint32_t lane) {
+    const uint32_t m = lane & 15u, g = lane >> 4;
+    const uint32_t r = g + 4u * p, rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row, store nothing
+    const uint32_t sp = 4u * (rr & 1u);
+    // the class's four bytes (j = 0..3) of accumulator rr / 2 in unit h
+    const uint8_t* rb = rec + (rr >> 1) * kWave + m * 4u;
+    uint32_t acc = 0;
+    for (uint32_t h0 = 0; h0 < upb; h0 += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int hh = 0; hh < 8; hh++) {
+            const uint32_t h = h0 + hh < upb ? h0 + hh : upb - 1;
+            x[hh] = *reinterpret_cast<const uint32_t*>(rb + uint64_t(h) * nacc * kWave);
+        }
+#pragma unroll
+        for (int hh = 0; hh < 8; hh++) {
+            if (h0 + hh >= upb) break;
+            const uint32_t y = x[hh] >> sp;
+            const uint32_t v = (y & 15u) | ((y >> 4) & 0xF0u) | ((y >> 8) & 0xF00u) | ((y >> 12) & 0xF000u);
+            acc = crc_pow4(sQ, 10 + kFusedUnitLog, acc) ^ v;  // earlier units move one unit further
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
+        const uint32_t t = __shfl_up(w, 1u << j);
+        if (m >= (1u << j)) acc ^= t;
+    }
+    uint32_t y = 0;  // A^e(acc), column form
+#pragma unroll
+    for (int bit = 0; bit < 16; bit++) y ^= ((acc >> bit) & 1u) ? sh.col[bit] : 0u;
+    if (m == 15 && r < nsh) out[r] = y;
+}
+
 // R(row) from rs_fused_mfma_kernel's unit records: a persistent grid whose waves take items
 // (block b, row group p) in turn, lane l = 16 g + m class m of row 4 p + g (the workgroup stages
 // the power tables once).  For each unit h
@@ -1119,38 +1188,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32
     for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
         const uint64_t b = it / npass;
         const uint32_t p = uint32_t(it - b * npass);
-        {
-            const uint32_t r = g + 4u * p, rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row, store nothing
-            const uint32_t sp = 4u * (rr & 1u);
-            // the class's four bytes (j = 0..3) of accumulator rr / 2 in unit h
-            const uint8_t* rb = rec + (b * upb * nacc + (rr >> 1)) * kWave + m * 4u;
-            uint32_t acc = 0;
-            for (uint32_t h0 = 0; h0 < upb; h0 += 8) {
-                uint32_t x[8];
-#pragma unroll
-                for (int hh = 0; hh < 8; hh++) {
-                    const uint32_t h = h0 + hh < upb ? h0 + hh : upb - 1;
-                    x[hh] = *reinterpret_cast<const uint32_t*>(rb + uint64_t(h) * nacc * kWave);
-                }
-#pragma unroll
-                for (int hh = 0; hh < 8; hh++) {
-                    if (h0 + hh >= upb) break;
-                    const uint32_t y = x[hh] >> sp;
-                    const uint32_t v = (y & 15u) | ((y >> 4) & 0xF0u) | ((y >> 8) & 0xF00u) | ((y >> 12) & 0xF000u);
-                    acc = crc_pow4(sQ, 10 + kFusedUnitLog, acc) ^ v;  // earlier units move one unit further
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
-                const uint32_t t = __shfl_up(w, 1u << j);
-                if (m >= (1u << j)) acc ^= t;
-            }
-            uint32_t y = 0;  // A^e(acc), column form
-#pragma unroll
-            for (int bit = 0; bit < 16; bit++) y ^= ((acc >> bit) & 1u) ? sh.col[bit] : 0u;
-            if (m == 15 && r < nsh) out[b * nsh + r] = y;
-        }
+        crc16_combine_rows(sQ, rec + b * upb * nacc * kWave, upb, nacc, nsh, sh, out + b * nsh, p, lane);
     }
 }
 

@@ -61,6 +61,9 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
 #define RSMI_FUSED_COOP 1
 #endif
+#ifndef RSMI_FUSED_INLINE_COMBINE  // 1 (with COOP): each block's last unit combines its records
+#define RSMI_FUSED_INLINE_COMBINE 1
+#endif
 // fused encode + CRC on the matrix cores: tiles per wave (one unit), 1, 2 or 4 (the two-shard
 // accumulators stay exact up to 4 tiles)
 constexpr int kFusedUnitTiles = RSMI_FUSED_UNIT;

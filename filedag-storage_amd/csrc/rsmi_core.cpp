@@ -343,6 +343,7 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
             if (c->d_chunks) (void)hipFree(c->d_chunks);
+            if (c->d_fctr) (void)hipFree(c->d_fctr);
             if (c->d_crc32_tbl) (void)hipFree(c->d_crc32_tbl);
             if (c->d_crc32) (void)hipFree(c->d_crc32);
         }

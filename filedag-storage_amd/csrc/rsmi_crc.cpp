@@ -159,6 +159,22 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
         uint32_t S32 = uint32_t(S), cpb32 = uint32_t(cpb), tpb32 = uint32_t(tpb), upb32 = uint32_t(upb);
         const uint32_t* tb = c->d_crc_tbl;
         uint64_t ibs = in_bs, irs = in_rs, obs = out_bs, ors = out_rs;
+        // A^e moves a row's value from the end of its last unit to the row's end
+        const int64_t unit_bytes = int64_t(kFusedUnitTiles) * kWave * 16;
+        const uint64_t e = uint64_t(((int64_t(S) - int64_t(upb) * unit_bytes) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
+        Crc16Shift sh;
+        for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), e);
+        constexpr bool inline_combine = RSMI_FUSED_COOP && RSMI_FUSED_INLINE_COMBINE;
+        // per-block unit counters of the inline combine: zeroed once when allocated, and every
+        // launch leaves them at zero again (atomicInc wraps at the block's last unit)
+        if (inline_combine && c->fctr_cap < nblocks) {
+            if (c->d_fctr) HIP_TRY(hipFree(c->d_fctr));
+            c->d_fctr = nullptr;
+            c->fctr_cap = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_fctr), nblocks * 4));
+            HIP_TRY(hipMemsetAsync(c->d_fctr, 0, nblocks * 4, st));
+            c->fctr_cap = nblocks;
+        }
         // launches of at most 2^31 units (32-bit unit index)
         const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / upb);
         for (uint64_t b0 = 0; b0 < nblocks; b0 += max_blocks) {
@@ -167,22 +183,23 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             const uint8_t* inb = in + b0 * in_bs;
             uint8_t* outb = out + b0 * out_bs;
             uint8_t* rb = rec + b0 * rec_per_block;
-            void* args[] = {&pd, &inb, &outb, &ibs, &irs, &obs, &ors, &S32, &cpb32, &tpb32, &upb32, &nunits, &tb, &rb};
+            uint32_t* cb = inline_combine ? c->d_fctr + b0 : nullptr;
+            uint32_t* rw = raw + b0 * nsh;
+            void* args[] = {&pd,  &inb,   &outb,   &ibs, &irs, &obs, &ors, &S32, &cpb32,
+                            &tpb32, &upb32, &nunits, &tb,  &rb,  &cb,  &rw,  &sh};
             const uint32_t wgs = RSMI_FUSED_COOP ? nunits : (nunits + kWG / kWave - 1) / (kWG / kWave);
             HIP_TRY(hipLaunchKernel(fn, dim3(wgs), dim3(kWG), args, 0, st));
         }
-        const int64_t unit_bytes = int64_t(kFusedUnitTiles) * kWave * 16;
-        const uint64_t e = uint64_t(((int64_t(S) - int64_t(upb) * unit_bytes) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
-        Crc16Shift sh;
-        for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), e);
-        uint32_t nacc32 = uint32_t(nacc), nsh32 = uint32_t(nsh);
-        uint64_t nb64 = nblocks;
-        const uint8_t* crec = rec;
-        void* cargs[] = {&tb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
-        // a persistent grid of up to 8 workgroups per CU, 4 waves each, over (block, 4-row group) items
-        const uint64_t items = nblocks * ((nsh + 3) / 4);
-        const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(c->num_cu) * 8)));
-        HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
+        if (!inline_combine) {
+            uint32_t nacc32 = uint32_t(nacc), nsh32 = uint32_t(nsh);
+            uint64_t nb64 = nblocks;
+            const uint8_t* crec = rec;
+            void* cargs[] = {&tb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
+            // a persistent grid of up to 8 workgroups per CU, 4 waves each, over (block, 4-row group) items
+            const uint64_t items = nblocks * ((nsh + 3) / 4);
+            const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(c->num_cu) * 8)));
+            HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
+        }
         char buf[96];
         std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>", tile.K, tile.MT,
                       auto_cache_policy(tile.K, tile.MT));

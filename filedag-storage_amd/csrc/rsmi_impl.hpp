@@ -92,6 +92,8 @@ struct rsmi_ctx {
     uint64_t crc32_shift_S = ~uint64_t(0);
     uint8_t* d_chunks = nullptr;    // fused encode + CRC-16: tile records and tails (CrcFuse)
     size_t chunks_cap = 0;
+    uint32_t* d_fctr = nullptr;     // fused encode + CRC-16 on the matrix cores: per-block unit counters
+    size_t fctr_cap = 0;
     // options
     int opt_crc16_fold = 1;     // aligned CRC-16 rows pass: 0 = nibble tables, 1 = matrix cores (fp4)
     int opt_fused_fold = 1;     // aligned fused encode + CRC-16: 0 = nibble tables, 1 = matrix cores (fp4)

@@ -109,10 +109,12 @@ _CLMUL_LENGTHS = [0, 1, 7, 8, 9, 15, 16, 17, 100, 255, 256, 257, 271, 272, 511, 
                   26227, 104858, 262147]
 
 
-def test_datanode_crc_slice_by_8_matches_byte_serial():
+@pytest.mark.parametrize("tables", [0, 1])
+def test_datanode_crc_slice_by_8_matches_byte_serial(tables):
     """The datanode entry CRC (slice-by-8 below 256 bytes, carry-less-multiply folding from 256,
     csrc/host/datanode.cpp + crc_clmul.cpp) equals the byte-serial restatement of
-    howeyc/crc16 Checksum(IBMTable) on every length class, from any register start value."""
+    howeyc/crc16 Checksum(IBMTable) on every length class, from any register start value.
+    tables=1 forces slice-by-8 at every length (the path of CPUs without VPCLMULQDQ)."""
     import ctypes
 
     L = ctypes.CDLL(rsmi.LIB_PATH)
@@ -120,17 +122,22 @@ def test_datanode_crc_slice_by_8_matches_byte_serial():
     f.restype = ctypes.c_uint16
     f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint16]
     rng = np.random.default_rng(5)
-    for n in _CLMUL_LENGTHS:
-        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
-        assert f(b, n, 0) == multi.crc16_ibm(b), n
-        # a continued checksum (the entry's header first, then the shard) equals the whole one
-        h = n // 3
-        assert f(b[h:], n - h, f(b[:h], h, 0)) == multi.crc16_ibm(b), n
+    L.rsmi_host_crc_force_tables(tables)
+    try:
+        for n in _CLMUL_LENGTHS:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            assert f(b, n, 0) == multi.crc16_ibm(b), n
+            # a continued checksum (the entry's header first, then the shard) equals the whole one
+            h = n // 3
+            assert f(b[h:], n - h, f(b[:h], h, 0)) == multi.crc16_ibm(b), n
+    finally:
+        L.rsmi_host_crc_force_tables(0)
 
 
-def test_datanode_value_crc32_matches_zlib():
+@pytest.mark.parametrize("tables", [0, 1])
+def test_datanode_value_crc32_matches_zlib(tables):
     """The mutcask value CRC-32 of the in-process datanode (slice-by-8 / carry-less-multiply
-    folding) equals zlib's crc32 (Go crc32.ChecksumIEEE) on every length class."""
+    folding) equals zlib's crc32 (Go crc32.ChecksumIEEE) on every length class, on both paths."""
     import ctypes
     import zlib
 
@@ -139,6 +146,10 @@ def test_datanode_value_crc32_matches_zlib():
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     rng = np.random.default_rng(6)
-    for n in _CLMUL_LENGTHS:
-        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
-        assert f(b, n) == zlib.crc32(b), n
+    L.rsmi_host_crc_force_tables(tables)
+    try:
+        for n in _CLMUL_LENGTHS:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            assert f(b, n) == zlib.crc32(b), n
+    finally:
+        L.rsmi_host_crc_force_tables(0)

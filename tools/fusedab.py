@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
 import rsmi  # noqa: E402
 
 
-def med(f, st, reps=20):
+def med(f, st, reps=40):
     ts = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
