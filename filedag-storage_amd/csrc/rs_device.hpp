@@ -13,6 +13,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));  // any byte alignment
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));  // dword alignment
 
 __device__ __forceinline__ uint32_t u4get(const u32x4& v, int i) { return v[i]; }
 

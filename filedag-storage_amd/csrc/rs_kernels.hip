@@ -176,13 +176,36 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
                 slot[r / 4] = (lane & 3u) == uint32_t(r & 3) ? cr : slot[r / 4];
             }
         };
+        // UA4 (read-heavy unaligned tiles): the lane's 16-byte window is loaded from the dword
+        // boundary at or below it (a 4-byte-aligned dwordx4 plus the dword after it) and
+        // funnel-shifted by the window's byte offset in that dword (v_alignbyte_b32), instead of
+        // one byte-aligned 16-byte load: +7% on the Split layout's RS(10,4) 1-row reconstruct
+        // (4.78 -> 5.11 TB/s, profiles/r03/ua/ua4_ab.txt).  Every dword loaded holds a byte of the row.
+        constexpr bool UA4 = UA && (RSMI_UA_DWORD_LOADS == 2 || (NT == 2 && RSMI_UA_DWORD_LOADS == 1));
+        uint32_t vx[UA4 ? P : 1];  // UA4: the dword after each row's window
         auto load_col = [&](int c) {
-            if constexpr (UA)
+            if constexpr (UA4) {
+                const uintptr_t a = reinterpret_cast<uintptr_t>(ib + in_off[c] + win) & ~uintptr_t(3);
+                vx[c % P] = *reinterpret_cast<const uint32_t*>(a + 16);
+                return u32x4(*reinterpret_cast<const u32x4a4*>(a));
+            } else if constexpr (UA) {
                 // nontemporal loads for write-heavy tiles; read-heavy UA tiles keep the lines
                 // they share with their neighbours in the L2
                 return ld16u<NT == 1>(ib + in_off[c] + win);
-            else
+            } else {
                 return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl);
+            }
+        };
+        // UA4: row c's window from its two loads
+        auto window = [&](int c, const u32x4& d) -> u32x4 {
+            if constexpr (UA4) {
+                const uint32_t r = uint32_t(reinterpret_cast<uintptr_t>(ib + in_off[c] + win)) & 3u;
+                const uint32_t e = vx[c % P];
+                return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], r), __builtin_amdgcn_alignbyte(d[2], d[1], r),
+                             __builtin_amdgcn_alignbyte(d[3], d[2], r), __builtin_amdgcn_alignbyte(e, d[3], r)};
+            } else {
+                return d;
+            }
         };
 
         // Software pipeline over the K input rows: a ring of P rows in flight, one
@@ -211,6 +234,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             u32x4 T[5];
 #pragma unroll
             for (int f = 0; f < 5; f++) T[f] = Tn[f];
+            if constexpr (UA4) v[slot] = window(c, v[slot]);
 #pragma unroll
             for (int w = 0; w < 4; w++) {
                 const uint32_t x = u4get(v[slot], w);

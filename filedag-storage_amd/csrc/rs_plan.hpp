@@ -10,6 +10,11 @@ constexpr int kMaxK = 256;      // k + m <= 256 (erasure.go:22)
 constexpr int kMaxMT = 4;       // outputs per launch tile
 constexpr int kColDwords = 20;  // per input column: 5 table fields x 4 outputs
 constexpr int kMinWavesPerSimd = 4;  // caps the fast kernels at 128 VGPRs (16 waves/CU)
+// unaligned-window tiles: dword-aligned loads funnel-shifted for read-heavy tiles (1, the
+// default), for every UA tile (2), or byte-aligned 16-byte loads (0)
+#ifndef RSMI_UA_DWORD_LOADS
+#define RSMI_UA_DWORD_LOADS 1
+#endif
 
 // One launch tile: MT (<= 4) output rows computed from K input rows.
 // tbl[c*20 + f*4 + j] = field-f product word for coefficient coef[j][c] (gf256.hpp
@@ -61,8 +66,12 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
 #define RSMI_FUSED_COOP 1
 #endif
-#ifndef RSMI_FUSED_INLINE_COMBINE  // 1 (with COOP): each block's last unit combines its records
-#define RSMI_FUSED_INLINE_COMBINE 1
+// 1 (with COOP, diagnostic): each block's last unit combines its records in the fused kernel.
+// Measured 8.2 ms instead of ~0.33 ms: the agent-scope release each unit needs before its
+// counter increment writes back its XCD's L2 (the 8 XCDs' L2s are not coherent with each
+// other), so the separate combine launch (0, the default) stays.
+#ifndef RSMI_FUSED_INLINE_COMBINE
+#define RSMI_FUSED_INLINE_COMBINE 0
 #endif
 // fused encode + CRC on the matrix cores: tiles per wave (one unit), 1, 2 or 4 (the two-shard
 // accumulators stay exact up to 4 tiles)

@@ -14,4 +14,4 @@ for r in 1 2; do
 import json; j=json.load(open('gpurun_out/uapitch.json'))
 print('$args'.ljust(16), 'pitch', j['config']['row_pitch'], 'encode', j['roofline']['achieved'], 'GB/s', j['roofline']['kernel'], '| reconstruct', j['reconstruct']['achieved_GBs'], 'GB/s', j['reconstruct']['kernel'])"
   done
-done
+done | tee gpurun_out/ua_pitch_ab.txt
