@@ -387,13 +387,19 @@ def copy_inclusive(codec, k, m, S, nb, lost, data_only, world, group=None):
             raise errs[0]
     if group:
         # the same host batch spread over a device group from this one process: contiguous
-        # block ranges, one member context (own streams and staging) and host thread each
+        # block ranges, one member context (own streams and staging) and NUMA-bound worker each,
+        # over buffers whose member ranges sit on the members' NUMA nodes (rsmi_group_host_alloc)
         with rsmi.DeviceGroup(k, m, group) as g:
-            gr = {"devices": list(group)}
-            gr["encode_GiBs"] = round(leg(lambda: g.encode_batch_host_ptr(din, k * S, dpar, m * S, S, nb)), 2)
+            gin, gpar, gsh = g.host_alloc(k * S, nb), g.host_alloc(m * S, nb), g.host_alloc(n * S, nb)
+            ctypes.memmove(gsh, dsh, nb * n * S)
+            ctypes.memmove(gin, din, nb * k * S)
+            gr = {"devices": list(group), "numa_nodes": [g.member_numa_node(i) for i in range(len(group))]}
+            gr["encode_GiBs"] = round(leg(lambda: g.encode_batch_host_ptr(gin, k * S, gpar, m * S, S, nb)), 2)
             if lost:
                 gr["reconstruct_GiBs"] = round(leg(lambda: g.reconstruct_batch_host_ptr(
-                    dsh, n * S, S, nb, present, data_only)), 2)
+                    gsh, n * S, S, nb, present, data_only)), 2)
+            for q in (gin, gpar, gsh):
+                g.host_free(q)
         res["group"] = gr
     for p in (din, dpar, dsh):
         L.rsmi_host_free(p)

@@ -208,3 +208,37 @@ def test_group_zero_blocks_validates_like_member():
         ]
         for call, gfn, cfn in cases:
             assert call(s._h, gfn) == call(ctx, cfn)
+
+
+@pytest.mark.gpu
+def test_group_host_alloc_places_member_ranges():
+    """rsmi_group_host_alloc: one page-locked buffer, zeroed, whose member ranges sit on the
+    members' NUMA nodes (checked page by page with get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR) where
+    the box reports a node), coded in place by the group's zero-copy path against the oracle."""
+    import ctypes.util
+
+    k, m, S, nb = 10, 4, 26215, 16
+    data = np.stack([orc.splitmix64_bytes(0xF11EDA6 ^ b, k * S) for b in range(nb)])
+    want = orc.encode_fast(k, m, data.reshape(nb, k, S))
+    libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+    with rsmi.DeviceGroup(k, m, [0, 0]) as g:
+        node = g.member_numa_node(0)
+        assert node == rsmi.device_numa_node(0)
+        pd = g.host_alloc(k * S, nb)
+        pp = g.host_alloc(m * S, nb)
+        try:
+            d = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * k * S)).from_address(pd))
+            p = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * m * S)).from_address(pp))
+            assert not d.any() and not p.any()
+            d[:] = data.reshape(-1)
+            g.encode_batch_host_ptr(pd, k * S, pp, m * S, S, nb)
+            assert np.array_equal(p.reshape(nb, m, S), want)
+            if node >= 0:
+                mode = ctypes.c_int(-1)
+                for off in range(0, nb * k * S, 1 << 16):  # MPOL_F_NODE | MPOL_F_ADDR: the page's node
+                    rc = libc.syscall(239, ctypes.byref(mode), None, ctypes.c_ulong(0), ctypes.c_void_p(pd + off),
+                                      ctypes.c_ulong(3))
+                    assert rc == 0 and mode.value == node, (off, rc, mode.value, node)
+        finally:
+            g.host_free(pd)
+            g.host_free(pp)

@@ -56,11 +56,10 @@ def main():
             c.close()
 
 
-def fused_vs_separate():
+def fused_vs_separate(k=10, m=4, B=262144, nb=4096):
     """The bench layout: encode then a separate R(row) pass, against the encode with the CRC
     fused (rsmi_encode_batch_dev_crc)."""
     st = torch.cuda.current_stream()
-    k, m, B, nb = 10, 4, 262144, 4096
     n = k + m
     S = (B + k - 1) // k
     p = rsmi.recommended_pitch(S)
@@ -117,7 +116,7 @@ def fused_vs_separate():
             ts[name].append(e0.elapsed_time(e1))
     for name in V:
         med = statistics.median(ts[name])
-        print(f"RS(10,4) 256 KiB x {nb}: {name:32s} {med * 1e3:8.1f} us  "
+        print(f"RS({k},{m}) {B // 1024} KiB x {nb}: {name:32s} {med * 1e3:8.1f} us  "
               f"{nb * n * S / med / 1e6:8.1f} GB/s of shard bytes", flush=True)
     c.close()
     cn.close()
@@ -125,5 +124,6 @@ def fused_vs_separate():
 
 if __name__ == "__main__":
     fused_vs_separate()
+    fused_vs_separate(16, 4, 4 << 20, 256)
     if "fused" not in sys.argv[1:]:
         main()
