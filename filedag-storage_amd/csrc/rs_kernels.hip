@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "crc16.hpp"
 #include "rs_device.hpp"
@@ -372,7 +373,16 @@ __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uin
 // bit 4 j + i of class m: chunks m, m + 16, m + 32, m + 48 of the unit's tiles, relative to the
 // end of chunk 48 + m of its last tile); four accumulators per dword, dword d of the unit at lane
 // slot 4 m + j, so a class's four dwords are contiguous for rs_crc16_combine_mfma_kernel.
-template <int K, int MT, int NT, int WPS>
+//
+// UA: rows at any alignment and pitch (S >= 16; the Split layout), with the unaligned-window
+// loads and stores of rs_fast_kernel's UA form.  The fold needs every lane's bytes at their
+// chunk position: only the lane holding a row's last, overlapping window (it starts at S - 16,
+// not at 16 ch) differs: its window must move right by d = 16 ch - (S - 16) bytes.  The rows go
+// into the fold unshifted, and the row's last tile then adds (window XOR shifted window) of that
+// lane alone (the counts only matter mod 2), for the output rows from registers and for the input
+// rows from a reload, so the common tiles carry none of it.  Workgroups take XCD-contiguous units,
+// as the UA coding kernels do.
+template <int K, int MT, int NT, int WPS, bool UA = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
                                                               const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                               uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -403,8 +413,10 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
 #if RSMI_FUSED_COOP
     // a workgroup codes a unit, wave w its tile w: every wave codes one tile, as in the plain
-    // encode, and the waves' counts meet in LDS at the end (below)
-    const uint32_t u = blockIdx.x;
+    // encode, and the waves' counts meet in LDS at the end (below); UA: each XCD takes one
+    // contiguous eighth of the units (their rows share boundary lines)
+    uint32_t u = blockIdx.x;
+    if (UA && (gridDim.x & 7u) == 0u) u = (u & 7u) * (gridDim.x >> 3) + (u >> 3);
 #else
     const uint32_t u = blockIdx.x * (kWG / kWave) + wid;
 #endif
@@ -439,10 +451,32 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #endif
         const uint32_t ch = (t0 + i) * kWave + lane;
         const uint32_t chl = ch < cpb ? ch : cpb - 1;  // load chunk, clamped: loads stay unconditional
+        // UA: byte offset of the lane's 16-byte window (the row's last one overlaps the one before)
+        const uint32_t win = UA ? (chl * 16u < S - 16u ? chl * 16u : S - 16u) : 0u;
+        const bool last_tile = (t0 + i + 1) * uint32_t(kWave * 16) > S;  // wave-uniform
+        // UA: the last window's shift to its chunk position (0 when S is a multiple of 16)
+        const uint32_t dsh = UA ? 16u * (cpb - 1u) - (S - 16u) : 0u;
+        // wave-uniform: this tile's last window moves
+        const bool fix = UA && last_tile && dsh != 0u;
+        const bool mine = ch == cpb - 1u;
+        // the window's 16 bytes shifted right by dsh bytes (1..15, zero fill): two u64 halves
+        auto shifted = [&](const u32x4& x) -> u32x4 {
+            const uint64_t lo = uint64_t(x[0]) | (uint64_t(x[1]) << 32), hi = uint64_t(x[2]) | (uint64_t(x[3]) << 32);
+            const uint32_t sb = 8u * dsh;
+            const uint64_t nlo = sb < 64u ? (lo >> sb) | (hi << (64u - sb)) : hi >> (sb - 64u);
+            const uint64_t nhi = sb < 64u ? hi >> sb : 0u;
+            return u32x4{uint32_t(nlo), uint32_t(nlo >> 32), uint32_t(nhi), uint32_t(nhi >> 32)};
+        };
+        // the correction that moves the window's bytes to their chunk position: the counts only
+        // matter mod 2, so adding (window XOR shifted window), its lane alone, does it
+        auto correction = [&](const u32x4& x) -> u32x4 {
+            const u32x4 y = shifted(x);
+            return u32x4{mine ? x[0] ^ y[0] : 0u, mine ? x[1] ^ y[1] : 0u, mine ? x[2] ^ y[2] : 0u, mine ? x[3] ^ y[3] : 0u};
+        };
         // bytes of the lane's chunk that count: those before S (lanes past the row's last chunk,
         // which loaded a clamped chunk, count nothing); all-ones except in a row's last tile
         uint32_t mk[4] = {~0u, ~0u, ~0u, ~0u};
-        if ((t0 + i + 1) * uint32_t(kWave * 16) > S) {  // wave-uniform: the row's last tile
+        if (last_tile) {
             const int valid = int(S) - int(ch * 16u);
 #pragma unroll
             for (int w = 0; w < 4; w++) {
@@ -495,118 +529,158 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         // loop, so without an anchor the MFMAs sink to the loop's end and every row's bit forms
         // stay live
         auto anchor = [&](int r) { asm volatile("" : "+v"(cacc[r / 2])); };
-        auto load_col = [&](int c) { return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl); };
+        // the tile's body; UA: the row's last tile with S % 16 != 0 moves its last window to its
+        // chunk position (a separate copy, so the common tiles carry none of it)
+        auto tile_body = [&]() {
+            auto load_col = [&](int c) {
+                if constexpr (UA)
+                    return ld16u<NT == 1>(ib + in_off[c] + win);
+                else
+                    return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl);
+            };
 
-        u32x4 v[P];
-#pragma unroll
-        for (int c = 0; c < P; c++) v[c] = load_col(c);
-        uint32_t acc[MT][4], pend[MT][4];
-        uint32_t tb = 0;
-        asm volatile("" : "+v"(tb));
-        const u32x4* tbl = s_tbl + tb;
-        u32x4 Tn[5];
-#pragma unroll
-        for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
-#pragma unroll
-        for (int c = 0; c < K; c++) {
-            const int slot = c % P;
-            u32x4 T[5];
-#pragma unroll
-            for (int f = 0; f < 5; f++) T[f] = Tn[f];
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t x = u4get(v[slot], w);
-                const uint32_t s1 = x & 0x07070707u;
-                const uint32_t s2 = (x >> 3) & 0x07070707u;
-                const uint32_t s3 = (x >> 6) & 0x03030303u;
-#pragma unroll
-                for (int j = 0; j < MT; j++) {
-                    const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
-                    const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
-                    const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
-                    uint32_t& a = acc[j][w];
-                    uint32_t& q = pend[j][w];
-                    if (c == 0 && K == 1) {
-                        a = xor3(p1, p2, p3);
-                    } else if (c == 0) {
-                        a = p1 ^ p2;
-                        q = p3;
-                    } else if (c & 1) {
-                        a = xor3(a, p1, p2);
-                        a = xor3(a, p3, q);
-                    } else if (c == K - 1) {
-                        a = xor3(a, p1, p2);
-                        a ^= p3;
-                    } else {
-                        a = xor3(a, p1, p2);
-                        q = p3;
+            u32x4 v[P];
+    #pragma unroll
+            for (int c = 0; c < P; c++) v[c] = load_col(c);
+            uint32_t acc[MT][4], pend[MT][4];
+            uint32_t tb = 0;
+            asm volatile("" : "+v"(tb));
+            const u32x4* tbl = s_tbl + tb;
+            u32x4 Tn[5];
+    #pragma unroll
+            for (int f = 0; f < 5; f++) Tn[f] = tbl[f];
+    #pragma unroll
+            for (int c = 0; c < K; c++) {
+                const int slot = c % P;
+                u32x4 T[5];
+    #pragma unroll
+                for (int f = 0; f < 5; f++) T[f] = Tn[f];
+    #pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const uint32_t x = u4get(v[slot], w);
+                    const uint32_t s1 = x & 0x07070707u;
+                    const uint32_t s2 = (x >> 3) & 0x07070707u;
+                    const uint32_t s3 = (x >> 6) & 0x03030303u;
+    #pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        const uint32_t p1 = __builtin_amdgcn_perm(u4get(T[1], j), u4get(T[0], j), s1);
+                        const uint32_t p2 = __builtin_amdgcn_perm(u4get(T[3], j), u4get(T[2], j), s2);
+                        const uint32_t p3 = __builtin_amdgcn_perm(u4get(T[4], j), u4get(T[4], j), s3);
+                        uint32_t& a = acc[j][w];
+                        uint32_t& q = pend[j][w];
+                        if (c == 0 && K == 1) {
+                            a = xor3(p1, p2, p3);
+                        } else if (c == 0) {
+                            a = p1 ^ p2;
+                            q = p3;
+                        } else if (c & 1) {
+                            a = xor3(a, p1, p2);
+                            a = xor3(a, p3, q);
+                        } else if (c == K - 1) {
+                            a = xor3(a, p1, p2);
+                            a ^= p3;
+                        } else {
+                            a = xor3(a, p1, p2);
+                            q = p3;
+                        }
                     }
+    #ifndef RSMI_FUSED_NOIL
+                    // form w's MFMA between the GF work of dword w and w + 1: its latency (and the
+                    // chain of the row's four MFMAs) hides under this wave's own VALU stream
+                    crc_mfma(v[slot], c, w);
+                    __builtin_amdgcn_sched_barrier(0);
+    #endif
                 }
-#ifndef RSMI_FUSED_NOIL
-                // form w's MFMA between the GF work of dword w and w + 1: its latency (and the
-                // chain of the row's four MFMAs) hides under this wave's own VALU stream
-                crc_mfma(v[slot], c, w);
+    #ifdef RSMI_FUSED_NOIL  // diagnostic: the row's four MFMAs back to back after its GF work
+    #pragma unroll
+                for (int q = 0; q < 4; q++) crc_mfma(v[slot], c, q);
+    #endif
+                anchor(c);
+                if (c + P < K) v[slot] = load_col(c + P);
+                if (c + 1 < K) {
+    #pragma unroll
+                    for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
+                }
                 __builtin_amdgcn_sched_barrier(0);
-#endif
             }
-#ifdef RSMI_FUSED_NOIL  // diagnostic: the row's four MFMAs back to back after its GF work
-#pragma unroll
-            for (int q = 0; q < 4; q++) crc_mfma(v[slot], c, q);
-#endif
-            anchor(c);
-            if (c + P < K) v[slot] = load_col(c + P);
-            if (c + 1 < K) {
-#pragma unroll
-                for (int f = 0; f < 5; f++) Tn[f] = tbl[(c + 1) * 5 + f];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int j = 0; j < MT; j++)
-#pragma unroll
-            for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
-        // the output rows: bit form by bit form, even rows before odd ones, so consecutive MFMAs
-        // go to different accumulators wherever two output rows do not share one
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-                for (int j = h; j < MT; j += 2) crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
-#pragma unroll
-        for (int j = 0; j < MT; j++) anchor(K + j);
-
-        if (ch < cpb) {
-            const uint32_t boff = ch * 16u;
-            if (boff + 16u <= S) {
-#pragma unroll
+    #pragma unroll
+            for (int j = 0; j < MT; j++)
+    #pragma unroll
+                for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
+            // the output rows: bit form by bit form, even rows before odd ones, so consecutive MFMAs
+            // go to different accumulators wherever two output rows do not share one
+    #pragma unroll
+            for (int q = 0; q < 4; q++)
+    #pragma unroll
+                for (int h = 0; h < 2; h++)
+    #pragma unroll
+                    for (int j = h; j < MT; j += 2) crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
+    #pragma unroll
+            for (int j = 0; j < MT; j++) anchor(K + j);
+            // UA: every row's last window went in unshifted; correct the output rows' counts here
+            // and the input rows' after the stores (reloaded: a shifted copy of every row in flight
+            // would not fit the registers)
+            if (UA && fix) {
+    #pragma unroll
                 for (int j = 0; j < MT; j++) {
-                    const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-                    if constexpr (NT == 1)
-                        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
-                    else
-                        *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                    const u32x4 d = correction(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
+    #pragma unroll
+                    for (int q = 0; q < 4; q++) crc_mfma(d, K + j, q);
+                    anchor(K + j);
                 }
-            } else {
-                // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
-#pragma unroll
-                for (int j = 0; j < MT; j++) {
-                    uint8_t* p = ob + out_off[j] + boff;
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        const uint32_t val = acc[j][w];
-                        const uint32_t o = boff + 4u * w;
-                        if (o + 4u <= S) {
-                            *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
-                        } else if (o < S) {
-                            p[4 * w] = uint8_t(val);
-                            if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
-                            if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+            }
+
+            if (UA && ch < cpb) {
+    #pragma unroll
+                for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
+            } else if (!UA && ch < cpb) {
+                const uint32_t boff = ch * 16u;
+                if (boff + 16u <= S) {
+    #pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                        if constexpr (NT == 1)
+                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                        else
+                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                    }
+                } else {
+                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+    #pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        uint8_t* p = ob + out_off[j] + boff;
+    #pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const uint32_t val = acc[j][w];
+                            const uint32_t o = boff + 4u * w;
+                            if (o + 4u <= S) {
+                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                            } else if (o < S) {
+                                p[4 * w] = uint8_t(val);
+                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                            }
                         }
                     }
                 }
             }
-        }
+            if (UA && fix) {
+                // an opaque base: the reloads must not be merged with the row loop's loads (that
+                // would keep every row's window live through the tile)
+                const uint8_t* rb = ib;
+                uint32_t rw = win;
+                asm volatile("" : "+s"(rb), "+v"(rw));
+    #pragma unroll
+                for (int c = 0; c < K; c++) {
+                    const u32x4 d = correction(ld16u<NT == 1>(rb + in_off[c] + rw));
+    #pragma unroll
+                    for (int q = 0; q < 4; q++) crc_mfma(d, c, q);
+                    anchor(c);  // one reload at a time
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+        tile_body();
     }
 
     // parities -> the unit's record: byte (accumulator a, lane slot), bits i / 4 + i = element i's
@@ -1324,6 +1398,7 @@ static void fill_km(FastKernelTable& t) {
     t.crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, true>);
     t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, true>);
     t.fused[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd>);
+    t.fused_ua[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true>);
 }
 
 template <int K>

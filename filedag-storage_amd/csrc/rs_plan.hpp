@@ -34,7 +34,8 @@ struct FastKernelTable {
     void* ua[17][kMaxMT + 1];
     void* crc[17][kMaxMT + 1];
     void* ua_crc[17][kMaxMT + 1];
-    void* fused[17][kMaxMT + 1];  // aligned, the CRC-16 folded on the matrix cores (rs_fused_mfma_kernel)
+    void* fused[17][kMaxMT + 1];     // aligned, the CRC-16 folded on the matrix cores (rs_fused_mfma_kernel)
+    void* fused_ua[17][kMaxMT + 1];  // the same on unaligned-window layouts (S >= 16)
 };
 
 const FastKernelTable& fast_kernels();

@@ -146,15 +146,18 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
     const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
                          in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (size_t(1) << 31);
-    if (aligned && c->opt_fused_fold == 1 && fast_kernels().fused[tile.K][tile.MT]) {
-        // the fold on the matrix cores (rs_fused_mfma_kernel): one unit of 4 tiles per wave, then
-        // the records' combine
+    // unaligned-window layouts (the Split layout, page-locked host rows at pitch S): S >= 16
+    const bool ua = !aligned && S >= 16 && S < (size_t(1) << 31) && in_rs >= S && out_rs >= S;
+    void* mfma_fn = aligned ? fast_kernels().fused[tile.K][tile.MT] : ua ? fast_kernels().fused_ua[tile.K][tile.MT] : nullptr;
+    if (mfma_fn && c->opt_fused_fold == 1) {
+        // the fold on the matrix cores (rs_fused_mfma_kernel): a unit of 4 tiles per workgroup,
+        // then the records' combine
         const size_t upb = (tpb + kFusedUnitTiles - 1) / kFusedUnitTiles;
         const size_t nacc = (nsh + 1) / 2;  // two-shard accumulators: a record byte per lane each
         const size_t rec_per_block = upb * nacc * kWave;
         if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * rec_per_block))) return rc;
         uint8_t* rec = c->d_chunks;
-        void* fn = fast_kernels().fused[tile.K][tile.MT];
+        void* fn = mfma_fn;
         const RsPlanDev* pd = tile.dev;
         uint32_t S32 = uint32_t(S), cpb32 = uint32_t(cpb), tpb32 = uint32_t(tpb), upb32 = uint32_t(upb);
         const uint32_t* tb = c->d_crc_tbl;
@@ -201,8 +204,8 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         }
         char buf[96];
-        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>", tile.K, tile.MT,
-                      auto_cache_policy(tile.K, tile.MT));
+        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s", tile.K, tile.MT,
+                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA");
         c->last_kernel = buf;
         return hip_status(hipGetLastError());
     }

@@ -371,8 +371,8 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opts):
     """Device-resident encode with the CRC fused into the encode pass: parity and every row's
     R(row) equal the oracle's (k > 16, m > 4, and S < 16 in unaligned layouts take the separate
     CRC pass).  Row padding in pitched layouts holds garbage, which must not reach the CRC.
-    crc16_fused_fold 1: aligned layouts fold on the matrix cores (rs_fused_mfma_kernel), 0: the
-    nibble-table variants; waves_per_cu=1 makes every nibble-fold wave code many tiles and every
+    crc16_fused_fold 1: aligned layouts and unaligned ones with S >= 16 fold on the matrix cores
+    (rs_fused_mfma_kernel, ",UA" on the latter), 0: the nibble-table variants; waves_per_cu=1 makes every nibble-fold wave code many tiles and every
     combine wave many blocks."""
     import torch
 
@@ -395,8 +395,9 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opts):
     want = orc.encode_fast(k, m, data)
     assert np.array_equal(got[:, k:, :S], want)
     if k <= 16 and m <= 4 and (S >= 16 or rs % 16 == 0):
-        if rs % 16 == 0 and opts[0][1] == 1:
+        if opts[0][1] == 1:
             assert kern.startswith("rs_fused_mfma_kernel"), kern
+            assert (",UA" in kern) == (rs % 16 != 0), kern
         else:
             assert ",CRC" in kern, kern
             assert (",UA" in kern) == (rs % 16 != 0), kern
@@ -438,8 +439,9 @@ def test_reconstruct_verify_survivor_crcs(k, m, S, nb, lost, pinned):
             kern = c.last_kernel()
             assert np.array_equal(sh, full)
             if pinned and lost and k <= 16 and S >= 16:
-                # one fused kernel: the matrix-core fold on 16-byte rows, the nibble fold otherwise
-                assert (kern.startswith("rs_fused_mfma_kernel") if S % 16 == 0 else ",CRC" in kern), kern
+                # one fused kernel: the matrix-core fold (",UA" when rows are not on the 16-byte grid)
+                assert kern.startswith("rs_fused_mfma_kernel"), kern
+                assert (",UA" in kern) == (S % 16 != 0), kern
             for b in range(nb):
                 for j, r in enumerate(used):
                     assert rsmi.crc16_entry(b"", int(raw[b, j]), S) == orc.crc16_ibm(full[b, r].tobytes()), (b, j)
@@ -487,3 +489,44 @@ def test_fused_mfma_counts_exact(k, m, fill):
             rows = list(data[b]) + list(want[b])
             for i in range(n):
                 assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (S, b, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m", [(10, 4), (16, 4), (2, 1), (5, 3)])
+@pytest.mark.parametrize("mis", [0, 1, 3])
+def test_fused_mfma_split_every_tail(k, m, mis):
+    """rs_fused_mfma_kernel on unaligned-window rows (the Split layout at a base misaligned by
+    `mis` bytes): the lane holding a row's last, overlapping window corrects its counts to the
+    chunk position, for every tail S % 16 (the shift d = 16 - S % 16) and rows that end in the
+    first, a middle and the last tile of a 4-tile unit; all-0xFF rows as well, so the correction's
+    extra counts show if they ever carried into the other shard's bits."""
+    import torch
+
+    n = k + m
+    for S in [4096 * 2 + 1024 + r for r in range(16)] + [17, 31, 1040, 4111, 26215]:
+        nb = 3
+        for fill in ("random", "ones"):
+            if fill == "ones":
+                data = np.full((nb, k, S), 0xFF, dtype=np.uint8)
+            else:
+                data = np.random.default_rng(S * 7 + k + mis).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+            buf = torch.zeros(nb * n * S + mis + 64, dtype=torch.uint8, device="cuda")
+            view = buf[mis:mis + nb * n * S].view(nb, n, S)
+            view[:, :k] = torch.from_numpy(data).cuda()
+            raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+            base = view.data_ptr()
+            with rsmi.Codec(k, m) as c:
+                c.encode_batch_dev_crc(base, S, n * S, base + k * S, S, n * S, S, nb, raw.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                kern = c.last_kernel()
+            assert kern.startswith("rs_fused_mfma_kernel"), kern
+            assert (",UA" in kern) == (S % 16 != 0 or mis != 0), kern
+            got = view.cpu().numpy()
+            want = orc.encode_fast(k, m, data)
+            assert np.array_equal(got[:, k:], want), (S, fill)
+            r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            for b in range(nb):
+                rows = list(data[b]) + list(want[b])
+                for i in range(n):
+                    assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (S, fill, b, i)
