@@ -672,7 +672,9 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                 asm volatile("" : "+s"(rb), "+v"(rw));
     #pragma unroll
                 for (int c = 0; c < K; c++) {
-                    const u32x4 d = correction(ld16u<NT == 1>(rb + in_off[c] + rw));
+                    u32x4 x = {0u, 0u, 0u, 0u};
+                    if (mine) x = ld16u<NT == 1>(rb + in_off[c] + rw);  // that lane's 16 bytes only
+                    const u32x4 d = correction(x);
     #pragma unroll
                     for (int q = 0; q < 4; q++) crc_mfma(d, c, q);
                     anchor(c);  // one reload at a time
