@@ -27,7 +27,8 @@ def med(f, st, reps=40):
 
 
 def main():
-    k, m, nb, B = 10, 4, 4096, 262144
+    # FUSED_SHAPE=k,m,blocks,block_bytes (default RS(10,4) 256 KiB x 4096)
+    k, m, nb, B = (int(x) for x in os.environ.get("FUSED_SHAPE", "10,4,4096,262144").split(","))
     n, S = k + m, (B + k - 1) // k
     st = torch.cuda.current_stream()
     sh = st.cuda_stream
@@ -50,7 +51,8 @@ def main():
         te, tf = med(enc, st), med(fz, st)
         res.append(f"{lay}: encode {te:.1f} us, fused {tf:.1f} us ({tf / te:.2f}x)")
         del buf
-    tag = os.path.basename(os.path.dirname(os.path.dirname(rsmi.LIB_PATH))) + " " + os.environ.get("FUSED_OPT", "")
+    tag = (os.path.basename(os.path.dirname(os.path.dirname(rsmi.LIB_PATH))) + f" RS({k},{m}) {B >> 10} KiB " +
+           os.environ.get("FUSED_OPT", ""))
     print(tag + ": " + "; ".join(res), flush=True)
 
 
