@@ -1072,12 +1072,14 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
 // the shift to the row's end is the nibble pass's.  4 MFMAs and 20 VALU per tile fold what the
 // nibble tables fold with 32 lookups and ~70 VALU.
 //
-// UA: rows at any byte alignment (the Split layout: rows back to back at pitch S).  The loads
-// stay 16-byte aligned: lane l loads the aligned chunk holding row byte 16 ch (ch = the lane's
-// chunk), takes its neighbour's aligned chunk by DPP (wave_shl:1; lane 63 loads its own), and
-// funnel-shifts the pair by the row's misalignment (v_alignbyte_b32, wave-uniform), so the fold
-// sees the row's chunk exactly as on an aligned row.  Loads are clamped to the aligned chunk that
-// holds the row's last byte, so nothing past it is read.
+// UA: rows at any byte alignment (the Split layout: rows back to back at pitch S).  The fold runs
+// on the memory's 16-byte grid instead of the row's: the row's bytes are folded where they lie,
+// from the aligned chunk at or below the row's first byte (its mis = row & 15 leading bytes, the
+// previous row's tail, masked to zero) to the aligned chunk holding its last byte (bytes past it
+// masked), so every load is the aligned pass's and no data moves between lanes.  Only the reference
+// point changes: an item's value is relative to its end on that grid, mis bytes before its end on
+// the row's grid, so the shift to the row's end takes mis bytes more (the launch's tiles per row
+// count mis + S bytes, S + 15 at most).
 template <bool UA>
 __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
@@ -1099,7 +1101,6 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
     const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
     for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
         const CrcItem x = crc_item(it, nsup, nrows, tpb);
         const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
@@ -1107,71 +1108,36 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
         // holds its last byte
         const uint32_t mis = UA ? uint32_t(__builtin_amdgcn_readfirstlane(int(reinterpret_cast<uintptr_t>(row) & 15u))) : 0u;
         const uint8_t* rowa = row - mis;
-        const uint64_t lasta = (mis + S - 1) / 16 * 16;
+        const uint64_t Sm = mis + S;  // the row's end on the memory grid
+        const uint64_t lasta = (Sm - 1) / 16 * 16;
         uint32_t acc = 0;  // lanes 0..15: class m's running value
         for (uint32_t g0 = 0; g0 < x.nt; g0 += kCrcSegTiles) {
             const uint32_t t0 = x.t0 + g0;
             const uint32_t nt = x.nt - g0 < uint32_t(kCrcSegTiles) ? x.nt - g0 : uint32_t(kCrcSegTiles);
             u32x4 v[kCrcSegTiles];
-            if constexpr (!UA) {
 #pragma unroll
-                for (int i = 0; i < kCrcSegTiles; i++) {
-                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
-                }
-            } else {
-                u32x4 nx = {0, 0, 0, 0};
-#pragma unroll
-                for (int i = 0; i < kCrcSegTiles; i++) {
-                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // aligned, unconditional, clamped
-                    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < lasta ? off : lasta)));
-                }
-                if (lane == kWave - 1) {  // the aligned chunk after the group's last one
-                    const uint64_t o2 = (uint64_t(t0 + kCrcSegTiles) * kWave) * 16;
-                    nx = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (o2 < lasta ? o2 : lasta)));
-                }
-#pragma unroll
-                for (int i = 0; i < kCrcSegTiles; i++) {
-                    // the next lane's aligned chunk (wave_shl:1); lane 63's is lane 0's of the next
-                    // tile (still unshifted), or the extra load after the group
-                    u32x4 hi;
-#pragma unroll
-                    for (int w = 0; w < 4; w++) {
-                        const uint32_t t = uint32_t(__builtin_amdgcn_update_dpp(0, int(v[i][w]), 0x130, 0xF, 0xF, false));
-                        const uint32_t n0 = i + 1 < kCrcSegTiles ? uint32_t(__builtin_amdgcn_readlane(int(v[i + 1][w]), 0)) : nx[w];
-                        hi[w] = lane == kWave - 1 ? n0 : t;
-                    }
-                    const uint32_t D[8] = {v[i][0], v[i][1], v[i][2], v[i][3], hi[0], hi[1], hi[2], hi[3]};
-                    const uint32_t q = mis >> 2, r = mis & 3u;
-                    u32x4 o;
-                    switch (q) {  // wave-uniform
-                        case 0:
-                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 1], D[w], r);
-                            break;
-                        case 1:
-                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 2], D[w + 1], r);
-                            break;
-                        case 2:
-                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 3], D[w + 2], r);
-                            break;
-                        default:
-                            for (int w = 0; w < 4; w++) o[w] = __builtin_amdgcn_alignbyte(D[w + 4], D[w + 3], r);
-                            break;
-                    }
-                    v[i] = o;
-                }
+            for (int i = 0; i < kCrcSegTiles; i++) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
+                v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < lasta ? off : lasta)));
             }
             mfma_v4f c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < kCrcSegTiles; i++) {
                 if (uint32_t(i) < nt) {
                     u32x4 d = v[i];
-                    if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
-                        const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+                    if ((uint64_t(t0 + i) + 1) * (kWave * 16) > Sm) {  // wave-uniform: the row's last tile
+                        const int64_t valid = int64_t(Sm) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
 #pragma unroll
                         for (int w = 0; w < 4; w++) {
                             const int64_t n = valid - 4 * w;
                             d[w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                        }
+                    }
+                    if (UA && t0 + i == 0 && mis != 0u && lane == 0) {  // UA: the bytes before the row
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const int n = int(mis) - 4 * w;  // leading bytes of dword w to drop
+                            d[w] &= n >= 4 ? 0u : n <= 0 ? ~0u : ~((1u << (8 * n)) - 1u);
                         }
                     }
 #pragma unroll
@@ -1207,7 +1173,8 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_mfma_kernel(const uint32_t*
             if (m >= (1u << j)) acc ^= t;
         }
         uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), 15));  // wave-uniform from here
-        const uint32_t dd = uint32_t((last_end - crc_item_end(x)) % kCrcOrder);
+        // UA: the item's end lies mis bytes before its end on the row's grid
+        const uint32_t dd = uint32_t((last_end - crc_item_end(x) + mis) % kCrcOrder);
 #pragma unroll
         for (int i = 0; i < kCrcPowers; i++)
             if ((dd >> i) & 1) val = crc_pow4(sQ, i, val);

@@ -44,7 +44,10 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
     // option crc16_fold 0: the nibble-table passes
     void* fn = c->opt_crc16_fold == 1 ? crc16_rows_mfma_kernel(aligned) : crc16_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16;
-    uint32_t tpb = uint32_t((S + tile - 1) / tile);
+    // the matrix-core pass folds unaligned rows on the memory's 16-byte grid, where a row spans
+    // its misalignment (< 16) + S bytes
+    const uint64_t span = S + (c->opt_crc16_fold == 1 && !aligned ? 15 : 0);
+    uint32_t tpb = uint32_t((span + tile - 1) / tile);
     constexpr uint32_t kSup = kCrcSupGroups * kCrcSegTiles;
     uint32_t nsup = (tpb + kSup - 1) / kSup;
     uint64_t nitems = nblocks * nrows * nsup;
