@@ -89,6 +89,7 @@ Crc32Tables::Crc32Tables() {
         for (int v = 0; v < 16; v++) SG[h][v] = apply(P[13], uint32_t(v) << (4 * h));
     for (int i = 0; i < kCrc32SegPowers; i++) shift_columns(uint64_t(8192) << i, SC[i]);
     unshift_columns(8192, SC[kCrc32SegPowers]);
+    for (int i = 0; i < kCrc32MisPowers; i++) shift_columns(uint64_t(1) << i, SC[kCrc32SegPowers + 1 + i]);
     // A^-1 really inverts A, on a basis
     for (int bit = 0; bit < 32; bit++)
         if (apply(Q[0], apply(P[0], 1u << bit)) != (1u << bit)) std::abort();

@@ -24,6 +24,7 @@ constexpr int kCrc32SegTiles = 8;    // device segment: 8 tiles of 1 KiB (rs_crc
 constexpr int kCrc32ScanPowers = 6;  // A^(16 * 2^j), j < 6: the 64-lane scan of a tile
 constexpr int kCrc32SegPowers = 19;  // A^(8192 * 2^i), i < 19: whole-segment shifts
 constexpr int kCrc32SupGroups = 4;   // 8-tile groups per device item (scan and end shift once per item)
+constexpr int kCrc32MisPowers = 4;   // A^(2^i), i < 4: an unaligned row's misalignment (< 16 bytes)
 
 struct Crc32Tables {
     uint32_t T[256];                          // reflected 0xEDB88320
@@ -33,11 +34,12 @@ struct Crc32Tables {
     // device tables.  NT[t][q][v]: the nibble table N[q] moved 1024 * (7 - t) bytes further
     // from the end, for a chunk in tile t of an 8-tile segment (value relative to the
     // segment's end); SN[j][h][v] = A^(16 * 2^j)(v << 4h), nibble-sliced scan powers;
-    // SC[i][b] = A^(8192 * 2^i)(1 << b), column-form segment powers, and SC[19] = A^-8192
+    // SC[i][b] = A^(8192 * 2^i)(1 << b), column-form segment powers, SC[19] = A^-8192 and
+    // SC[20 + i] = A^(2^i), i < 4 (the unaligned pass's shift by the row's misalignment)
     uint32_t NT[kCrc32SegTiles][32][16];
     uint32_t SN[kCrc32ScanPowers][8][16];
     uint32_t SG[8][16];  // A^8192 nibble-sliced: the step between an item's 8-tile groups
-    uint32_t SC[kCrc32SegPowers + 1][32];
+    uint32_t SC[kCrc32SegPowers + 1 + kCrc32MisPowers][32];
     Crc32Tables();
     static uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {
         return t[0][s & 0xFF] ^ t[1][(s >> 8) & 0xFF] ^ t[2][(s >> 16) & 0xFF] ^ t[3][s >> 24];

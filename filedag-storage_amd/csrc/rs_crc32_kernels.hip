@@ -87,12 +87,13 @@ __device__ __forceinline__ uint32_t crc32_nib_chunk(const uint8_t* t, const u32x
 }
 
 // The item's value -> row word: lane scan (lane 63 ends with the value relative to the end of
-// group gl), the shift to the row's end, one atomic XOR.  With S = 8192 q8 + r8, an inner group
-// gl moves by 8192 (q8 - gl - 1) + r8; the row's last group ends at 8192 q8 (r8 = 0: the row's
-// end) or at the row's end + 8192 - r8, so it moves by r8 - 8192.
+// group gl), the shift to the row's end, one atomic XOR.  With S = 8192 q8 + r8, a group gl < q8
+// moves by 8192 (q8 - gl - 1) + r8; a group that ends past S (the row's last one, r8 != 0) moves
+// back by 8192 (gl - q8 + 1) - r8.  Unaligned rows fold on the memory's grid, where every group
+// ends mis bytes earlier than on the row's (and a row may reach into group q8 + 1): mis more.
 __device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_t* sC, uint32_t col_r, uint32_t lane,
-                                               uint32_t l32, uint32_t acc, uint32_t gl, uint32_t nseg, uint32_t q8,
-                                               uint32_t r8, uint32_t* word) {
+                                               uint32_t l32, uint32_t acc, uint32_t gl, uint32_t q8, uint32_t mis,
+                                               uint32_t* word) {
 #pragma unroll
     for (int j = 0; j < kCrc32ScanPowers; j++) {
         const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
@@ -100,15 +101,18 @@ __device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_
         if (lane >= (1u << j)) acc ^= t;
     }
     uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // wave-uniform from here on
-    if (gl + 1 < nseg) {
+    if (gl < q8) {
         // whole segments, then the remainder r8
         uint32_t a = q8 - gl - 1;
         for (int i = 0; a; i++, a >>= 1)
             if (a & 1) val = apply_lanes(sC[32 * i + l32], val, l32);
-        val = apply_lanes(col_r, val, l32);
-    } else if (r8) {
-        val = apply_lanes(col_r, apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32), l32);
+    } else {
+        for (uint32_t g = q8; g <= gl; g++) val = apply_lanes(sC[32 * kCrc32SegPowers + l32], val, l32);  // A^-8192
     }
+    val = apply_lanes(col_r, val, l32);
+#pragma unroll
+    for (int i = 0; i < kCrc32MisPowers; i++)
+        if ((mis >> i) & 1) val = apply_lanes(sC[32 * (kCrc32SegPowers + 1 + i) + l32], val, l32);
     if (lane == 0) atomicXor(word, val);
 }
 
@@ -149,76 +153,25 @@ __device__ __forceinline__ Crc32Item crc32_item(uint64_t it, uint32_t nsup, uint
     const uint32_t* sS = s_tbl + kCrc32FoldWords;                                                         \
     const uint32_t* sG = sS + kCrc32ScanPowers * kCrc32PowWords;                                          \
     const uint32_t* sC = tbl + kCrc32LdsWords;                                                            \
-    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024)), r8 = uint32_t(S % (kCrc32SegTiles * 1024)); \
+    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024));                                           \
     const uint32_t l32 = threadIdx.x & 31;                                                                \
     uint32_t col_r = 0; /* A^r8, lane-distributed */                                                      \
     _Pragma("unroll") for (int b_ = 0; b_ < 32; b_++) col_r = l32 == uint32_t(b_) ? sh.col[b_] : col_r;
 
-// tbl: NT[8][32][16] | SN[6][8][16] | SG[8][16] (staged in LDS) | SC[20][32] (rs_plan.hpp).
+// tbl: NT[8][32][16] | SN[6][8][16] | SG[8][16] (staged in LDS) | SC[24][32] (rs_plan.hpp).
 // An item is up to kCrc32SupGroups 8-tile groups of one row: each group folds through the
 // tile-set tables into a value relative to its end, a running register steps by A^8192 (SG)
-// between groups, and the scan and the end shift run once per item (the CRC-16 pass's
-// round-2 structure; 8-tile items spent a quarter of the pass there).  (A software-pipelined
-// loop measured level with the plain one in round 1, -3% to +5%.)
-template <bool ALIGNED>
-__global__ __launch_bounds__(kWG) void rs_crc32_rows_kernel(const uint32_t* __restrict__ tbl,
-                                                            const uint8_t* __restrict__ base, uint64_t bstride,
-                                                            uint64_t rpitch, uint32_t nrows, uint64_t S, uint32_t tpb,
-                                                            uint32_t nseg, uint32_t nsup, uint64_t nitems,
-                                                            uint32_t* __restrict__ out, uint64_t out_bs, Crc32Shift sh) {
-    RSMI_CRC32_ROWS_STAGE()
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    for (uint64_t it = uint64_t(blockIdx.x) * (kWG / kWave) + wid; it < nitems; it += nw) {
-        uint32_t sup, r;
-        uint64_t b;
-        if (it < (uint64_t(1) << 32)) {  // 32-bit divisions (scalar), the common case
-            const uint32_t i32 = uint32_t(it), rid = i32 / nsup;
-            sup = i32 - rid * nsup;
-            const uint32_t b32 = rid / nrows;
-            b = b32;
-            r = rid - b32 * nrows;
-        } else {
-            sup = uint32_t(it % nsup);
-            const uint64_t rid = it / nsup;
-            b = rid / nrows;
-            r = uint32_t(rid - b * nrows);
-        }
-        const uint8_t* row = base + b * bstride + uint64_t(r) * rpitch;
-        const uint32_t g0 = sup * kCrc32SupGroups;
-        const uint32_t g1 = nseg - g0 < uint32_t(kCrc32SupGroups) ? nseg : g0 + kCrc32SupGroups;  // past the last
-        uint32_t acc = 0;
-        for (uint32_t g = g0; g < g1; g++) {
-            const uint32_t t0 = g * kCrc32SegTiles;
-            const uint32_t nt = tpb - t0 < uint32_t(kCrc32SegTiles) ? tpb - t0 : uint32_t(kCrc32SegTiles);
-            u32x4 v[kCrc32SegTiles];
-#pragma unroll
-            for (int i = 0; i < kCrc32SegTiles; i++)
-                if (uint32_t(i) < nt) {
-                    const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;
-                    // wave-uniform: only a row's last tile needs the per-lane bounds and masks
-                    if (ALIGNED && (uint64_t(t0 + i) + 1) * (kWave * 16) <= S)
-                        v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off));
-                    else
-                        v[i] = crc_chunk_load<ALIGNED>(row, off, S);
-                }
-            uint32_t gs = 0;  // the group's value, relative to the end of its 8-tile span
-#pragma unroll
-            for (int i = 0; i < kCrc32SegTiles; i++)
-                if (uint32_t(i) < nt) gs ^= crc32_nib_chunk(nb + 2048 * i, v[i]);
-            acc = (g == g0 ? 0u : pow_nib(sG, acc)) ^ gs;  // earlier groups move 8 KiB further
-        }
-        crc32_item_out(sS, sC, col_r, lane, l32, acc, g1 - 1, nseg, q8, r8, out + b * out_bs + r);
-    }
-}
-
-// The nibble rows pass, software-pipelined, for 16-byte-aligned rows (the default): the CRC-16
-// pass's structure (rs_crc16_rows_pipe_kernel).  A wave works in units of half a group (4
-// tiles) and issues the loads of its next unit, of this item or its next one, before it folds
-// the current one (two register sets of 16 VGPRs, the loop unrolled by two).  Loads are
-// unconditional: chunks past the row's end re-read the row's last chunk and are masked to zero
-// in the fold, and the prefetch past the wave's last unit re-reads that unit.
+// between groups, and the scan and the end shift run once per item (8-tile items spent a
+// quarter of the pass there).  Software-pipelined as rs_crc16_rows_pipe_kernel: a wave works in
+// units of half a group (4 tiles) and issues the loads of its next unit, of this item or its next
+// one, before it folds the current one (two register sets of 16 VGPRs, the loop unrolled by two).
+// Loads are unconditional: chunks past the row's end re-read the row's last chunk and are masked
+// to zero in the fold, and the prefetch past the wave's last unit re-reads that unit.
+// UA: rows at any alignment (the Split layout) fold on the memory's 16-byte grid, as the CRC-16
+// matrix-core pass does: loads from the aligned chunk at or below the row's first byte (its mis
+// leading bytes masked), the launch's tiles per row counting mis + S <= S + 15 bytes, and the end
+// shift mis bytes longer.
+template <bool UA>
 __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t* __restrict__ tbl,
                                                                  const uint8_t* __restrict__ base, uint64_t bstride,
                                                                  uint64_t rpitch, uint32_t nrows, uint64_t S,
@@ -230,7 +183,6 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t nw = uint64_t(gridDim.x) * (kWG / kWave);
-    const uint64_t last = (S - 1) / 16 * 16;  // the row's last chunk (S > 0)
     struct Unit {
         uint64_t it;
         Crc32Item x;
@@ -241,12 +193,19 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
         if ((u.h + 1) * kU < u.x.nt) return Unit{u.it, u.x, u.h + 1};
         return at(u.it + nw);
     };
+    // the row's misalignment (wave-uniform; 0 for aligned rows)
+    auto misof = [&](const Crc32Item& x) -> uint32_t {
+        const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
+        return UA ? uint32_t(__builtin_amdgcn_readfirstlane(int(reinterpret_cast<uintptr_t>(row) & 15u))) : 0u;
+    };
     auto issue = [&](const Unit& u, u32x4(&v)[kU]) {
-        const uint8_t* row = base + u.x.b * bstride + uint64_t(u.x.r) * rpitch;
+        const uint32_t mis = misof(u.x);
+        const uint8_t* rowa = base + u.x.b * bstride + uint64_t(u.x.r) * rpitch - mis;
+        const uint64_t last = (S + mis - 1) / 16 * 16;  // the aligned chunk holding the row's last byte
 #pragma unroll
         for (int i = 0; i < kU; i++) {
             const uint64_t off = (uint64_t(u.x.t0 + u.h * kU + i) * kWave + lane) * 16;
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + (off < last ? off : last)));
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < last ? off : last)));
         }
     };
     uint32_t acc = 0, gs = 0;
@@ -255,15 +214,24 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
         const uint32_t u0 = u.h * kU, t0 = x.t0 + u0;
         const uint32_t nt = x.nt - u0 < uint32_t(kU) ? x.nt - u0 : uint32_t(kU);
         const uint8_t* gt = nb + 2048 * kU * (u.h & 1);  // table sets of this half of the group
+        const uint32_t mis = misof(x);
+        const uint64_t Sm = S + mis;  // the row's end on the memory grid
 #pragma unroll
         for (int i = 0; i < kU; i++) {
             if (uint32_t(i) < nt) {
-                if ((uint64_t(t0 + i) + 1) * (kWave * 16) > S) {  // wave-uniform: the row's last tile
-                    const int64_t valid = int64_t(S) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+                if ((uint64_t(t0 + i) + 1) * (kWave * 16) > Sm) {  // wave-uniform: the row's last tile
+                    const int64_t valid = int64_t(Sm) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
 #pragma unroll
                     for (int w = 0; w < 4; w++) {
                         const int64_t n = valid - 4 * w;
                         v[i][w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                    }
+                }
+                if (UA && t0 + i == 0 && mis != 0u && lane == 0) {  // the bytes before the row
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const int n = int(mis) - 4 * w;
+                        v[i][w] &= n >= 4 ? 0u : n <= 0 ? ~0u : ~((1u << (8 * n)) - 1u);
                     }
                 }
                 gs ^= crc32_nib_chunk(gt + 2048 * i, v[i]);
@@ -275,7 +243,7 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
             gs = 0;
         }
         if (item_end) {
-            crc32_item_out(sS, sC, col_r, lane, l32, acc, (x.t0 + x.nt - 1) / kCrc32SegTiles, nseg, q8, r8,
+            crc32_item_out(sS, sC, col_r, lane, l32, acc, (x.t0 + x.nt - 1) / kCrc32SegTiles, q8, mis,
                            out + x.b * out_bs + x.r);
             acc = 0;
         }
@@ -302,8 +270,8 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
 }
 
 void* crc32_rows_kernel(bool aligned) {
-    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_pipe_kernel)
-                   : reinterpret_cast<void*>(&rs_crc32_rows_kernel<false>);
+    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_pipe_kernel<false>)
+                   : reinterpret_cast<void*>(&rs_crc32_rows_pipe_kernel<true>);
 }
 
 }  // namespace rsmi

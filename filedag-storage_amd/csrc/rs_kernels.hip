@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         auto shifted = [&](const u32x4& x) -> u32x4 {
             const uint64_t lo = uint64_t(x[0]) | (uint64_t(x[1]) << 32), hi = uint64_t(x[2]) | (uint64_t(x[3]) << 32);
             const uint32_t sb = 8u * dsh;
-            const uint64_t nlo = sb < 64u ? (lo >> sb) | (hi << (64u - sb)) : hi >> (sb - 64u);
+            const uint64_t nlo = sb == 0u ? lo : sb < 64u ? (lo >> sb) | (hi << ((64u - sb) & 63u)) : hi >> ((sb - 64u) & 63u);
             const uint64_t nhi = sb < 64u ? hi >> sb : 0u;
             return u32x4{uint32_t(nlo), uint32_t(nlo >> 32), uint32_t(nhi), uint32_t(nhi >> 32)};
         };

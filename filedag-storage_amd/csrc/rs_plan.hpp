@@ -84,11 +84,11 @@ static_assert(kFusedUnitTiles == 1 << kFusedUnitLog, "unit of 1, 2 or 4 tiles");
 #endif
 constexpr int kFusedWavesPerSimd = RSMI_FUSED_WPS;  // its register budget: 168 VGPRs (the row accumulators)
 // CRC-32 (crc32.hpp) device tables, u32 words: NT[8][32][16] | SN[6][8][16] (both staged in
-// LDS, 19 KiB) | SC[20][32] (column form, read with scalar loads)
+// LDS, 19 KiB) | SC[24][32] (column form, read with scalar loads)
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
 constexpr int kCrc32PowWords = 8 * 16;  // one nibble-sliced power
 constexpr int kCrc32LdsWords = kCrc32FoldWords + 7 * kCrc32PowWords;  // NT | SN[6] | SG
-constexpr int kCrc32TableWords = kCrc32LdsWords + 20 * 32;
+constexpr int kCrc32TableWords = kCrc32LdsWords + 24 * 32;
 // per-launch shift to the row's end, column form (crc32.hpp), passed by value: A^(S mod 8192),
 // the end of an inner segment moved over whatever of the row follows whole segments
 struct Crc32Shift {

@@ -97,7 +97,8 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     void* fn = crc32_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16, span = tile * kCrc32SegTiles;
     if (S / span >= (uint64_t(1) << kCrc32SegPowers)) return RSMI_ERR_INVALID_ARG;  // rows below 4 GiB
-    uint32_t tpb = uint32_t((S + tile - 1) / tile);
+    // unaligned rows fold on the memory's 16-byte grid, where a row spans its misalignment + S bytes
+    uint32_t tpb = uint32_t((S + (aligned ? 0 : 15) + tile - 1) / tile);
     uint32_t nseg = (tpb + kCrc32SegTiles - 1) / kCrc32SegTiles;
     uint32_t nsup = (nseg + kCrc32SupGroups - 1) / kCrc32SupGroups;
     // the per-launch shift to the row's end (crc32.hpp), cached for the last S

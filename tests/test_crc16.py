@@ -125,11 +125,12 @@ def test_rows_dev_matches_oracle(S, layout, wpc, fold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S", [1, 15, 16, 17, 1023, 1024, 1040, 8191, 8193, 26215, 104858])
+@pytest.mark.parametrize("S", [1, 15, 16, 17, 1023, 1024, 1040, 8191, 8193, 26215, 32761, 32768, 104858])
 def test_rows_dev_split_layout_every_misalignment(S):
     """The Split layout (rows back to back at pitch S) from each of the 16 byte offsets of an
-    aligned base: every row misalignment (0..15) and so every funnel-shift case of the
-    matrix-core pass's unaligned loads, against the oracle."""
+    aligned base: every row misalignment (0..15) of the matrix-core pass's memory-grid fold
+    (leading bytes masked, rows reaching one tile, group or item further on the memory grid, the
+    end shift by the misalignment), against the oracle."""
     import torch
 
     nrows, nb = 4, 3

@@ -96,6 +96,32 @@ def test_rows_dev_matches_zlib(S, layout, wpc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("S", [17, 1009, 1024, 8177, 8185, 8192, 16383, 26215, 32761, 32768, 73729])
+def test_rows_dev_split_layout_every_misalignment(S):
+    """The Split layout (rows back to back at pitch S) from each of the 16 byte offsets of an
+    aligned base: every row misalignment of the unaligned pass's memory-grid fold (leading bytes
+    masked, rows reaching one tile or one 8 KiB group further on the memory grid, the end shift
+    by the misalignment), against zlib."""
+    import torch
+
+    nrows, nb = 4, 3
+    for off in range(16):
+        g = torch.Generator().manual_seed(S * 7 + off)
+        host = torch.randint(0, 256, (off + nb * nrows * S + 64,), dtype=torch.uint8, generator=g)
+        dev = host.to("cuda")
+        out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+        with rsmi.Codec(4, 2) as c:
+            c.crc32_rows_dev(dev.data_ptr() + off, S, nrows * S, nrows, S, nb, out.data_ptr(), nrows)
+            torch.cuda.synchronize()
+        got = out.cpu().numpy().astype(np.int64) & M32
+        h = host.numpy()
+        for b in range(nb):
+            for r in range(nrows):
+                row = h[off + (b * nrows + r) * S:][:S].tobytes()
+                assert got[b, r] == raw32(row), (off, b, r)
+
+
+@pytest.mark.gpu
 def test_rows_dev_full_size_batch():
     """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows, against zlib on a sample of rows."""
     import torch
