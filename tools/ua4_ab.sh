@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 for r in 1 2; do
   for lib in "" tools/build/v_*/lib/librsmi.so; do
     [ -z "$lib" ] || [ -e "$lib" ] || continue
-    RSMI_LIB=${lib:+$PWD/$lib} timeout -k 10 200 python bench.py --layout split --cpu-seconds 0 --sustained-steps 0 > gpurun_out/ua4.json 2> gpurun_out/ua4.err || { echo "bench failed"; tail gpurun_out/ua4.err; exit 1; }
+    RSMI_LIB=${lib:+$PWD/$lib} timeout -k 10 200 python bench.py --layout split --cpu-seconds 0 --sustained-steps 0 ${UA_BENCH_ARGS:-} > gpurun_out/ua4.json 2> gpurun_out/ua4.err || { echo "bench failed"; tail gpurun_out/ua4.err; exit 1; }
     python3 -c "
 import json; j=json.load(open('gpurun_out/ua4.json'))
 print(('$lib'.split('/')[2] if '$lib' else 'product').ljust(10), 'encode', j['roofline']['achieved'], '| reconstruct', j['reconstruct']['achieved_GBs'], 'GB/s', j['reconstruct']['kernel'], 'verified', j['verify']['verified'])"
