@@ -181,6 +181,37 @@ def test_rows_dev_random_shapes_both_folds():
 
 
 @pytest.mark.gpu
+def test_rows_dev_random_unaligned_shapes_both_folds():
+    """40 random unaligned geometries (any base offset, pitch >= S and block stride at any byte
+    granularity, so rows of one launch take many misalignments): the matrix-core pass's
+    memory-grid fold and the nibble pass give the oracle's R(row) on every row."""
+    import torch
+
+    rng = random.Random(2027)
+    for _ in range(40):
+        S = rng.choice([rng.randrange(16, 2048), rng.randrange(2048, 70000), rng.randrange(70000, 200000)])
+        nrows, nb = rng.randrange(1, 6), rng.randrange(1, 6)
+        off = rng.randrange(0, 16)
+        pitch = S + rng.randrange(0, 40)
+        bstride = nrows * pitch + rng.randrange(0, 40)
+        g = torch.Generator().manual_seed(S + off)
+        host = torch.randint(0, 256, (off + nb * bstride + 64,), dtype=torch.uint8, generator=g)
+        dev = host.to("cuda")
+        h = host.numpy()
+        for fold in (1, 0):
+            out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+            with rsmi.Codec(4, 2) as c:
+                c.set_option("crc16_fold", fold)
+                c.crc16_rows_dev(dev.data_ptr() + off, pitch, bstride, nrows, S, nb, out.data_ptr(), nrows)
+                torch.cuda.synchronize()
+            got = out.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+            for b in range(nb):
+                for r in range(nrows):
+                    row = h[off + b * bstride + r * pitch:][:S].tobytes()
+                    assert rsmi.crc16_entry(b"", int(got[b, r]), S) == orc.crc16_ibm(row), (S, off, pitch, bstride, fold, b, r)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fold", [1, 0])
 def test_rows_dev_full_size_batch(fold):
     """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows: a checksum of checksums against the

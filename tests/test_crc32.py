@@ -122,6 +122,36 @@ def test_rows_dev_split_layout_every_misalignment(S):
 
 
 @pytest.mark.gpu
+def test_rows_dev_random_unaligned_shapes():
+    """40 random unaligned geometries (any base offset, pitch >= S and block stride at any byte
+    granularity): the unaligned pass's memory-grid fold against zlib on every row."""
+    import random
+
+    import torch
+
+    rng = random.Random(2028)
+    for _ in range(40):
+        S = rng.choice([rng.randrange(1, 2048), rng.randrange(2048, 70000), rng.randrange(70000, 200000)])
+        nrows, nb = rng.randrange(1, 6), rng.randrange(1, 6)
+        off = rng.randrange(1, 16)
+        pitch = S + rng.randrange(0, 40)
+        bstride = nrows * pitch + rng.randrange(0, 40)
+        g = torch.Generator().manual_seed(S + off)
+        host = torch.randint(0, 256, (off + nb * bstride + 64,), dtype=torch.uint8, generator=g)
+        dev = host.to("cuda")
+        h = host.numpy()
+        out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+        with rsmi.Codec(4, 2) as c:
+            c.crc32_rows_dev(dev.data_ptr() + off, pitch, bstride, nrows, S, nb, out.data_ptr(), nrows)
+            torch.cuda.synchronize()
+        got = out.cpu().numpy().astype(np.int64) & M32
+        for b in range(nb):
+            for r in range(nrows):
+                row = h[off + b * bstride + r * pitch:][:S].tobytes()
+                assert got[b, r] == raw32(row), (S, off, pitch, bstride, b, r)
+
+
+@pytest.mark.gpu
 def test_rows_dev_full_size_batch():
     """RS(10,4) 256 KiB geometry, 4096 blocks x 14 rows, against zlib on a sample of rows."""
     import torch
