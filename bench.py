@@ -93,7 +93,10 @@ def parse(argv=None):
     p.add_argument("--mock", action="store_true",
                    help="test only: a CPU stand-in for the device step, to exercise the launcher, the "
                         "ranks and the JSON line on a host without a GPU; never a measurement")
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    if a.steps < 1 or a.warmup < 0 or a.event_every < 1:
+        p.error("--steps and --event-every must be at least 1, --warmup at least 0")
+    return a
 
 
 # ---------------------------------------------------------------- launcher and ranks
