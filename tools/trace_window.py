@@ -29,13 +29,20 @@ def main():
         per.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     ev = {bench["roofline"]["kernel"]: bench["roofline"]["avg_launch_ms"] * 1e3}
     if "reconstruct" in bench:
-        ev[bench["reconstruct"]["kernel"]] = bench["reconstruct"]["avg_launch_ms_incl_event_gap"] * 1e3
+        rec = bench["reconstruct"]
+        ev[rec["kernel"]] = rec.get("avg_launch_ms", rec.get("avg_launch_ms_incl_event_gap")) * 1e3
+    # bench.py times every `every`-th step with HIP events (round 3; every step before)
+    timed = bench["roofline"].get("launches_timed", steps)
+    every = -(-steps // timed)
     for k, d in per.items():
         w = d[first:first + steps]
         avg = sum(w) / len(w)
+        ws = w[::every]
+        avs = sum(ws) / len(ws)
         e = ev.get(k)
-        extra = f"; bench.py HIP events {e:.1f} us ({(e / avg - 1) * 100:+.1f} %)" if e else ""
-        print(f"{k}: {len(d)} dispatches, timed window (last {len(w)}) avg {avg:.1f} us, "
+        extra = (f"; the {len(ws)} event-timed steps avg {avs:.1f} us, bench.py HIP events {e:.1f} us "
+                 f"({(e / avs - 1) * 100:+.1f} %)") if e else ""
+        print(f"{k}: {len(d)} dispatches, timed window ({len(w)} steps) avg {avg:.1f} us, "
               f"min {min(w):.1f}, max {max(w):.1f}{extra}")
 
 
