@@ -105,21 +105,25 @@ int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
 extern "C" {
 
 int rsmi_encode_block_coalesced_crcs(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
-                                     uint32_t* raw16_out, uint32_t* raw32_out) {
+                                     uint32_t* raw16_out, uint32_t* raw32_out) try {
     if (!c) return RSMI_ERR_INVALID_ARG;
     if (B == 0) return RSMI_ERR_SHORT_DATA;
     if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
     rsmi_ctx::CoalReq req{block, B, shards_out, raw16_out, raw32_out, "E" + std::to_string(rsmi_shard_size(B, c->k)) + ":",
                           RSMI_OK, false};
     return coalesce(c, req);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_encode_block_coalesced(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out,
-                                uint32_t* raw_out) {
+                                uint32_t* raw_out) try {
     return rsmi_encode_block_coalesced_crcs(c, block, B, shards_out, raw_out, nullptr);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) try {
     if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     const std::vector<uint8_t> want = want_mask(c, present, data_only);
@@ -131,6 +135,8 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     for (int i = 0; i < c->n; i++) key.push_back(want[i] ? '1' : '0');
     rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, nullptr, std::move(key), RSMI_OK, false};
     return coalesce(c, req);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 long rsmi_get_stat(const rsmi_ctx* c, const char* key) {

@@ -33,6 +33,7 @@ const char* rsmi_status_string(int s) {
         case RSMI_ERR_INVALID_ARG: return "invalid argument";
         case RSMI_ERR_DEVICE: return "HIP device error";
         case RSMI_ERR_NO_DEVICE: return "no usable gfx950 device";
+        case RSMI_ERR_HOST: return "host resources exhausted (memory or threads)";
         default: return "unknown status";
     }
 }

@@ -297,6 +297,13 @@ int reconstruct_dev_impl(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, si
                        static_cast<hipStream_t>(stream));
 }
 
+int exception_status() noexcept {
+    // std::bad_alloc, std::system_error from a thread or mutex, or anything else a host-side
+    // container throws: the call failed for want of host resources.  Unwinding released the
+    // context's locks; the call's outputs are undefined, as after any failed call
+    return RSMI_ERR_HOST;
+}
+
 }  // namespace impl
 }  // namespace rsmi
 
@@ -308,7 +315,7 @@ int rsmi_device_count(void) {
     return n;
 }
 
-int rsmi_open(int k, int m, int device, rsmi_ctx** out) {
+int rsmi_open(int k, int m, int device, rsmi_ctx** out) try {
     if (!out) return RSMI_ERR_INVALID_ARG;
     *out = nullptr;
     if (k <= 0 || m <= 0) return RSMI_ERR_INV_SHARD_NUM;
@@ -321,6 +328,8 @@ int rsmi_open(int k, int m, int device, rsmi_ctx** out) {
     c->M = build_encode_matrix(k, m);
     *out = c;
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 void rsmi_close(rsmi_ctx* c) {
@@ -351,13 +360,15 @@ void rsmi_close(rsmi_ctx* c) {
     delete c;
 }
 
-int rsmi_encode_matrix(const rsmi_ctx* c, uint8_t* out) {
+int rsmi_encode_matrix(const rsmi_ctx* c, uint8_t* out) try {
     if (!c || !out) return RSMI_ERR_INVALID_ARG;
     std::memcpy(out, c->M.v.data(), c->M.v.size());
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_decode_matrix(const rsmi_ctx* c, const uint8_t* present, uint8_t* out, int* used_rows) {
+int rsmi_decode_matrix(const rsmi_ctx* c, const uint8_t* present, uint8_t* out, int* used_rows) try {
     if (!c || !present || !out) return RSMI_ERR_INVALID_ARG;
     Matrix dec;
     std::vector<int> used;
@@ -367,9 +378,11 @@ int rsmi_decode_matrix(const rsmi_ctx* c, const uint8_t* present, uint8_t* out, 
     if (used_rows)
         for (int i = 0; i < c->k; i++) used_rows[i] = used[i];
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
+int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     if (!c || !key) return RSMI_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     if (!std::strcmp(key, "zero_copy")) {
@@ -397,6 +410,8 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
         return RSMI_ERR_INVALID_ARG;
     }
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 const char* rsmi_last_kernel(const rsmi_ctx* c) { return c ? c->last_kernel.c_str() : ""; }
@@ -414,7 +429,7 @@ void rsmi_host_free(void* p) {
 // ---------------------------------------------------------------- device-resident batches
 int rsmi_encode_batch_dev(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_stride, size_t data_block_stride,
                           uint8_t* d_parity, size_t parity_shard_stride, size_t parity_block_stride, size_t S,
-                          size_t nblocks, void* stream) {
+                          size_t nblocks, void* stream) try {
     if (!c || !d_data || !d_parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (data_shard_stride < S || parity_shard_stride < S) return RSMI_ERR_INVALID_ARG;
@@ -429,19 +444,25 @@ int rsmi_encode_batch_dev(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_
         return launch_plan(c, *plan, d_data, data_shard_stride, data_block_stride, d_parity, parity_shard_stride,
                            parity_block_stride, S, nblocks, static_cast<hipStream_t>(stream));
     }
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride, size_t S,
-                               size_t nblocks, const uint8_t* present, int data_only, void* stream) {
+                               size_t nblocks, const uint8_t* present, int data_only, void* stream) try {
     if (!c || !present) return RSMI_ERR_INVALID_ARG;
     const std::vector<uint8_t> w = want_mask(c, present, data_only);
     return reconstruct_dev_impl(c, d_shards, shard_stride, block_stride, S, nblocks, present, w.data(), stream);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* c, uint8_t* d_shards, size_t shard_stride, size_t block_stride,
                                     size_t S, size_t nblocks, const uint8_t* present, const uint8_t* required,
-                                    void* stream) {
+                                    void* stream) try {
     return reconstruct_dev_impl(c, d_shards, shard_stride, block_stride, S, nblocks, present, required, stream);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 }  // extern "C"

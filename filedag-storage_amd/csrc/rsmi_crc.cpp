@@ -250,7 +250,7 @@ extern "C" {
 
 int rsmi_encode_batch_dev_crc(rsmi_ctx* c, const uint8_t* d_data, size_t data_shard_stride, size_t data_block_stride,
                               uint8_t* d_parity, size_t parity_shard_stride, size_t parity_block_stride, size_t S,
-                              size_t nblocks, uint32_t* d_raw_out, void* stream) {
+                              size_t nblocks, uint32_t* d_raw_out, void* stream) try {
     if (!c || !d_data || !d_parity || !d_raw_out) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (data_shard_stride < S || parity_shard_stride < S) return RSMI_ERR_INVALID_ARG;
@@ -277,10 +277,12 @@ int rsmi_encode_batch_dev_crc(rsmi_ctx* c, const uint8_t* d_data, size_t data_sh
         return rc;
     return launch_crc(c, d_parity, parity_shard_stride, parity_block_stride, uint32_t(m), S, nblocks, d_raw_out + k, n,
                       st, false);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
-                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) {
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) try {
     if (!c || !d_rows || !d_raw_out || nrows < 0 || out_block_stride < size_t(nrows)) return RSMI_ERR_INVALID_ARG;
     if (nrows > 1 && shard_stride < S) return RSMI_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
@@ -294,10 +296,12 @@ int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     c->last_kernel = c->opt_crc16_fold == 1 ? (aligned ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel,MFMA,UA")
                                             : "rs_crc16_rows_kernel";
     return hip_status(hipGetLastError());
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride, size_t block_stride, int nrows,
-                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) {
+                        size_t S, size_t nblocks, uint32_t* d_raw_out, size_t out_block_stride, void* stream) try {
     if (!c || !d_rows || !d_raw_out || nrows < 0 || out_block_stride < size_t(nrows)) return RSMI_ERR_INVALID_ARG;
     if (nrows > 1 && shard_stride < S) return RSMI_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(c->mu);
@@ -312,10 +316,12 @@ int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     if (rc) return rc;
     c->last_kernel = "rs_crc32_rows_kernel";
     return hip_status(hipGetLastError());
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size_t nrows, size_t S,
-                       uint32_t* raw16_out, uint32_t* raw32_out) {
+                       uint32_t* raw16_out, uint32_t* raw32_out) try {
     if (!c || !rows || (!raw16_out && !raw32_out) || (nrows > 1 && row_stride < S)) return RSMI_ERR_INVALID_ARG;
     if (nrows == 0) return RSMI_OK;
     std::lock_guard<std::mutex> g(c->mu);
@@ -349,6 +355,8 @@ int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size
     if (raw16_out) HIP_TRY(hipMemcpy(raw16_out, c->d_crc, sz, hipMemcpyDeviceToHost));
     if (raw32_out) HIP_TRY(hipMemcpy(raw32_out, c->d_crc32, sz, hipMemcpyDeviceToHost));
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 }  // extern "C"

@@ -73,7 +73,7 @@ private:
             if (busy_) {
                 std::function<void()> job = std::move(job_);
                 lk.unlock();
-                job();  // the member calls below return status codes, they do not throw
+                job();  // run_parts' jobs catch everything and return status codes
                 lk.lock();
                 busy_ = false;
                 cv_.notify_all();
@@ -128,7 +128,15 @@ int run_parts(rsmi_group* s, size_t nblocks, F f) {
         size_t st, cnt;
         rsmi_partition(nblocks, int(parts), int(i), &st, &cnt);
         if (!cnt) continue;
-        s->workers[i]->post([&rc, &f, i, st, cnt] { rc[i] = f(i, st, cnt); });
+        s->workers[i]->post([&rc, &f, i, st, cnt] {
+            // an exception must not leave the worker thread (std::terminate): the member's host
+            // code allocates (std::bad_alloc), so it becomes the part's status
+            try {
+                rc[i] = f(i, st, cnt);
+            } catch (...) {
+                rc[i] = rsmi::impl::exception_status();
+            }
+        });
         posted.push_back(i);
     }
     for (size_t i : posted) s->workers[i]->wait();
@@ -143,7 +151,7 @@ extern "C" {
 
 // ---------------------------------------------------------------- NUMA helpers (host only)
 
-int rsmi_sysfs_numa_node(const char* sysfs_root, const char* pci_bus_id) {
+int rsmi_sysfs_numa_node(const char* sysfs_root, const char* pci_bus_id) try {
     if (!sysfs_root || !pci_bus_id) return -1;
     std::string id(pci_bus_id);
     for (auto& ch : id) ch = char(std::tolower(static_cast<unsigned char>(ch)));
@@ -151,9 +159,11 @@ int rsmi_sysfs_numa_node(const char* sysfs_root, const char* pci_bus_id) {
     if (txt.empty()) return -1;
     const int v = std::atoi(txt.c_str());
     return v >= 0 ? v : -1;
+} catch (...) {
+    return -1;  // host allocation failed
 }
 
-int rsmi_sysfs_node_cpus(const char* sysfs_root, int node, int* cpus, int max_cpus) {
+int rsmi_sysfs_node_cpus(const char* sysfs_root, int node, int* cpus, int max_cpus) try {
     if (!sysfs_root || node < 0 || (!cpus && max_cpus > 0)) return -1;
     const std::string txt =
         read_file(std::string(sysfs_root) + "/devices/system/node/node" + std::to_string(node) + "/cpulist");
@@ -174,9 +184,11 @@ int rsmi_sysfs_node_cpus(const char* sysfs_root, int node, int* cpus, int max_cp
         }
     }
     return n;
+} catch (...) {
+    return -1;  // host allocation failed
 }
 
-int rsmi_device_numa_node(int device) {
+int rsmi_device_numa_node(int device) try {
     int v = -1;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeHostNumaId, device) == hipSuccess && v >= 0) return v;
     (void)hipGetLastError();
@@ -186,9 +198,11 @@ int rsmi_device_numa_node(int device) {
         return -1;
     }
     return rsmi_sysfs_numa_node("/sys", bus);
+} catch (...) {
+    return -1;  // host allocation failed
 }
 
-int rsmi_bind_thread_to_numa_node(int node) {
+int rsmi_bind_thread_to_numa_node(int node) try {
     if (node < 0) return RSMI_ERR_INVALID_ARG;
     std::vector<int> cpus(4096);
     const int n = rsmi_sysfs_node_cpus("/sys", node, cpus.data(), int(cpus.size()));
@@ -210,11 +224,13 @@ int rsmi_bind_thread_to_numa_node(int node) {
     mask[node / (8 * sizeof(unsigned long))] |= 1UL << (node % (8 * sizeof(unsigned long)));
     if (syscall(SYS_set_mempolicy, MPOL_PREFERRED, mask, sizeof mask * 8) != 0) return RSMI_ERR_INVALID_ARG;
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 // ---------------------------------------------------------------- groups
 
-int rsmi_group_open(int k, int m, const int* devices, int ndev, rsmi_group** out) {
+int rsmi_group_open(int k, int m, const int* devices, int ndev, rsmi_group** out) try {
     if (!out) return RSMI_ERR_INVALID_ARG;
     *out = nullptr;
     if (k <= 0 || m <= 0) return RSMI_ERR_INV_SHARD_NUM;
@@ -243,6 +259,8 @@ int rsmi_group_open(int k, int m, const int* devices, int ndev, rsmi_group** out
     }
     *out = s;
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 void rsmi_group_close(rsmi_group* s) {
@@ -332,18 +350,20 @@ void rsmi_group_host_free(rsmi_group* s, void* p) {
 }
 
 int rsmi_group_encode_batch_host(rsmi_group* s, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                               size_t parity_block_stride, size_t S, size_t nblocks) {
+                               size_t parity_block_stride, size_t S, size_t nblocks) try {
     if (!s || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     return run_parts(s, nblocks, [&](size_t i, size_t st, size_t cnt) {
         return rsmi_encode_batch_host(s->ctx[i], data + st * data_block_stride, data_block_stride,
                                       parity + st * parity_block_stride, parity_block_stride, S, cnt);
     });
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_group_encode_batch_host_crcs(rsmi_group* s, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                     size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
-                                    uint32_t* raw32_out) {
+                                    uint32_t* raw32_out) try {
     if (!s || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     const size_t n = size_t(s->k + s->m);
@@ -353,26 +373,32 @@ int rsmi_group_encode_batch_host_crcs(rsmi_group* s, const uint8_t* data, size_t
                                            raw16_out ? raw16_out + st * n : nullptr,
                                            raw32_out ? raw32_out + st * n : nullptr);
     });
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_group_reconstruct_batch_host(rsmi_group* s, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                    const uint8_t* present, int data_only) {
+                                    const uint8_t* present, int data_only) try {
     if (!s || !shards || !present) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     return run_parts(s, nblocks, [&](size_t i, size_t st, size_t cnt) {
         return rsmi_reconstruct_batch_host(s->ctx[i], shards + st * block_stride, block_stride, S, cnt, present,
                                            data_only);
     });
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_group_reconstruct_rows_batch_host(rsmi_group* s, uint8_t* shards, size_t block_stride, size_t S,
-                                         size_t nblocks, const uint8_t* present, const uint8_t* required) {
+                                         size_t nblocks, const uint8_t* present, const uint8_t* required) try {
     if (!s || !shards || !present || !required) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     return run_parts(s, nblocks, [&](size_t i, size_t st, size_t cnt) {
         return rsmi_reconstruct_rows_batch_host(s->ctx[i], shards + st * block_stride, block_stride, S, cnt, present,
                                                 required);
     });
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 }  // extern "C"

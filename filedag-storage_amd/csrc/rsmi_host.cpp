@@ -421,13 +421,15 @@ int reconstruct_host_impl(rsmi_ctx* c, uint8_t* shards, size_t block_stride, siz
 extern "C" {
 
 // ---------------------------------------------------------------- host memory, one block
-int rsmi_encode(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
+int rsmi_encode(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) try {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     return rsmi_encode_batch_host(c, data, size_t(c->k) * S, parity, size_t(c->m) * S, S, 1);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_encode_block(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out) {
+int rsmi_encode_block(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out) try {
     if (!c) return RSMI_ERR_INVALID_ARG;
     if (B == 0) return RSMI_ERR_SHORT_DATA;  // upstream Split checks this first
     if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
@@ -435,33 +437,43 @@ int rsmi_encode_block(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shar
     std::memcpy(shards_out, block, B);
     std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
     return rsmi_encode(c, shards_out, shards_out + size_t(c->k) * S, S);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_reconstruct(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) {
+int rsmi_reconstruct(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* present, int data_only) try {
     if (!c || !shards || !present) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     return rsmi_reconstruct_batch_host(c, shards, size_t(c->n) * S, S, 1, present, data_only);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                           size_t parity_block_stride, size_t S, size_t nblocks) {
+                           size_t parity_block_stride, size_t S, size_t nblocks) try {
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, nullptr);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
-                               size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) {
+                               size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) try {
     if (!raw_out) return RSMI_ERR_INVALID_ARG;
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                 size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
-                                uint32_t* raw32_out) {
+                                uint32_t* raw32_out) try {
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw16_out,
                             raw32_out);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
-int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out) {
+int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* shards_out, uint32_t* raw_out) try {
     if (!c) return RSMI_ERR_INVALID_ARG;
     if (B == 0) return RSMI_ERR_SHORT_DATA;
     if (!block || !shards_out || !raw_out) return RSMI_ERR_INVALID_ARG;
@@ -470,31 +482,39 @@ int rsmi_encode_block_crc(rsmi_ctx* c, const uint8_t* block, size_t B, uint8_t* 
     std::memset(shards_out + B, 0, size_t(c->k) * S - B);  // Split zero-padding
     return encode_host_impl(c, shards_out, size_t(c->k) * S, shards_out + size_t(c->k) * S, size_t(c->m) * S, S, 1,
                             raw_out);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                const uint8_t* present, int data_only) {
+                                const uint8_t* present, int data_only) try {
     if (!c || !present) return RSMI_ERR_INVALID_ARG;
     const std::vector<uint8_t> w = want_mask(c, present, data_only);
     return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, w.data());
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_rows_batch_host(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                     const uint8_t* present, const uint8_t* required) {
+                                     const uint8_t* present, const uint8_t* required) try {
     return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S,
                                           size_t nblocks, const uint8_t* present, const uint8_t* required,
-                                          uint32_t* raw16_out, uint32_t* raw32_out) {
+                                          uint32_t* raw16_out, uint32_t* raw32_out) try {
     if (!c) return RSMI_ERR_INVALID_ARG;
     if (raw16_out) std::memset(raw16_out, 0, nblocks * size_t(c->n) * 4);
     if (raw32_out) std::memset(raw32_out, 0, nblocks * size_t(c->n) * 4);
     return reconstruct_host_impl(c, shards, block_stride, S, nblocks, present, required, raw16_out, raw32_out);
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t block_stride, size_t S, size_t nblocks,
-                                       const uint8_t* present, int data_only, uint32_t* raw16_in) {
+                                       const uint8_t* present, int data_only, uint32_t* raw16_in) try {
     if (!c || !shards || !present || !raw16_in) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     if (block_stride < size_t(c->n) * S) return RSMI_ERR_INVALID_ARG;
@@ -542,6 +562,8 @@ int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t bloc
         for (size_t b = 0; b < nblocks; b++) raw16_in[b * k + j] = r[b];
     }
     return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
 }
 
 }  // extern "C"

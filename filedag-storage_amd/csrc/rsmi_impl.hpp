@@ -33,6 +33,10 @@ namespace impl {
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// The status of the exception being handled at the C-ABI boundary (the entry points' function
+// try blocks): a C++ exception must not unwind into C or cgo callers.
+int exception_status() noexcept;
+
 
 struct DevTile {
     RsPlanDev* dev = nullptr;

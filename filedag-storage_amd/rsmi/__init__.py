@@ -30,6 +30,7 @@ ErrSingular = 7
 ErrInvalidArg = 8
 ErrDevice = 100
 ErrNoDevice = 101
+ErrHost = 102
 
 
 class RsmiError(Exception):

@@ -28,8 +28,10 @@ extern "C" {
 
 /* 2: rsmi_set_option lost the keys of kernel variants measured slower than the defaults (they
  * return RSMI_ERR_INVALID_ARG); device groups, NUMA placement, the key slot hash and
- * rsmi_reconstruct_batch_host_verify were added; "crc16_fused_fold" is new. */
-#define RSMI_ABI_VERSION 2
+ * rsmi_reconstruct_batch_host_verify were added; "crc16_fused_fold" is new.
+ * 3: no C++ exception crosses the boundary: every status-returning entry point that can allocate
+ * on the host returns RSMI_ERR_HOST instead (new status). */
+#define RSMI_ABI_VERSION 3
 
 typedef struct rsmi_ctx rsmi_ctx;
 
@@ -44,7 +46,9 @@ enum rsmi_status {
     RSMI_ERR_SINGULAR = 7,       /* matrix not invertible (cannot happen for valid patterns) */
     RSMI_ERR_INVALID_ARG = 8,    /* NULL pointer, stride smaller than a shard, ...          */
     RSMI_ERR_DEVICE = 100,       /* a HIP call failed                                       */
-    RSMI_ERR_NO_DEVICE = 101     /* no usable gfx950 device / kernels not loadable          */
+    RSMI_ERR_NO_DEVICE = 101,    /* no usable gfx950 device / kernels not loadable          */
+    RSMI_ERR_HOST = 102          /* host resources exhausted (memory, threads): a C++
+                                  * exception caught at the boundary, never propagated     */
 };
 
 /* ------------------------------------------------------------------ lifecycle */
