@@ -297,7 +297,7 @@ int rsmi_group_member_of_key(const rsmi_group* s, const uint8_t* key, size_t len
     return int(size_t(slot) * s->ctx.size() / kClusterSlots);
 }
 
-void* rsmi_group_host_alloc(rsmi_group* s, size_t block_bytes, size_t nblocks) {
+void* rsmi_group_host_alloc(rsmi_group* s, size_t block_bytes, size_t nblocks) try {
     if (!s || !block_bytes || !nblocks) return nullptr;
     const size_t page = size_t(sysconf(_SC_PAGESIZE));
     const size_t bytes = (block_bytes * nblocks + page - 1) / page * page;
@@ -333,6 +333,8 @@ void* rsmi_group_host_alloc(rsmi_group* s, size_t block_bytes, size_t nblocks) {
     std::lock_guard<std::mutex> g(s->alloc_mu);
     s->allocs[p] = bytes;
     return p;
+} catch (...) {
+    return nullptr;  // host allocation failed (a pinned range may stay mapped: never freed twice)
 }
 
 void rsmi_group_host_free(rsmi_group* s, void* p) {
