@@ -204,7 +204,11 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             void* cargs[] = {&tb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
             // a persistent grid of up to 8 workgroups per CU, 4 waves each, over (block, 4-row group) items
             const uint64_t items = nblocks * ((nsh + 3) / 4);
-            const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((items + 3) / 4, uint64_t(c->num_cu) * 8)));
+#ifndef RSMI_COMBINE_WGS_PER_CU
+#define RSMI_COMBINE_WGS_PER_CU 8
+#endif
+            const uint32_t grid = uint32_t(std::max<uint64_t>(
+                1, std::min<uint64_t>((items + 3) / 4, uint64_t(c->num_cu) * RSMI_COMBINE_WGS_PER_CU)));
             HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         }
         char buf[96];
