@@ -650,6 +650,9 @@ def main():
             "unit": "GB/s",
             "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
             "traffic": load_traffic(enc_kernel) if headline else None,
+            "traffic_source": ("profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE + WRITE_SIZE passes over this "
+                               "kernel (tools/gpu_session.sh prof), per launch, gfx950-corrected; refreshed each "
+                               "evidence session, not measured in this run") if headline else None,
             "kernel": enc_kernel + (" + its CRC-16 combine kernel" if a.fused_crc else ""),
             "algorithmic_bytes_per_launch": enc_bytes,
             "avg_launch_ms": round(enc_ms, 4),
