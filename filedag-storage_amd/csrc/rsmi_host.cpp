@@ -214,8 +214,19 @@ int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride,
                                            hipMemcpyHostToDevice, st.stream));
             if ((rc = repitch(st.d_in, Sp, st.d_lin, S, S, nb * k, st.stream))) return rc;
         }
-        if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) return rc;
-        if (raw_out) {  // R(shard) of the k data rows and the m parity rows, [block][row]
+        // one chunk (a latency-bound call): the encode with the CRC-16 fused in, one launch plus
+        // the combine, instead of the encode and two rows passes.  Several chunks run on three
+        // streams; the fused path's record buffer is one per context, so they keep the rows
+        // passes (which the PCIe copies hide).
+        const bool fused = raw_out && ns == 1 && S >= 16 && k <= 16 && m <= 4;
+        if (fused) {
+            uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n;
+            rc = launch_encode_crc(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, cr, st.stream);
+            if (rc) return rc;
+        } else if ((rc = launch_plan(c, *plan, st.d_in, Sp, in_bs, st.d_out, Sp, out_bs, S, nb, st.stream))) {
+            return rc;
+        }
+        if (raw_out && !fused) {  // R(shard) of the k data rows and the m parity rows, [block][row]
             uint32_t* cr = reinterpret_cast<uint32_t*>(c->d_crc) + b0 * n;
             HIP_TRY(hipMemsetAsync(cr, 0, nb * n * 4, st.stream));
             if ((rc = launch_crc(c, st.d_in, Sp, in_bs, uint32_t(k), S, nb, cr, n, st.stream, false))) return rc;
