@@ -90,6 +90,21 @@ Crc32Tables::Crc32Tables() {
     for (int i = 0; i < kCrc32SegPowers; i++) shift_columns(uint64_t(8192) << i, SC[i]);
     unshift_columns(8192, SC[kCrc32SegPowers]);
     for (int i = 0; i < kCrc32MisPowers; i++) shift_columns(uint64_t(1) << i, SC[kCrc32SegPowers + 1 + i]);
+    const uint32_t code4[4] = {4, 2, 1, 1};
+    for (int t = 0; t < kCrc32SegTiles; t++)
+        for (int s = 0; s < 4; s++)
+            for (int h = 0; h < 2; h++)
+                for (int l = 0; l < 64; l++) {
+                    const int j = l >> 4, n = 16 * h + (l & 15);
+                    for (int w = 0; w < 4; w++) MW[t][s][h][l][w] = 0;
+                    for (int e = 0; e < 32; e++) {
+                        // bit s of byte e >> 1's low (e even) or high (e odd) nibble, relative to the
+                        // chunk's end (N), then to the end of chunk 48 + m of tile 7
+                        const uint32_t c = shift(N[2 * (e >> 1) + (e & 1)][1u << s],
+                                                 uint64_t(256 * (3 - j) + 1024 * (kCrc32SegTiles - 1 - t)));
+                        if ((c >> n) & 1) MW[t][s][h][l][e / 8] |= code4[s] << (4 * (e % 8));
+                    }
+                }
     // A^-1 really inverts A, on a basis
     for (int bit = 0; bit < 32; bit++)
         if (apply(Q[0], apply(P[0], 1u << bit)) != (1u << bit)) std::abort();

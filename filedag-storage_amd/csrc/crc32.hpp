@@ -40,6 +40,13 @@ struct Crc32Tables {
     uint32_t SN[kCrc32ScanPowers][8][16];
     uint32_t SG[8][16];  // A^8192 nibble-sliced: the step between an item's 8-tile groups
     uint32_t SC[kCrc32SegPowers + 1 + kCrc32MisPowers][32];
+    // fp4 weight operands of the matrix-core rows pass (rs_crc32_rows_mfma_kernel), the CRC-16
+    // pass's MW with a 32-bit register: per tile t of an 8-tile group, bit group s (data bits s
+    // and s + 4 of every byte), half h (CRC bits 16 h .. 16 h + 15: one MFMA each), lane
+    // l = 16 j + n: nibble e of the lane's 16 bytes weighs data bit s + 4 (e & 1) of byte e >> 1
+    // of chunk 16 j + m for CRC bit 16 h + n, relative to the end of chunk 48 + m of the group's
+    // tile 7; fp4 codes 2.0 / 1.0 / 0.5 / 0.5 (s = 0..3) against data values 0.5 / 1 / 2 / 2
+    uint32_t MW[kCrc32SegTiles][4][2][64][4];
     Crc32Tables();
     static uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {
         return t[0][s & 0xFF] ^ t[1][(s >> 8) & 0xFF] ^ t[2][(s >> 16) & 0xFF] ^ t[3][s >> 24];

@@ -91,16 +91,10 @@ __device__ __forceinline__ uint32_t crc32_nib_chunk(const uint8_t* t, const u32x
 // moves by 8192 (q8 - gl - 1) + r8; a group that ends past S (the row's last one, r8 != 0) moves
 // back by 8192 (gl - q8 + 1) - r8.  Unaligned rows fold on the memory's grid, where every group
 // ends mis bytes earlier than on the row's (and a row may reach into group q8 + 1): mis more.
-__device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_t* sC, uint32_t col_r, uint32_t lane,
-                                               uint32_t l32, uint32_t acc, uint32_t gl, uint32_t q8, uint32_t mis,
-                                               uint32_t* word) {
-#pragma unroll
-    for (int j = 0; j < kCrc32ScanPowers; j++) {
-        const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
-        const uint32_t t = __shfl_up(w, 1u << j);
-        if (lane >= (1u << j)) acc ^= t;
-    }
-    uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // wave-uniform from here on
+// The shift of a wave-uniform value relative to the end of group gl to the row's end, then one
+// atomic XOR into the row's word (the second half of crc32_item_out).
+__device__ __forceinline__ void crc32_shift_out(const uint32_t* sC, uint32_t col_r, uint32_t lane, uint32_t l32,
+                                                uint32_t val, uint32_t gl, uint32_t q8, uint32_t mis, uint32_t* word) {
     if (gl < q8) {
         // whole segments, then the remainder r8
         uint32_t a = q8 - gl - 1;
@@ -114,6 +108,19 @@ __device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_
     for (int i = 0; i < kCrc32MisPowers; i++)
         if ((mis >> i) & 1) val = apply_lanes(sC[32 * (kCrc32SegPowers + 1 + i) + l32], val, l32);
     if (lane == 0) atomicXor(word, val);
+}
+
+__device__ __forceinline__ void crc32_item_out(const uint32_t* sS, const uint32_t* sC, uint32_t col_r, uint32_t lane,
+                                               uint32_t l32, uint32_t acc, uint32_t gl, uint32_t q8, uint32_t mis,
+                                               uint32_t* word) {
+#pragma unroll
+    for (int j = 0; j < kCrc32ScanPowers; j++) {
+        const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
+        const uint32_t t = __shfl_up(w, 1u << j);
+        if (lane >= (1u << j)) acc ^= t;
+    }
+    const uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), kWave - 1));  // wave-uniform from here on
+    crc32_shift_out(sC, col_r, lane, l32, val, gl, q8, mis, word);
 }
 
 // Position of item `it` (nsup items per row): its row, first tile and tile count.
@@ -267,6 +274,135 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
         if (!more) break;
         cur = nx;
     }
+}
+
+// The rows pass with the fold on the matrix cores: rs_crc16_rows_mfma_kernel (rs_kernels.hip)
+// with a 32-bit register.  B = the tile's data, one data bit per fp4 nibble (forms x & 0x11..,
+// 0x22.., 0x44.., (x >> 1) & 0x44..), column m = lane & 15, k block j = lane >> 4; two MFMAs per
+// form, A = the weights of CRC bits 0-15 and 16-31 of tile t of an 8-tile group (MW, 64 KiB of
+// LDS shared by a workgroup of 8 waves); a group's counts accumulate in two f32 quads (at most
+// 4096 per count, exact) and eight ballots give class m's 32-bit value in lane m (chunks m,
+// m + 16, m + 32, m + 48 of the group's tiles, relative to the end of chunk 48 + m of tile 7).
+// Groups step by A^8192 (SG); at the item's end a 4-level scan over lanes 0..15 (SN, A^(16 2^j))
+// takes lane 15 to the end of the item's last group, and crc32_shift_out moves it to the row's
+// end.  UA: the memory-grid fold of the CRC-16 pass (loads from the aligned chunk at or below the
+// row's first byte, its mis leading bytes masked, the end shift mis bytes longer).
+typedef int mfma32_v8i __attribute__((ext_vector_type(8)));
+typedef float mfma32_v4f __attribute__((ext_vector_type(4)));
+constexpr int kCrc32MfmaWG = 512;  // 8 waves share one staging of the 64 KiB of weights
+
+template <bool UA>
+__global__ __launch_bounds__(kCrc32MfmaWG) void rs_crc32_rows_mfma_kernel(
+    const uint32_t* __restrict__ tbl, const uint8_t* __restrict__ base, uint64_t bstride, uint64_t rpitch,
+    uint32_t nrows, uint64_t S, uint32_t tpb, uint32_t nseg, uint32_t nsup, uint64_t nitems,
+    uint32_t* __restrict__ out, uint64_t out_bs, Crc32Shift sh) {
+    __shared__ u32x4 s_w[kCrc32MWWords / 4];
+    __shared__ uint32_t s_pw[5 * kCrc32PowWords];  // SN[0..3] | SG
+    {
+        const u32x4* w = reinterpret_cast<const u32x4*>(tbl + kCrc32MWOff);
+        for (int i = threadIdx.x; i < kCrc32MWWords / 4; i += kCrc32MfmaWG) s_w[i] = w[i];
+        for (int i = threadIdx.x; i < 4 * kCrc32PowWords; i += kCrc32MfmaWG) s_pw[i] = tbl[kCrc32FoldWords + i];
+        for (int i = threadIdx.x; i < kCrc32PowWords; i += kCrc32MfmaWG)
+            s_pw[4 * kCrc32PowWords + i] = tbl[kCrc32FoldWords + 6 * kCrc32PowWords + i];
+    }
+    __syncthreads();
+    const uint32_t* sS = s_pw;
+    const uint32_t* sG = s_pw + 4 * kCrc32PowWords;
+    const uint32_t* sC = tbl + kCrc32LdsWords;
+    const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024));
+    const uint32_t l32 = threadIdx.x & 31;
+    uint32_t col_r = 0;  // A^r8, lane-distributed
+#pragma unroll
+    for (int b = 0; b < 32; b++) col_r = l32 == uint32_t(b) ? sh.col[b] : col_r;
+    constexpr uint32_t kWaves = kCrc32MfmaWG / kWave;
+    const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint64_t nw = uint64_t(gridDim.x) * kWaves;
+    for (uint64_t it = uint64_t(blockIdx.x) * kWaves + wid; it < nitems; it += nw) {
+        const Crc32Item x = crc32_item(it, nsup, nrows, tpb);
+        const uint8_t* row = base + x.b * bstride + uint64_t(x.r) * rpitch;
+        const uint32_t mis = UA ? uint32_t(__builtin_amdgcn_readfirstlane(int(reinterpret_cast<uintptr_t>(row) & 15u))) : 0u;
+        const uint8_t* rowa = row - mis;
+        const uint64_t Sm = mis + S;  // the row's end on the memory grid
+        const uint64_t lasta = (Sm - 1) / 16 * 16;
+        uint32_t acc = 0;  // lanes 0..15: class m's running value
+        for (uint32_t g0 = 0; g0 < x.nt; g0 += kCrc32SegTiles) {
+            const uint32_t t0 = x.t0 + g0;
+            const uint32_t nt = x.nt - g0 < uint32_t(kCrc32SegTiles) ? x.nt - g0 : uint32_t(kCrc32SegTiles);
+            u32x4 v[kCrc32SegTiles];
+#pragma unroll
+            for (int i = 0; i < kCrc32SegTiles; i++) {
+                const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
+                v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < lasta ? off : lasta)));
+            }
+            mfma32_v4f c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < kCrc32SegTiles; i++) {
+                if (uint32_t(i) < nt) {
+                    u32x4 d = v[i];
+                    if ((uint64_t(t0 + i) + 1) * (kWave * 16) > Sm) {  // wave-uniform: the row's last tile
+                        const int64_t valid = int64_t(Sm) - int64_t((uint64_t(t0 + i) * kWave + lane) * 16);
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const int64_t n = valid - 4 * w;
+                            d[w] &= n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+                        }
+                    }
+                    if (UA && t0 + i == 0 && mis != 0u && lane == 0) {  // the bytes before the row
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const int n = int(mis) - 4 * w;
+                            d[w] &= n >= 4 ? 0u : n <= 0 ? ~0u : ~((1u << (8 * n)) - 1u);
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        mfma32_v8i bd;
+#pragma unroll
+                        for (int w = 0; w < 4; w++)
+                            bd[w] = int(q < 3 ? d[w] & (0x11111111u << q) : (d[w] >> 1) & 0x44444444u);
+                        bd[4] = bd[5] = bd[6] = bd[7] = 0;
+                        const u32x4 w0 = s_w[((i * 4 + q) * 2 + 0) * kWave + lane];
+                        const u32x4 w1 = s_w[((i * 4 + q) * 2 + 1) * kWave + lane];
+                        const mfma32_v8i a0 = {int(w0[0]), int(w0[1]), int(w0[2]), int(w0[3]), 0, 0, 0, 0};
+                        const mfma32_v8i a1 = {int(w1[0]), int(w1[1]), int(w1[2]), int(w1[3]), 0, 0, 0, 0};
+                        c0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a0, bd, c0, 4, 4, 0, 127, 0, 127);
+                        c1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a1, bd, c1, 4, 4, 0, 127, 0, 127);
+                    }
+                }
+            }
+            // parity bits -> class m's 32-bit value: bit n of half h is bit 16 (n >> 2) + m of
+            // ballot n & 3 of that half's accumulator
+            uint32_t Y0 = 0, Y1 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint64_t b0 = __builtin_amdgcn_ballot_w64((int(c0[i]) & 1) != 0);
+                const uint64_t b1 = __builtin_amdgcn_ballot_w64((int(c1[i]) & 1) != 0);
+                const uint32_t lo0 = uint32_t(b0) >> m, hi0 = uint32_t(b0 >> 32) >> m;
+                const uint32_t lo1 = uint32_t(b1) >> m, hi1 = uint32_t(b1 >> 32) >> m;
+                Y0 |= ((lo0 & 0x10001u) | ((hi0 & 0x10001u) << 8)) << i;
+                Y1 |= ((lo1 & 0x10001u) | ((hi1 & 0x10001u) << 8)) << i;
+            }
+            const uint32_t val = ((Y0 & 0x0F0Fu) | ((Y0 >> 12) & 0xF0F0u)) |
+                                 (((Y1 & 0x0F0Fu) | ((Y1 >> 12) & 0xF0F0u)) << 16);
+            acc = (g0 == 0 ? 0u : pow_nib(sG, acc)) ^ val;  // earlier groups move 8 KiB further from the end
+        }
+        // classes -> the end of the item's last group: lane 15 takes sum_m A^(16 (15 - m)) (class m)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t w = pow_nib(sS + j * kCrc32PowWords, acc);  // 16 * 2^j bytes
+            const uint32_t t = __shfl_up(w, 1u << j);
+            if (m >= (1u << j)) acc ^= t;
+        }
+        const uint32_t val = uint32_t(__builtin_amdgcn_readlane(int(acc), 15));  // wave-uniform from here
+        crc32_shift_out(sC, col_r, lane, l32, val, (x.t0 + x.nt - 1) / kCrc32SegTiles, q8, mis,
+                        out + x.b * out_bs + x.r);
+    }
+}
+
+void* crc32_rows_mfma_kernel(bool aligned) {
+    return aligned ? reinterpret_cast<void*>(&rs_crc32_rows_mfma_kernel<false>)
+                   : reinterpret_cast<void*>(&rs_crc32_rows_mfma_kernel<true>);
 }
 
 void* crc32_rows_kernel(bool aligned) {

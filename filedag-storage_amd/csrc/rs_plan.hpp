@@ -88,7 +88,12 @@ constexpr int kFusedWavesPerSimd = RSMI_FUSED_WPS;  // its register budget: 168 
 constexpr int kCrc32FoldWords = 8 * 32 * 16;
 constexpr int kCrc32PowWords = 8 * 16;  // one nibble-sliced power
 constexpr int kCrc32LdsWords = kCrc32FoldWords + 7 * kCrc32PowWords;  // NT | SN[6] | SG
-constexpr int kCrc32TableWords = kCrc32LdsWords + 24 * 32;
+#ifndef RSMI_CRC32_FOLD_DEFAULT
+#define RSMI_CRC32_FOLD_DEFAULT 1
+#endif
+constexpr int kCrc32MWOff = kCrc32LdsWords + 24 * 32;       // MW[8][4][2][64][4] (matrix-core pass)
+constexpr int kCrc32MWWords = 8 * 4 * 2 * 64 * 4;
+constexpr int kCrc32TableWords = kCrc32MWOff + kCrc32MWWords;
 // per-launch shift to the row's end, column form (crc32.hpp), passed by value: A^(S mod 8192),
 // the end of an inner segment moved over whatever of the row follows whole segments
 struct Crc32Shift {
@@ -104,5 +109,6 @@ void* crc16_rows_mfma_kernel(bool aligned);  // the fold on the matrix cores (un
 void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8, rounded up)
 void* crc16_combine_mfma_kernel();    // records of rs_fused_mfma_kernel
 void* crc32_rows_kernel(bool aligned);
+void* crc32_rows_mfma_kernel(bool aligned);  // the fold on the matrix cores (512-thread workgroups)
 
 }  // namespace rsmi

@@ -400,6 +400,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     } else if (!std::strcmp(key, "crc16_fold")) {
         if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
         c->opt_crc16_fold = int(value);
+    } else if (!std::strcmp(key, "crc32_fold")) {
+        if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_crc32_fold = int(value);
     } else if (!std::strcmp(key, "crc16_fused_fold")) {
         if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
         c->opt_fused_fold = int(value);

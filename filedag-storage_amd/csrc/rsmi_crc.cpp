@@ -73,13 +73,15 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 int ensure_crc32_tables(rsmi_ctx* c) {
     if (c->d_crc32_tbl) return RSMI_OK;
     const Crc32Tables& t = crc32_tables();
-    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SG) + sizeof(t.SC) == size_t(kCrc32TableWords) * 4,
+    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SG) + sizeof(t.SC) + sizeof(t.MW) == size_t(kCrc32TableWords) * 4,
                   "CRC-32 table layout");
+    static_assert(sizeof(t.MW) == size_t(kCrc32MWWords) * 4, "CRC-32 MFMA weights");
     std::vector<uint32_t> h(static_cast<size_t>(kCrc32TableWords));
     std::memcpy(h.data(), t.NT, sizeof(t.NT));
     std::memcpy(h.data() + kCrc32FoldWords, t.SN, sizeof(t.SN));
     std::memcpy(h.data() + kCrc32FoldWords + 6 * kCrc32PowWords, t.SG, sizeof(t.SG));
     std::memcpy(h.data() + kCrc32LdsWords, t.SC, sizeof(t.SC));
+    std::memcpy(h.data() + kCrc32MWOff, t.MW, sizeof(t.MW));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc32_tbl), h.size() * 4));
     HIP_TRY(hipMemcpy(c->d_crc32_tbl, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -94,7 +96,8 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     int rc = ensure_crc32_tables(c);
     if (rc) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(base) % 16 == 0 && rpitch % 16 == 0 && bstride % 16 == 0;
-    void* fn = crc32_rows_kernel(aligned);
+    const bool mfma = c->opt_crc32_fold == 1;
+    void* fn = mfma ? crc32_rows_mfma_kernel(aligned) : crc32_rows_kernel(aligned);
     const uint64_t tile = uint64_t(kWave) * 16, span = tile * kCrc32SegTiles;
     if (S / span >= (uint64_t(1) << kCrc32SegPowers)) return RSMI_ERR_INVALID_ARG;  // rows below 4 GiB
     // unaligned rows fold on the memory's 16-byte grid, where a row spans its misalignment + S bytes
@@ -109,12 +112,16 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     Crc32Shift sh = c->crc32_shift;
     uint64_t nitems = nblocks * nrows * nsup;
     // 96 waves per CU as for the CRC-16 pass
-    uint64_t cap = uint64_t(c->num_cu) * 96 / 4;
-    if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / 4);
-    const uint64_t wgs = std::min<uint64_t>((nitems + 3) / 4, cap);
+    // (the matrix-core pass: workgroups of 8 waves, 2 resident per CU by its 66 KiB of LDS, each
+    // staging the 64 KiB of weights: 48 waves per CU, three rounds, measured best of 16-96,
+    // profiles/r03/crc/crc32_mfma_wpc.txt)
+    const uint64_t wpg = mfma ? 8 : 4;
+    uint64_t cap = uint64_t(c->num_cu) * (mfma ? 48 : 96) / wpg;
+    if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / wpg);
+    const uint64_t wgs = std::min<uint64_t>((nitems + wpg - 1) / wpg, cap);
     const uint32_t* tb = c->d_crc32_tbl;
     void* args[] = {&tb, &base, &bstride, &rpitch, &nrows, &S, &tpb, &nseg, &nsup, &nitems, &out, &out_bs, &sh};
-    HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(kWG), args, 0, stream));
+    HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
     return RSMI_OK;
 }
 
@@ -318,7 +325,7 @@ int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     rc = launch_crc32(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
                       st);
     if (rc) return rc;
-    c->last_kernel = "rs_crc32_rows_kernel";
+    c->last_kernel = c->opt_crc32_fold == 1 ? "rs_crc32_rows_kernel,MFMA" : "rs_crc32_rows_kernel";
     return hip_status(hipGetLastError());
 } catch (...) {
     return rsmi::impl::exception_status();

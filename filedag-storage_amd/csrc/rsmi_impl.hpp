@@ -100,6 +100,7 @@ struct rsmi_ctx {
     size_t fctr_cap = 0;
     // options
     int opt_crc16_fold = 1;     // aligned CRC-16 rows pass: 0 = nibble tables, 1 = matrix cores (fp4)
+    int opt_crc32_fold = RSMI_CRC32_FOLD_DEFAULT;  // CRC-32 rows pass: 0 = nibble tables, 1 = matrix cores
     int opt_fused_fold = 1;     // aligned fused encode + CRC-16: 0 = nibble tables, 1 = matrix cores (fp4)
     long opt_waves_per_cu = 0;  // grid cap (0 = one tile per wave / the CRC passes' defaults)
     int opt_zero_copy = 1;  // results into page-locked host buffers by kernel stores

@@ -69,7 +69,8 @@ def test_oracle_mutcask_entry_crc_is_checksum_of_framed_entry():
                                32768, 32769, 40961, 65536, 73729, 104858, 262144, 1048579])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 @pytest.mark.parametrize("wpc", [0, 1])
-def test_rows_dev_matches_zlib(S, layout, wpc):
+@pytest.mark.parametrize("fold", [1, 0])
+def test_rows_dev_matches_zlib(S, layout, wpc, fold):
     import torch
 
     nrows, nb = 3, 5
@@ -83,9 +84,10 @@ def test_rows_dev_matches_zlib(S, layout, wpc):
     out = torch.full((nb, nrows + 1), 0xDEAD, dtype=torch.int32, device="cuda")
     with rsmi.Codec(4, 2) as c:
         c.set_option("waves_per_cu", wpc)
+        c.set_option("crc32_fold", fold)
         c.crc32_rows_dev(dev.data_ptr() + off, pitch, nrows * pitch, nrows, S, nb, out.data_ptr(), nrows + 1)
         torch.cuda.synchronize()
-        assert c.last_kernel() == "rs_crc32_rows_kernel"
+        assert c.last_kernel() == ("rs_crc32_rows_kernel,MFMA" if fold else "rs_crc32_rows_kernel")
     got = out.cpu().numpy().astype(np.int64) & M32
     h = host.numpy()
     for b in range(nb):
@@ -109,16 +111,18 @@ def test_rows_dev_split_layout_every_misalignment(S):
         g = torch.Generator().manual_seed(S * 7 + off)
         host = torch.randint(0, 256, (off + nb * nrows * S + 64,), dtype=torch.uint8, generator=g)
         dev = host.to("cuda")
-        out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
-        with rsmi.Codec(4, 2) as c:
-            c.crc32_rows_dev(dev.data_ptr() + off, S, nrows * S, nrows, S, nb, out.data_ptr(), nrows)
-            torch.cuda.synchronize()
-        got = out.cpu().numpy().astype(np.int64) & M32
         h = host.numpy()
-        for b in range(nb):
-            for r in range(nrows):
-                row = h[off + (b * nrows + r) * S:][:S].tobytes()
-                assert got[b, r] == raw32(row), (off, b, r)
+        for fold in (1, 0):
+            out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+            with rsmi.Codec(4, 2) as c:
+                c.set_option("crc32_fold", fold)
+                c.crc32_rows_dev(dev.data_ptr() + off, S, nrows * S, nrows, S, nb, out.data_ptr(), nrows)
+                torch.cuda.synchronize()
+            got = out.cpu().numpy().astype(np.int64) & M32
+            for b in range(nb):
+                for r in range(nrows):
+                    row = h[off + (b * nrows + r) * S:][:S].tobytes()
+                    assert got[b, r] == raw32(row), (off, fold, b, r)
 
 
 @pytest.mark.gpu
@@ -140,15 +144,17 @@ def test_rows_dev_random_unaligned_shapes():
         host = torch.randint(0, 256, (off + nb * bstride + 64,), dtype=torch.uint8, generator=g)
         dev = host.to("cuda")
         h = host.numpy()
-        out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
-        with rsmi.Codec(4, 2) as c:
-            c.crc32_rows_dev(dev.data_ptr() + off, pitch, bstride, nrows, S, nb, out.data_ptr(), nrows)
-            torch.cuda.synchronize()
-        got = out.cpu().numpy().astype(np.int64) & M32
-        for b in range(nb):
-            for r in range(nrows):
-                row = h[off + b * bstride + r * pitch:][:S].tobytes()
-                assert got[b, r] == raw32(row), (S, off, pitch, bstride, b, r)
+        for fold in (1, 0):
+            out = torch.zeros((nb, nrows), dtype=torch.int32, device="cuda")
+            with rsmi.Codec(4, 2) as c:
+                c.set_option("crc32_fold", fold)
+                c.crc32_rows_dev(dev.data_ptr() + off, pitch, bstride, nrows, S, nb, out.data_ptr(), nrows)
+                torch.cuda.synchronize()
+            got = out.cpu().numpy().astype(np.int64) & M32
+            for b in range(nb):
+                for r in range(nrows):
+                    row = h[off + b * bstride + r * pitch:][:S].tobytes()
+                    assert got[b, r] == raw32(row), (S, off, pitch, bstride, fold, b, r)
 
 
 @pytest.mark.gpu
