@@ -87,6 +87,8 @@ Crc32Tables::Crc32Tables() {
             for (int v = 0; v < 16; v++) SN[j][h][v] = apply(P[4 + j], uint32_t(v) << (4 * h));
     for (int h = 0; h < 8; h++)
         for (int v = 0; v < 16; v++) SG[h][v] = apply(P[13], uint32_t(v) << (4 * h));
+    for (int h = 0; h < 8; h++)
+        for (int v = 0; v < 16; v++) SG4[h][v] = apply(P[12], uint32_t(v) << (4 * h));
     for (int i = 0; i < kCrc32SegPowers; i++) shift_columns(uint64_t(8192) << i, SC[i]);
     unshift_columns(8192, SC[kCrc32SegPowers]);
     for (int i = 0; i < kCrc32MisPowers; i++) shift_columns(uint64_t(1) << i, SC[kCrc32SegPowers + 1 + i]);

@@ -47,6 +47,7 @@ struct Crc32Tables {
     // of chunk 16 j + m for CRC bit 16 h + n, relative to the end of chunk 48 + m of the group's
     // tile 7; fp4 codes 2.0 / 1.0 / 0.5 / 0.5 (s = 0..3) against data values 0.5 / 1 / 2 / 2
     uint32_t MW[kCrc32SegTiles][4][2][64][4];
+    uint32_t SG4[8][16];  // A^4096 nibble-sliced: the half-group step of the matrix-core pass
     Crc32Tables();
     static uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {
         return t[0][s & 0xFF] ^ t[1][(s >> 8) & 0xFF] ^ t[2][(s >> 16) & 0xFF] ^ t[3][s >> 24];

@@ -289,25 +289,29 @@ __global__ __launch_bounds__(kWG) void rs_crc32_rows_pipe_kernel(const uint32_t*
 // row's first byte, its mis leading bytes masked, the end shift mis bytes longer).
 typedef int mfma32_v8i __attribute__((ext_vector_type(8)));
 typedef float mfma32_v4f __attribute__((ext_vector_type(4)));
-constexpr int kCrc32MfmaWG = 512;  // 8 waves share one staging of the 64 KiB of weights
 
 template <bool UA>
 __global__ __launch_bounds__(kCrc32MfmaWG) void rs_crc32_rows_mfma_kernel(
     const uint32_t* __restrict__ tbl, const uint8_t* __restrict__ base, uint64_t bstride, uint64_t rpitch,
     uint32_t nrows, uint64_t S, uint32_t tpb, uint32_t nseg, uint32_t nsup, uint64_t nitems,
     uint32_t* __restrict__ out, uint64_t out_bs, Crc32Shift sh) {
-    __shared__ u32x4 s_w[kCrc32MWWords / 4];
-    __shared__ uint32_t s_pw[5 * kCrc32PowWords];  // SN[0..3] | SG
+    constexpr int kWWords = kCrc32MWWords * kCrc32MfmaTiles / kCrc32SegTiles;  // the staged tiles' weights
+    __shared__ u32x4 s_w[kWWords / 4];
+    __shared__ uint32_t s_pw[6 * kCrc32PowWords];  // SN[0..3] | SG | SG4
     {
-        const u32x4* w = reinterpret_cast<const u32x4*>(tbl + kCrc32MWOff);
-        for (int i = threadIdx.x; i < kCrc32MWWords / 4; i += kCrc32MfmaWG) s_w[i] = w[i];
+        // half groups: tiles 4..7 of MW weigh a half group's tiles relative to its end
+        const u32x4* w = reinterpret_cast<const u32x4*>(tbl + kCrc32MWOff + (kCrc32MWWords - kWWords));
+        for (int i = threadIdx.x; i < kWWords / 4; i += kCrc32MfmaWG) s_w[i] = w[i];
         for (int i = threadIdx.x; i < 4 * kCrc32PowWords; i += kCrc32MfmaWG) s_pw[i] = tbl[kCrc32FoldWords + i];
-        for (int i = threadIdx.x; i < kCrc32PowWords; i += kCrc32MfmaWG)
+        for (int i = threadIdx.x; i < kCrc32PowWords; i += kCrc32MfmaWG) {
             s_pw[4 * kCrc32PowWords + i] = tbl[kCrc32FoldWords + 6 * kCrc32PowWords + i];
+            s_pw[5 * kCrc32PowWords + i] = tbl[kCrc32SG4Off + i];
+        }
     }
     __syncthreads();
     const uint32_t* sS = s_pw;
     const uint32_t* sG = s_pw + 4 * kCrc32PowWords;
+    const uint32_t* sG4 = s_pw + 5 * kCrc32PowWords;
     const uint32_t* sC = tbl + kCrc32LdsWords;
     const uint32_t q8 = uint32_t(S / (kCrc32SegTiles * 1024));
     const uint32_t l32 = threadIdx.x & 31;
@@ -335,9 +339,12 @@ __global__ __launch_bounds__(kCrc32MfmaWG) void rs_crc32_rows_mfma_kernel(
                 const uint64_t off = (uint64_t(t0 + i) * kWave + lane) * 16;  // unconditional, clamped
                 v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowa + (off < lasta ? off : lasta)));
             }
+            uint32_t gval = 0;  // the group's value, relative to its end
+#pragma unroll
+            for (int hh = 0; hh < kCrc32SegTiles / kCrc32MfmaTiles; hh++) {
             mfma32_v4f c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < kCrc32SegTiles; i++) {
+            for (int i = hh * kCrc32MfmaTiles; i < (hh + 1) * kCrc32MfmaTiles; i++) {
                 if (uint32_t(i) < nt) {
                     u32x4 d = v[i];
                     if ((uint64_t(t0 + i) + 1) * (kWave * 16) > Sm) {  // wave-uniform: the row's last tile
@@ -362,8 +369,9 @@ __global__ __launch_bounds__(kCrc32MfmaWG) void rs_crc32_rows_mfma_kernel(
                         for (int w = 0; w < 4; w++)
                             bd[w] = int(q < 3 ? d[w] & (0x11111111u << q) : (d[w] >> 1) & 0x44444444u);
                         bd[4] = bd[5] = bd[6] = bd[7] = 0;
-                        const u32x4 w0 = s_w[((i * 4 + q) * 2 + 0) * kWave + lane];
-                        const u32x4 w1 = s_w[((i * 4 + q) * 2 + 1) * kWave + lane];
+                        const int ti = i % kCrc32MfmaTiles;  // the tile's weights (relative to the read-out's end)
+                        const u32x4 w0 = s_w[((ti * 4 + q) * 2 + 0) * kWave + lane];
+                        const u32x4 w1 = s_w[((ti * 4 + q) * 2 + 1) * kWave + lane];
                         const mfma32_v8i a0 = {int(w0[0]), int(w0[1]), int(w0[2]), int(w0[3]), 0, 0, 0, 0};
                         const mfma32_v8i a1 = {int(w1[0]), int(w1[1]), int(w1[2]), int(w1[3]), 0, 0, 0, 0};
                         c0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a0, bd, c0, 4, 4, 0, 127, 0, 127);
@@ -385,7 +393,9 @@ __global__ __launch_bounds__(kCrc32MfmaWG) void rs_crc32_rows_mfma_kernel(
             }
             const uint32_t val = ((Y0 & 0x0F0Fu) | ((Y0 >> 12) & 0xF0F0u)) |
                                  (((Y1 & 0x0F0Fu) | ((Y1 >> 12) & 0xF0F0u)) << 16);
-            acc = (g0 == 0 ? 0u : pow_nib(sG, acc)) ^ val;  // earlier groups move 8 KiB further from the end
+            gval = (hh == 0 ? 0u : pow_nib(sG4, gval)) ^ val;  // an earlier half moves 4 KiB further
+            }
+            acc = (g0 == 0 ? 0u : pow_nib(sG, acc)) ^ gval;  // earlier groups move 8 KiB further from the end
         }
         // classes -> the end of the item's last group: lane 15 takes sum_m A^(16 (15 - m)) (class m)
 #pragma unroll

@@ -93,7 +93,17 @@ constexpr int kCrc32LdsWords = kCrc32FoldWords + 7 * kCrc32PowWords;  // NT | SN
 #endif
 constexpr int kCrc32MWOff = kCrc32LdsWords + 24 * 32;       // MW[8][4][2][64][4] (matrix-core pass)
 constexpr int kCrc32MWWords = 8 * 4 * 2 * 64 * 4;
-constexpr int kCrc32TableWords = kCrc32MWOff + kCrc32MWWords;
+// RSMI_CRC32_MFMA_HALF 1: the matrix-core CRC-32 pass reads the parity per half group (4 tiles,
+// weights MW[4..7], 32 KiB, the halves joined by A^4096), so 4-wave workgroups stage half the
+// weights; 0: per 8-tile group, all 64 KiB staged by 8-wave workgroups
+#ifndef RSMI_CRC32_MFMA_HALF
+#define RSMI_CRC32_MFMA_HALF 0
+#endif
+constexpr bool kCrc32MfmaHalf = RSMI_CRC32_MFMA_HALF;
+constexpr int kCrc32MfmaWG = kCrc32MfmaHalf ? 256 : 512;
+constexpr int kCrc32MfmaTiles = kCrc32MfmaHalf ? 4 : 8;  // tiles per parity read-out
+constexpr int kCrc32SG4Off = kCrc32MWOff + kCrc32MWWords;  // SG4[8][16]: A^4096, nibble-sliced
+constexpr int kCrc32TableWords = kCrc32SG4Off + 8 * 16;
 // per-launch shift to the row's end, column form (crc32.hpp), passed by value: A^(S mod 8192),
 // the end of an inner segment moved over whatever of the row follows whole segments
 struct Crc32Shift {

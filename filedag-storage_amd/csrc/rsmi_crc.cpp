@@ -73,7 +73,8 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 int ensure_crc32_tables(rsmi_ctx* c) {
     if (c->d_crc32_tbl) return RSMI_OK;
     const Crc32Tables& t = crc32_tables();
-    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SG) + sizeof(t.SC) + sizeof(t.MW) == size_t(kCrc32TableWords) * 4,
+    static_assert(sizeof(t.NT) + sizeof(t.SN) + sizeof(t.SG) + sizeof(t.SC) + sizeof(t.MW) + sizeof(t.SG4) ==
+                      size_t(kCrc32TableWords) * 4,
                   "CRC-32 table layout");
     static_assert(sizeof(t.MW) == size_t(kCrc32MWWords) * 4, "CRC-32 MFMA weights");
     std::vector<uint32_t> h(static_cast<size_t>(kCrc32TableWords));
@@ -82,6 +83,7 @@ int ensure_crc32_tables(rsmi_ctx* c) {
     std::memcpy(h.data() + kCrc32FoldWords + 6 * kCrc32PowWords, t.SG, sizeof(t.SG));
     std::memcpy(h.data() + kCrc32LdsWords, t.SC, sizeof(t.SC));
     std::memcpy(h.data() + kCrc32MWOff, t.MW, sizeof(t.MW));
+    std::memcpy(h.data() + kCrc32SG4Off, t.SG4, sizeof(t.SG4));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_crc32_tbl), h.size() * 4));
     HIP_TRY(hipMemcpy(c->d_crc32_tbl, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     return RSMI_OK;
@@ -115,8 +117,8 @@ int launch_crc32(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bst
     // (the matrix-core pass: workgroups of 8 waves, 2 resident per CU by its 66 KiB of LDS, each
     // staging the 64 KiB of weights: 48 waves per CU, three rounds, measured best of 16-96,
     // profiles/r03/crc/crc32_mfma_wpc.txt)
-    const uint64_t wpg = mfma ? 8 : 4;
-    uint64_t cap = uint64_t(c->num_cu) * (mfma ? 48 : 96) / wpg;
+    const uint64_t wpg = mfma ? uint64_t(kCrc32MfmaWG) / kWave : 4;
+    uint64_t cap = uint64_t(c->num_cu) * (mfma && !kCrc32MfmaHalf ? 48 : 96) / wpg;
     if (c->opt_waves_per_cu > 0) cap = std::max<uint64_t>(1, uint64_t(c->num_cu) * uint64_t(c->opt_waves_per_cu) / wpg);
     const uint64_t wgs = std::min<uint64_t>((nitems + wpg - 1) / wpg, cap);
     const uint32_t* tb = c->d_crc32_tbl;
