@@ -1248,7 +1248,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_combine_mfma_kernel(const uint32
     for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = tbl[kCrcP4Off + i];
     __syncthreads();
     const uint16_t* sQ = reinterpret_cast<const uint16_t*>(s_p4);
-    const uint32_t lane = threadIdx.x & (kWave - 1), m = lane & 15u, g = lane >> 4;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t npass = (nsh + 3) / 4;  // wave-uniform
     const uint64_t nitems = nblocks * npass, nw = uint64_t(gridDim.x) * (kWG / kWave);
