@@ -37,8 +37,22 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "filedag-storage_amd"))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
+# numpy and torch load after the launcher decision (main) or on import as a module: the launcher
+# of `--gpus N` must not map or initialise the HIP runtime before it spawns the ranks (torch links
+# libamdhip64, so importing it maps the runtime).
+np = torch = None
+
+
+def _heavy_imports():
+    global np, torch
+    import numpy
+    import torch as _torch
+
+    np, torch = numpy, _torch
+
+
+if __name__ != "__main__":
+    _heavy_imports()
 
 METRIC = "GiB/s device-resident RS encode+reconstruct, 256 KiB blocks; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -109,13 +123,26 @@ def _free_port():
 
 
 def launch(a):
-    """--gpus N with no launcher: start N ranks of this script, one per GPU, before anything
-    here touches the GPU (torch.cuda.device_count() does not initialise it), and exit with the
-    first failing rank's code."""
-    if not (a.share_device or a.mock):
-        have = torch.cuda.device_count()
-        if have < a.gpus:
-            raise SystemExit(f"bench.py --gpus {a.gpus}: only {have} GPU(s) visible")
+    """--gpus N with no launcher: start N ranks of this script, one per GPU, and exit with the
+    first failing rank's code.  Nothing here maps or initialises the HIP runtime: numpy and
+    torch are not imported yet, and the GPUs are counted from sysfs (rsmi.multi.visible_gpu_count,
+    honouring ROCR/HIP_VISIBLE_DEVICES), or by a child process where sysfs has no KFD topology.
+    --share-device (a rehearsal on one GPU) needs one visible GPU, --mock none."""
+    from rsmi import multi
+
+    need = 0 if a.mock else (1 if a.share_device else a.gpus)
+    have = None
+    if need:
+        have = multi.visible_gpu_count()
+        if have is None:  # no KFD topology in sysfs: a child process counts (and initialises HIP)
+            out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                                 capture_output=True, text=True)
+            have = int(out.stdout.strip() or "0") if out.returncode == 0 else 0
+    probe = os.environ.get("RSMI_BENCH_LAUNCH_PROBE")
+    if probe:  # test hook: what this process has mapped and opened at spawn time
+        _launch_probe(probe, have)
+    if need and have < need:
+        raise SystemExit(f"bench.py --gpus {a.gpus}: only {have} GPU(s) visible")
     port = _free_port()
     procs = []
     for r in range(a.gpus):
@@ -135,6 +162,24 @@ def launch(a):
                     q.terminate()
         time.sleep(0.05)
     return rc
+
+
+def _launch_probe(path, have):
+    """Record the launcher's state just before it spawns ranks: shared objects of the HIP / HSA
+    runtimes mapped into this process (/proc/self/maps), descriptors open on /dev/kfd (the
+    runtime opens it when it initialises), and whether torch or numpy were imported."""
+    with open("/proc/self/maps") as f:
+        maps = sorted({ln.split()[-1] for ln in f if len(ln.split()) >= 6})
+    hip = [m for m in maps if any(x in os.path.basename(m) for x in ("libamdhip64", "libhsa-runtime"))]
+    kfd = 0
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            kfd += os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd"
+        except OSError:
+            pass
+    with open(path, "w") as f:
+        json.dump({"gpus_counted": have, "hip_libs_mapped": hip, "kfd_fds": kfd,
+                   "torch_imported": "torch" in sys.modules, "numpy_imported": "numpy" in sys.modules}, f)
 
 
 _JSON_OUT = None  # multi-rank: the real stdout, kept for the one JSON line
@@ -314,7 +359,8 @@ def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds, world=1):
         "kind": "port",
         "sample": f"{reps} passes x the bench's own {nb} blocks of {B // 1024} KiB RS({k},{m}) {what}, "
                   f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s"
-                  + (f"; rank 0 of {world}, timed after every rank's GPU legs finished" if world > 1 else ""),
+                  + (f"; rank 0 of {world}, timed after every rank's GPU legs finished, the other ranks idle at a "
+                     "barrier" if world > 1 else ""),
         "single_core_value": round(reps1 * nb * B / el1 / 2**30, 3),
         "host_cpus": os.cpu_count(),
         "ranks": world,
@@ -492,6 +538,7 @@ def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         return launch(a)
+    _heavy_imports()
     world, rank, local = dist_setup()
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
@@ -683,7 +730,8 @@ def main():
                                                world, group)
     if rank == 0 and a.cpu_seconds > 0:
         # every rank's GPU legs are done (gather above), so the host cores are free; at N > 1 the
-        # other ranks exit while rank 0 times the CPU codec on its own share of the job's blocks
+        # other ranks wait idle at finish()'s barrier (their processes stay alive, sleeping) while
+        # rank 0 times the CPU codec on its own share of the job's blocks
         data_host = lay.rows(buf, 0, k).cpu().numpy()  # the bench's own blocks
         out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds, world)
     if rank == 0:

@@ -41,7 +41,19 @@ public:
             if (wait_us > 0 && pending_.size() < cap)
                 cv_.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return pending_.size() >= cap; });
             const size_t take = std::min(cap, pending_.size());
-            std::vector<Req*> batch(pending_.begin(), pending_.begin() + take);
+            std::vector<Req*> batch;
+            try {
+                batch.assign(pending_.begin(), pending_.begin() + take);
+            } catch (...) {  // no memory for the batch list: fail these requests in place
+                for (size_t i = 0; i < take; i++) {
+                    pending_[i]->rc = fail_rc_;
+                    pending_[i]->done = true;
+                }
+                pending_.erase(pending_.begin(), pending_.begin() + take);
+                executing_ = false;
+                cv_.notify_all();
+                continue;
+            }
             pending_.erase(pending_.begin(), pending_.begin() + take);
             lk.unlock();
             try {

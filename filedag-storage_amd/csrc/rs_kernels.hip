@@ -181,13 +181,19 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         // boundary at or below it (a 4-byte-aligned dwordx4 plus the dword after it) and
         // funnel-shifted by the window's byte offset in that dword (v_alignbyte_b32), instead of
         // one byte-aligned 16-byte load: +7% on the Split layout's RS(10,4) 1-row reconstruct
-        // (4.78 -> 5.11 TB/s, profiles/r03/ua/ua4_ab.txt).  Every dword loaded holds a byte of the row.
+        // (4.78 -> 5.11 TB/s, profiles/r03/ua/ua4_ab.txt).  Every dword loaded holds a byte of the
+        // row: the dwordx4 holds the window's first byte, and the extra dword is the one holding its
+        // last byte, (p + 15) & ~3.  That is the dword after the dwordx4 when the window is not
+        // 4-aligned; when it is (r == 0: a row's last window at S - 16 with S a multiple of 4, as in
+        // a page-exact buffer), it is the dwordx4's own last dword again, never the dword at S, and
+        // alignbyte with r == 0 ignores it.
         constexpr bool UA4 = UA && (RSMI_UA_DWORD_LOADS == 2 || (NT == 2 && RSMI_UA_DWORD_LOADS == 1));
-        uint32_t vx[UA4 ? P : 1];  // UA4: the dword after each row's window
+        uint32_t vx[UA4 ? P : 1];  // UA4: the dword holding each row's window's last byte
         auto load_col = [&](int c) {
             if constexpr (UA4) {
-                const uintptr_t a = reinterpret_cast<uintptr_t>(ib + in_off[c] + win) & ~uintptr_t(3);
-                vx[c % P] = *reinterpret_cast<const uint32_t*>(a + 16);
+                const uintptr_t p = reinterpret_cast<uintptr_t>(ib + in_off[c] + win);
+                const uintptr_t a = p & ~uintptr_t(3);
+                vx[c % P] = *reinterpret_cast<const uint32_t*>((p + 15) & ~uintptr_t(3));
                 return u32x4(*reinterpret_cast<const u32x4a4*>(a));
             } else if constexpr (UA) {
                 // nontemporal loads for write-heavy tiles; read-heavy UA tiles keep the lines

@@ -76,6 +76,9 @@ void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
 
 void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
     const size_t n = size_t(c->n);
+    // test hook (option "inject_host_fault"): this batch fails as a host allocation would
+    for (int v = c->opt_inject_host_fault.load(); v > 0;)
+        if (c->opt_inject_host_fault.compare_exchange_weak(v, v - 1)) throw std::bad_alloc();
     std::map<std::string, std::vector<rsmi_ctx::CoalReq*>> groups;
     for (auto* r : batch) groups[r->key].push_back(r);
     for (auto& g : groups) {

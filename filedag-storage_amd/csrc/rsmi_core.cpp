@@ -409,6 +409,9 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     } else if (!std::strcmp(key, "waves_per_cu")) {
         if (value < 0) return RSMI_ERR_INVALID_ARG;
         c->opt_waves_per_cu = value;
+    } else if (!std::strcmp(key, "inject_host_fault")) {
+        if (value < 0 || value > 1000) return RSMI_ERR_INVALID_ARG;
+        c->opt_inject_host_fault.store(int(value));
     } else {
         return RSMI_ERR_INVALID_ARG;
     }

@@ -123,12 +123,16 @@ int run_parts(rsmi_group* s, size_t nblocks, F f) {
     const size_t parts = s->ctx.size();
     std::vector<int> rc(parts, RSMI_OK);
     std::lock_guard<std::mutex> g(s->call_mu);
-    std::vector<size_t> posted;
+    // Every allocation happens before the first post: the jobs capture rc and f by reference, so
+    // once one is posted this frame must not unwind (a std::bad_alloc from a later std::function
+    // or push_back would leave a worker writing through dangling references).
+    std::vector<std::pair<size_t, std::function<void()>>> jobs;
+    jobs.reserve(parts);
     for (size_t i = 0; i < parts; i++) {
         size_t st, cnt;
         rsmi_partition(nblocks, int(parts), int(i), &st, &cnt);
         if (!cnt) continue;
-        s->workers[i]->post([&rc, &f, i, st, cnt] {
+        jobs.emplace_back(i, [&rc, &f, i, st, cnt] {
             // an exception must not leave the worker thread (std::terminate): the member's host
             // code allocates (std::bad_alloc), so it becomes the part's status
             try {
@@ -137,9 +141,9 @@ int run_parts(rsmi_group* s, size_t nblocks, F f) {
                 rc[i] = rsmi::impl::exception_status();
             }
         });
-        posted.push_back(i);
     }
-    for (size_t i : posted) s->workers[i]->wait();
+    for (auto& j : jobs) s->workers[j.first]->post(std::move(j.second));  // moves only: no allocation
+    for (auto& j : jobs) s->workers[j.first]->wait();
     for (int r : rc)
         if (r != RSMI_OK) return r;
     return RSMI_OK;

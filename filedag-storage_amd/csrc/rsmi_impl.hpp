@@ -123,7 +123,10 @@ struct rsmi_ctx {
         int rc;
         bool done;
     };
-    rsmi::GroupCommit<CoalReq> coal{RSMI_ERR_DEVICE};
+    // a batch that throws (std::bad_alloc from the executor's host containers) fails its
+    // requests as the boundary reports host-resource exceptions (include/rsmi.h ABI v3)
+    rsmi::GroupCommit<CoalReq> coal{RSMI_ERR_HOST};
+    std::atomic<int> opt_inject_host_fault{0};  // test hook: the next coalesced batches throw std::bad_alloc
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;
 };

@@ -387,8 +387,8 @@ class DeviceGroup:
     def host_alloc(self, block_bytes: int, nblocks: int) -> int:
         """Page-locked buffer whose member block ranges sit on the members' NUMA nodes."""
         p = lib().rsmi_group_host_alloc(self._h, block_bytes, nblocks)
-        if not p:
-            raise RsmiError(ErrDevice, "rsmi_group_host_alloc failed")
+        if not p:  # mmap, NUMA placement or page-locking the host range failed
+            raise RsmiError(ErrHost, "rsmi_group_host_alloc failed")
         return p
 
     def host_free(self, p: int) -> None:

@@ -7,9 +7,69 @@ into per-rank ranges; SURVEY.md 8(e).  Two mappings:
     keyHashSlot = crc16(key) & 0x3FFF over 16384 slots (dag/pool/poolservice/hash_slot.go:20-22),
     then slot -> GPU by contiguous slot ranges.
 """
-from typing import Tuple
+import os
+from typing import Mapping, Optional, Tuple
 
 CLUSTER_SLOTS = 16384  # dag/slotsmgr/slots_mgr.go:8
+KFD_NODES = "class/kfd/kfd/topology/nodes"  # under the sysfs root
+
+
+def sysfs_gpu_count(sysfs_root: str = "/sys") -> Optional[int]:
+    """GPUs the kernel driver lists, read from sysfs without touching the HIP runtime: KFD
+    topology nodes whose `properties` carry a non-zero gfx_target_version (CPU nodes carry 0).
+    None when the topology is absent (no amdgpu driver, or sysfs not mounted)."""
+    base = os.path.join(sysfs_root, KFD_NODES)
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(base, d, "properties")) as f:
+                for line in f:
+                    key, _, val = line.partition(" ")
+                    if key == "gfx_target_version":
+                        n += int(val.strip() or "0") != 0
+                        break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def _visible(spec: str, have: int, uuids: bool) -> int:
+    """Devices a *_VISIBLE_DEVICES list leaves out of `have`: the runtime takes entries in
+    order and stops at the first it cannot use (an index out of range, or garbage); ROCr also
+    takes GPU UUIDs ("GPU-<hex>")."""
+    n = 0
+    for e in spec.split(","):
+        e = e.strip()
+        if uuids and e.startswith("GPU-"):
+            n += 1
+            continue
+        if not e.isdigit() or int(e) >= have:
+            break
+        n += 1
+    return min(n, have)
+
+
+def visible_gpu_count(sysfs_root: str = "/sys", env: Optional[Mapping[str, str]] = None) -> Optional[int]:
+    """GPUs a child process will see, counted without initialising HIP in this process (the
+    launcher must stay GPU-free before it spawns one process per GPU: bench.py --gpus N).
+    sysfs gives the physical count; ROCR_VISIBLE_DEVICES filters it first, then
+    HIP_VISIBLE_DEVICES (or CUDA_VISIBLE_DEVICES) indexes the ROCr-visible list.  None when
+    sysfs has no KFD topology."""
+    env = os.environ if env is None else env
+    have = sysfs_gpu_count(sysfs_root)
+    if have is None:
+        return None
+    rocr = env.get("ROCR_VISIBLE_DEVICES")
+    if rocr is not None:
+        have = _visible(rocr, have, uuids=True)
+    hip = env.get("HIP_VISIBLE_DEVICES", env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        have = _visible(hip, have, uuids=False)
+    return have
 
 
 def partition_blocks(nblocks: int, world: int, rank: int) -> Tuple[int, int]:

@@ -345,7 +345,9 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * bit-exact), "crc16_fused_fold" (the encode with the CRC-16 fused in, on
  * 16-byte-aligned layouts: 1 = default, rs_fused_mfma_kernel folds on the matrix cores; 0 = the
  * nibble-table variants), "crc32_fold" (the mutcask CRC-32 rows pass: 1 = the fold on the
- * matrix cores, 0 = the nibble-table fold; both bit-exact).  Kernel variants measured slower than the defaults are not
+ * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
+ * next N coalesced batches throw std::bad_alloc in the executor, so their requests return
+ * RSMI_ERR_HOST; default 0).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);

@@ -94,7 +94,7 @@ int par_blocks(size_t nblocks, F f) {
 
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0;
-    rsmi::GroupCommit<Req> coal{RSMI_ERR_DEVICE};
+    rsmi::GroupCommit<Req> coal{RSMI_ERR_HOST};
 };
 
 namespace {

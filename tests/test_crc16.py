@@ -335,6 +335,33 @@ def test_coalesced_encode_lone_caller_and_errors():
 
 
 @pytest.mark.gpu
+def test_coalesced_host_fault_reports_err_host():
+    """A coalesced batch whose executor throws std::bad_alloc (option "inject_host_fault") fails
+    its requests with RSMI_ERR_HOST, the status the boundary gives host-resource exceptions
+    (include/rsmi.h), not a device error; the queue keeps working afterwards, for encode and
+    for reconstruct (the degraded DagNode.Get's coalesced form, node.go:220-326)."""
+    k, m = 4, 2
+    block = b"123456" * 1000
+    with rsmi.Codec(k, m) as c:
+        c.set_option("inject_host_fault", 2)
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.encode_block_coalesced(block)
+        assert e.value.code == rsmi.ErrHost
+        sh = orc.split(k, m, block)
+        sh[k:] = orc.encode(k, m, sh[:k])
+        work = bytearray(sh.tobytes())
+        S = sh.shape[1]
+        work[0:S] = bytes(S)
+        present = [r != 0 for r in range(k + m)]
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.reconstruct_coalesced(work, S, present, True)
+        assert e.value.code == rsmi.ErrHost
+        assert c.encode_block_coalesced(block) == c.encode_block(block)
+        c.reconstruct_coalesced(work, S, present, True)
+        assert bytes(work) == sh.tobytes()
+
+
+@pytest.mark.gpu
 def test_coalesced_reconstruct_concurrent_callers():
     """rsmi_reconstruct_coalesced from 16 threads (concurrent degraded DagNode.Gets): two
     erasure patterns, both data_only modes and two shard sizes in flight together; every
