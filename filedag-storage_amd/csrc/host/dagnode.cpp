@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <future>
 #include <map>
 #include <stdexcept>
 
@@ -253,28 +254,36 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     Erasure enc;
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
     if (!s.ok()) return s;
-    std::vector<Bytes> shards;
-    std::vector<uint32_t> raw, raw32;
+    const int n = int(nodes_.size());
+    const size_t S = size_t(enc.ShardSize());
     bool want32 = false;  // mutcask-backed datanodes keep a CRC-32 of every value as well
     for (auto& sn : nodes_) want32 |= gpu_checksums_ && gpu_value_checksums_ && sn.client->WantsValueChecksum();
-    s = gpu_checksums_ ? enc.EncodeDataWithCrcs(block, &shards, &raw, want32 ? &raw32 : nullptr)
-                       : enc.EncodeData(block, &shards);
+    // Split + Encode into one page-locked buffer (coded there in place on the GPU), and each
+    // datanode gets its shard as a view of it, as the Go slices alias Split's buffer
+    const auto t0 = PhaseClock::now();
+    uint8_t* flat = block.empty() ? nullptr : block_scratch(size_t(n) * S);
+    if (!block.empty() && !flat) return Status::Error("out of host memory");
+    std::vector<uint32_t> raw(gpu_checksums_ && !block.empty() ? size_t(n) : 0), raw32(want32 ? size_t(n) : 0);
+    s = enc.EncodeDataFlat(block, flat, raw.empty() ? nullptr : raw.data(), raw32.empty() ? nullptr : raw32.data());
     if (!s.ok()) return s;
+    phase_add(Phase::Codec, t0);
+    const auto t1 = PhaseClock::now();
     const int wq = EntryQuorum().second;
     std::vector<Status> res(nodes_.size());
-    const size_t S = shards.empty() ? 0 : shards[0].size();
     last_shard_ = S;
-    fan(int(nodes_.size()), [&](int i) {  // one goroutine per datanode, no cancel
+    fan(n, [&](int i) {  // one goroutine per datanode, no cancel
         DataNodeClient& cl = *nodes_[i].client;
+        const ByteView shard(flat ? flat + size_t(i) * S : nullptr, block.empty() ? 0 : S);  // empty block: nil shards
         if (raw.empty()) {
-            res[i] = cl.Put(key, meta, shards[i]);
+            res[i] = cl.Put(key, meta, shard);
             return;
         }
         const uint16_t c16 = entry_checksum(meta, S, raw[i]);
         res[i] = !raw32.empty() && cl.WantsValueChecksum()
-                     ? cl.PutWithChecksums(key, meta, shards[i], c16, value_checksum(meta, S, c16, raw32[i]))
-                     : cl.PutWithChecksum(key, meta, shards[i], c16);
+                     ? cl.PutWithChecksums(key, meta, shard, c16, value_checksum(meta, S, c16, raw32[i]))
+                     : cl.PutWithChecksum(key, meta, shard, c16);
     }, S);
+    phase_add(Phase::Put, t1);
     QuorumWait w(wq, int(nodes_.size()) - wq + 1);
     for (const Status& r : res) w.add(r);
     return w.result("Write failed. Insufficient number of nodes online");
@@ -313,15 +322,20 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             const size_t nb = std::min(chunk, g.second.size() - c0);
             const size_t* idx = g.second.data() + c0;
             // per block: k data rows (Split, zero-padded) + m parity rows
+            const auto t0 = PhaseClock::now();
             uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
             if (!flat) {
                 for (size_t j = 0; j < nb; j++) results[idx[j]] = Status::Error("out of host memory");
                 continue;
             }
-            for (size_t j = 0; j < nb; j++) {
-                std::memcpy(flat + j * n * S, blocks[idx[j]].data(), B);
-                std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
-            }
+            fan_keys(int(std::min<size_t>(nb, 16)), [&](int t) {
+                for (size_t j = size_t(t); j < nb; j += std::min<size_t>(nb, 16)) {
+                    std::memcpy(flat + j * n * S, blocks[idx[j]].data(), B);
+                    std::memset(flat + j * n * S + B, 0, size_t(k) * S - B);
+                }
+            });
+            phase_add(Phase::Stage, t0);
+            const auto t1 = PhaseClock::now();
             if (gpu_checksums_) {
                 raw.resize(nb * size_t(n));
                 raw32.resize(want32 ? nb * size_t(n) : 0);
@@ -330,17 +344,19 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             } else {
                 rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
             }
+            phase_add(Phase::Codec, t1);
             if (rc) {
                 for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
                 continue;
             }
             // the blocks' datanode writes run concurrently (the reference's concurrent Puts),
             // each with its own node fan-out
+            const auto t2 = PhaseClock::now();
             fan_keys(int(nb), [&](int j) {
                 const uint8_t* base = flat + size_t(j) * n * S;
                 std::vector<Status> res(static_cast<size_t>(n));
                 fan(n, [&](int i) {
-                    Bytes shard(base + size_t(i) * S, base + size_t(i + 1) * S);
+                    const ByteView shard(base + size_t(i) * S, S);
                     DataNodeClient& cl = *nodes_[i].client;
                     if (!gpu_checksums_) {
                         res[i] = cl.Put(keys[idx[j]], meta, shard);
@@ -356,6 +372,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 for (const Status& r : res) w.add(r);
                 results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
             });
+            phase_add(Phase::Put, t2);
         }
     }
     // node.go:411-416 returns the error of the last Put
@@ -870,6 +887,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     };
     // (block size, survivor pattern) -> pending keys
     std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
+    DataNodeClient& target = *nodes_[to].client;
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
@@ -880,13 +898,18 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
         required[to] = 1;
+        // the fetch returns exactly the k survivors the plan reads (fetch_for_repair stops at
+        // the read quorum k), and only those are staged; the rows being rebuilt are not
+        const auto t0 = PhaseClock::now();
         uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
         if (!flat) return Status::Error("out of host memory");
-        for (size_t j = 0; j < nb; j++)
+        fan_keys(int(nb), [&](int j) {
             for (int i = 0; i < n; i++)
-                if (present[i]) std::memcpy(flat + (j * n + i) * S, pend[j].shards[i].data(), S);
+                if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, pend[j].shards[i].data(), S);
+        });
+        phase_add(Phase::Stage, t0);
         // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
-        DataNodeClient& target = *nodes_[to].client;
+        const auto t1 = PhaseClock::now();
         const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
         std::vector<uint32_t> r16(gpu_checksums_ ? nb * size_t(n) : 0), r32(want32 ? nb * size_t(n) : 0);
         rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, nb, present.data(),
@@ -894,13 +917,15 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                                                                     want32 ? r32.data() : nullptr)
                             : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(),
                                                                required.data());
+        phase_add(Phase::Codec, t1);
         if (rc) return rsmi_status(rc);
         const Bytes meta = encode_meta(size);
-        // the rebuilt rows go to the target concurrently; outcomes are taken in key order
+        // the rebuilt rows go to the target concurrently, each as a view of the staging buffer;
+        // outcomes are taken in key order
+        const auto t2 = PhaseClock::now();
         std::vector<Status> ps(nb);
         fan_keys(int(nb), [&](int j) {
-            const uint8_t* row = flat + (size_t(j) * n + size_t(to)) * S;
-            const Bytes shard(row, row + S);
+            const ByteView shard(flat + (size_t(j) * n + size_t(to)) * S, S);
             if (!gpu_checksums_) {
                 ps[j] = target.Put(pend[j].key, meta, shard);
                 return;
@@ -910,6 +935,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                                                      value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
                            : target.PutWithChecksum(pend[j].key, meta, shard, c16);
         });
+        phase_add(Phase::Put, t2);
         for (size_t j = 0; j < nb; j++) {
             if (!ps[j].ok()) return ps[j];
             done++;
@@ -919,26 +945,46 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     };
     // Each key's checks and fetch (the target's GetMeta, the meta quorum, the k-of-n fetch) run
     // concurrently over a window of keys; the results are then taken in key order, so the
-    // grouping, the flushes and the errors returned are those of the sequential loop.
+    // grouping, the flushes and the errors returned are those of the sequential loop.  The next
+    // window is fetched on a helper thread while this thread stages, codes and writes the
+    // current one (the GPU call no longer leaves the host idle); fetches only read, so running
+    // one ahead changes no outcome, and a failing flush still returns before any later write.
     struct Fetch {
         bool use = false;
         int size = 0;
         std::vector<Bytes> shards;
     };
-    const size_t window = std::min<size_t>(std::max<size_t>(batch, 1), 64);
-    for (size_t c0 = 0; c0 < keys.size(); c0 += window) {
-        const size_t nk = std::min(window, keys.size() - c0);
+    auto fetch_window = [this, &keys, to](size_t c0, size_t nk) {
+        const auto t0 = PhaseClock::now();
         std::vector<Fetch> fr(nk);
         fan_keys(int(nk), [&](int q) {
-            const std::string& key = keys[c0 + q];
+            const std::string& key = keys[c0 + size_t(q)];
             Bytes mb;
             if (nodes_[to].client->GetMeta(key, &mb).ok()) return;
             int size;
             if (!GetSize(key, &size).ok()) return;
-            if (!fetch_for_repair(key, to, &fr[q].shards).ok()) return;
-            fr[q].size = size;
-            fr[q].use = true;
+            if (!fetch_for_repair(key, to, &fr[size_t(q)].shards).ok()) return;
+            fr[size_t(q)].size = size;
+            fr[size_t(q)].use = true;
         });
+        phase_add(Phase::Fetch, t0);
+        return fr;
+    };
+    // windows as large as one flush (staging-bounded by the shard size seen last), at most batch
+    size_t window = std::min<size_t>(batch, 16);
+    auto next_window = [&](const std::vector<Fetch>& fr) {
+        for (auto& f : fr)
+            if (f.use && f.size > 0)
+                window = std::max<size_t>(
+                    1, std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(f.size), k))));
+    };
+    std::future<std::vector<Fetch>> ahead;
+    size_t c0 = 0, nk = std::min(window, keys.size());
+    std::vector<Fetch> fr = fetch_window(c0, nk);
+    while (c0 < keys.size()) {
+        next_window(fr);
+        const size_t c1 = c0 + nk, nk1 = std::min(window, keys.size() - std::min(c1, keys.size()));
+        if (nk1) ahead = std::async(std::launch::async, fetch_window, c1, nk1);
         for (size_t q = 0; q < nk; q++) {
             if (!fr[q].use) continue;
             const std::string& key = keys[c0 + q];
@@ -948,7 +994,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 Erasure enc;
                 s = Erasure::New(k, m, size, &enc, device_);
                 if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
-                if (!s.ok()) return s;
+                if (!s.ok()) return s;  // `ahead` (reads only) is joined by its destructor
                 continue;
             }
             std::string pat(size_t(n), '0');
@@ -961,6 +1007,9 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 if (!s.ok()) return s;
             }
         }
+        c0 = c1;
+        nk = nk1;
+        if (nk1) fr = ahead.get();
     }
     for (auto& g : groups) {
         s = flush(g.first, g.second);
@@ -968,6 +1017,21 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     }
     if (repaired) *repaired = done;
     return Status::Ok();
+}
+
+void DagNode::phase_add(Phase p, PhaseClock::time_point t0) {
+    if (!phase_on_.load(std::memory_order_relaxed)) return;
+    phase_ns_[int(p)] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t0).count());
+}
+
+std::array<double, 4> DagNode::PhaseSeconds() const {
+    std::array<double, 4> r{};
+    for (int i = 0; i < 4; i++) r[size_t(i)] = double(phase_ns_[i].load()) * 1e-9;
+    return r;
+}
+
+void DagNode::ResetPhases() {
+    for (auto& x : phase_ns_) x = 0;
 }
 
 }  // namespace host

@@ -23,7 +23,9 @@
 //   * GetMany decodes the blocks that need it in GPU batches (8(f) rank 3);
 //   * MigrateBlocks moves blocks between erasure sets as batched decode + encode (rank 4).
 #pragma once
+#include <array>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -129,8 +131,20 @@ public:
     void SetFanoutMinBytes(size_t v) { fanout_min_ = v; }
     std::pair<int, int> EntryQuorum() const;  // (read, write)
     size_t RepairQueueLen();
+    // Per-phase host time of Put / PutMany / RepairDataNodeBatched (diagnostic, off by default):
+    // seconds spent fetching shards (window fetches of the batched repair), staging rows into
+    // page-locked memory, in the codec call, and writing to the datanodes, summed over the
+    // calling and helper threads since the last ResetPhases (overlapped phases both count).
+    enum class Phase { Fetch = 0, Stage = 1, Codec = 2, Put = 3 };
+    void SetPhaseTiming(bool v) { phase_on_ = v; }
+    std::array<double, 4> PhaseSeconds() const;
+    void ResetPhases();
 
 private:
+    using PhaseClock = std::chrono::steady_clock;
+    void phase_add(Phase p, PhaseClock::time_point t0);
+    std::atomic<bool> phase_on_{false};
+    std::atomic<uint64_t> phase_ns_[4] = {};
     struct Fetched {
         Meta meta;
         std::vector<Bytes> shards;

@@ -99,36 +99,46 @@ uint32_t crc32_ieee(const uint8_t* p, size_t n) {
     return ~crc;
 }
 
-Status DataNodeServer::store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc,
+Status DataNodeServer::store(const std::string& key, const Bytes& meta, ByteView data, const uint16_t* crc,
                              const uint32_t* value_crc) {
     if (key.empty()) return Status::Error("Key cannot be empty");  // badger, server_test.go:14-22
     const size_t pre = prefix();  // mutcask: | crc32 (4 LE) | entry |  (cask.go:73-79)
-    Bytes v(pre + size_t(kHeaderSize) + meta.size() + data.size());
-    uint8_t* e = v.data() + pre;
+    const size_t len = pre + size_t(kHeaderSize) + meta.size() + data.size();
+    // the entry is framed straight into the value the KV keeps (a recycled buffer when one is
+    // large enough; every byte is written below), outside the lock, with no second copy
+    Value nv;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        for (size_t i = spare_.size(); i-- > 0;)
+            if (spare_[i].cap >= len) {
+                nv = std::move(spare_[i]);
+                spare_.erase(spare_.begin() + long(i));
+                break;
+            }
+    }
+    if (!nv.p) {
+        nv.p.reset(new uint8_t[len]);
+        nv.cap = len;
+    }
+    nv.len = len;
+    uint8_t* e = nv.p.get() + pre;
     put_le32(e + 4, uint32_t(meta.size()));
     put_le32(e + 8, uint32_t(data.size()));
     if (!meta.empty()) std::memcpy(e + kHeaderSize, meta.data(), meta.size());
     if (!data.empty()) std::memcpy(e + kHeaderSize + meta.size(), data.data(), data.size());
-    put_le32(e, crc ? *crc : crc16_ibm(e + 4, v.size() - pre - 4));  // server.go:70-75
-    if (pre) put_le32(v.data(), value_crc ? *value_crc : crc32_ieee(e, v.size() - pre));
+    put_le32(e, crc ? *crc : crc16_ibm(e + 4, len - pre - 4));  // server.go:70-75
+    if (pre) put_le32(nv.p.get(), value_crc ? *value_crc : crc32_ieee(e, len - pre));
     std::lock_guard<std::mutex> g(mu_);
-    auto it = kv_.find(key);
-    if (it != kv_.end() && it->second.capacity() >= v.size()) {
-        // overwrite in place: the stored buffer may come from another thread's malloc arena
-        // (concurrent Puts), and freeing it here would leave this thread's arena to fault in
-        // fresh pages for every later entry
-        it->second.assign(v.begin(), v.end());
-    } else {
-        kv_[key] = std::move(v);
-    }
+    std::swap(kv_[key], nv);
+    if (nv.p && spare_.size() < kSpareValues) spare_.push_back(std::move(nv));
     return Status::Ok();
 }
 
 // the KV engine's read: mutcask re-checks its value checksum on every read (cask.go:250)
-Status DataNodeServer::read_entry(const std::string& key, const Bytes** entry) {
+Status DataNodeServer::read_entry(const std::string& key, const Value** entry) {
     auto it = kv_.find(key);
     if (it == kv_.end()) return not_found();
-    const Bytes& v = it->second;
+    const Value& v = it->second;
     if (engine_ == KvEngine::Mutcask) {
         if (v.size() <= 4) return Status::Error("mutcask: invalid value format");
         if (get_le32(v.data()) != crc32_ieee(v.data() + 4, v.size() - 4))
@@ -138,22 +148,22 @@ Status DataNodeServer::read_entry(const std::string& key, const Bytes** entry) {
     return Status::Ok();
 }
 
-Status DataNodeServer::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
+Status DataNodeServer::Put(const std::string& key, const Bytes& meta, ByteView data) {
     return store(key, meta, data, nullptr, nullptr);
 }
 
-Status DataNodeServer::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+Status DataNodeServer::PutWithChecksum(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc) {
     return store(key, meta, data, &crc, nullptr);
 }
 
-Status DataNodeServer::PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+Status DataNodeServer::PutWithChecksums(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc,
                                         uint32_t value_crc) {
     return store(key, meta, data, &crc, &value_crc);
 }
 
 Status DataNodeServer::Get(const std::string& key, Bytes* meta, Bytes* data) {
     std::lock_guard<std::mutex> g(mu_);
-    const Bytes* v = nullptr;
+    const Value* v = nullptr;
     Status s = read_entry(key, &v);
     if (!s.ok()) return s;
     return unpack(v->data() + prefix(), v->size() - prefix(), meta, data);
@@ -163,7 +173,7 @@ Status DataNodeServer::GetUnverified(const std::string& key, Bytes* meta, Bytes*
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
     if (it == kv_.end()) return not_found();
-    const Bytes& v = it->second;
+    const Value& v = it->second;
     const size_t pre = prefix();
     if (v.size() < pre + size_t(kHeaderSize)) return Status::Error("unexpected EOF");
     const uint8_t* e = v.data() + pre;
@@ -182,7 +192,7 @@ Status DataNodeServer::GetUnverified(const std::string& key, Bytes* meta, Bytes*
 
 Status DataNodeServer::GetMeta(const std::string& key, Bytes* meta) {
     std::lock_guard<std::mutex> g(mu_);
-    const Bytes* v = nullptr;
+    const Value* v = nullptr;
     Status s = read_entry(key, &v);
     if (!s.ok()) return s;
     return unpack(v->data() + prefix(), v->size() - prefix(), meta, nullptr);
@@ -214,7 +224,7 @@ bool DataNodeServer::RawEntry(const std::string& key, Bytes* entry) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
     if (it == kv_.end()) return false;
-    entry->assign(it->second.begin() + long(prefix()), it->second.end());
+    entry->assign(it->second.data() + prefix(), it->second.data() + it->second.size());
     return true;
 }
 
@@ -222,30 +232,31 @@ bool DataNodeServer::RawValue(const std::string& key, Bytes* value) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
     if (it == kv_.end()) return false;
-    *value = it->second;
+    value->assign(it->second.data(), it->second.data() + it->second.size());
     return true;
 }
 
 void DataNodeServer::CorruptByte(const std::string& key, size_t offset) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = kv_.find(key);
-    if (it != kv_.end() && prefix() + offset < it->second.size()) it->second[prefix() + offset] ^= 0x5A;
+    if (it != kv_.end() && prefix() + offset < it->second.size()) it->second.p[prefix() + offset] ^= 0x5A;
 }
 
 void DataNodeServer::Wipe() {
     std::lock_guard<std::mutex> g(mu_);
     kv_.clear();
+    spare_.clear();
 }
 
 Status InProcDataNode::down() const { return Status::Error("rpc error: code = Unavailable desc = " + addr_); }
 
-Status InProcDataNode::Put(const std::string& key, const Bytes& meta, const Bytes& data) {
+Status InProcDataNode::Put(const std::string& key, const Bytes& meta, ByteView data) {
     return offline_ ? down() : server_.Put(key, meta, data);
 }
-Status InProcDataNode::PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+Status InProcDataNode::PutWithChecksum(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc) {
     return offline_ ? down() : server_.PutWithChecksum(key, meta, data, crc);
 }
-Status InProcDataNode::PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+Status InProcDataNode::PutWithChecksums(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc,
                                         uint32_t value_crc) {
     return offline_ ? down() : server_.PutWithChecksums(key, meta, data, crc, value_crc);
 }

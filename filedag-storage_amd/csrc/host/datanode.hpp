@@ -24,6 +24,23 @@ namespace host {
 
 using Bytes = std::vector<uint8_t>;
 
+// A read-only view of bytes: what a Go []byte argument is (node.go:376-399 hands each datanode a
+// sub-slice of the one buffer Split + Encode filled, with no copy).  Built from a Bytes or from
+// a pointer and a length; the caller keeps the bytes alive for the call.
+class ByteView {
+public:
+    ByteView(const Bytes& b) : p_(b.data()), n_(b.size()) {}  // NOLINT: implicit, like a slice
+    ByteView(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+    const uint8_t* data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    Bytes bytes() const { return Bytes(p_, p_ + n_); }
+
+private:
+    const uint8_t* p_;
+    size_t n_;
+};
+
 // A Go-style error value: ok() when empty.
 struct Status {
     std::string err;
@@ -47,17 +64,17 @@ constexpr int kHeaderSize = 12;  // server.go:37
 class DataNodeClient {
 public:
     virtual ~DataNodeClient() = default;
-    virtual Status Put(const std::string& key, const Bytes& meta, const Bytes& data) = 0;
+    virtual Status Put(const std::string& key, const Bytes& meta, ByteView data) = 0;
     // Put with the entry checksum computed by the sender (the DagNode gets R(shard) from the
     // GPU encode).  Over gRPC this is an optional AddRequest field; a
     // datanode without it recomputes, which is what this default does.
-    virtual Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) {
+    virtual Status PutWithChecksum(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc) {
         (void)crc;
         return Put(key, meta, data);
     }
     // ... and with the mutcask value checksum of that entry as well (cask.go:73-79), for a
     // datanode whose engine keeps one (WantsValueChecksum); others drop it
-    virtual Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+    virtual Status PutWithChecksums(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc,
                                     uint32_t value_crc) {
         (void)value_crc;
         return PutWithChecksum(key, meta, data, crc);
@@ -91,12 +108,12 @@ class DataNodeServer {
 public:
     explicit DataNodeServer(KvEngine engine = KvEngine::Badger) : engine_(engine) {}
     KvEngine engine() const { return engine_; }
-    Status Put(const std::string& key, const Bytes& meta, const Bytes& data);
+    Status Put(const std::string& key, const Bytes& meta, ByteView data);
     // the same entry, with the sender's checksum in place of the server.go:70 CRC pass; Get
     // and GetMeta still verify it, so a wrong sender checksum fails the read like corruption
-    Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc);
+    Status PutWithChecksum(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc);
     // mutcask: the value checksum too (a wrong one fails later reads with "data may be rotted")
-    Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+    Status PutWithChecksums(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc,
                             uint32_t value_crc);
     Status Get(const std::string& key, Bytes* meta, Bytes* data);
     // the entry's parts and stored checksums without checking either (the reader verifies)
@@ -113,13 +130,24 @@ public:
     void Wipe();
 
 private:
-    Status store(const std::string& key, const Bytes& meta, const Bytes& data, const uint16_t* crc,
+    // a stored value: len bytes in a buffer of cap bytes
+    struct Value {
+        std::unique_ptr<uint8_t[]> p;
+        size_t len = 0, cap = 0;
+        const uint8_t* data() const { return p.get(); }
+        size_t size() const { return len; }
+    };
+    Status store(const std::string& key, const Bytes& meta, ByteView data, const uint16_t* crc,
                  const uint32_t* value_crc);
-    Status read_entry(const std::string& key, const Bytes** entry);  // caller holds mu_
+    Status read_entry(const std::string& key, const Value** entry);  // caller holds mu_
     size_t prefix() const { return engine_ == KvEngine::Mutcask ? 4 : 0; }
     KvEngine engine_;
     std::mutex mu_;
-    std::map<std::string, Bytes> kv_;
+    std::map<std::string, Value> kv_;
+    // replaced values kept for reuse: an overwrite frames into a recycled buffer instead of a
+    // fresh allocation (whose pages the kernel would fault in again on every Put of a key)
+    std::vector<Value> spare_;
+    static constexpr size_t kSpareValues = 64;
 };
 
 // An in-process client; Offline(true) makes every call fail like a dead gRPC peer.
@@ -127,9 +155,9 @@ class InProcDataNode : public DataNodeClient {
 public:
     explicit InProcDataNode(std::string addr, KvEngine engine = KvEngine::Badger)
         : addr_(std::move(addr)), server_(engine) {}
-    Status Put(const std::string& key, const Bytes& meta, const Bytes& data) override;
-    Status PutWithChecksum(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc) override;
-    Status PutWithChecksums(const std::string& key, const Bytes& meta, const Bytes& data, uint16_t crc,
+    Status Put(const std::string& key, const Bytes& meta, ByteView data) override;
+    Status PutWithChecksum(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc) override;
+    Status PutWithChecksums(const std::string& key, const Bytes& meta, ByteView data, uint16_t crc,
                             uint32_t value_crc) override;
     bool WantsValueChecksum() const override { return server_.engine() == KvEngine::Mutcask; }
     Status Get(const std::string& key, Bytes* meta, Bytes* data) override;

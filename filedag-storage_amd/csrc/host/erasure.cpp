@@ -63,20 +63,15 @@ PinnedBuf& thread_staging() {
     return buf;
 }
 
-namespace {
 // per-thread scratch for one block's (k+m)*S rows around a single-block encode or
 // reconstruct: neither zero-filled (the call writes every byte it returns) nor allocated per
-// call (a 364 KB vector per Put or Get was a fresh value-initialised allocation each time)
+// call (a 364 KB vector per Put or Get was a fresh value-initialised allocation each time), and
+// page-locked, so a lone coalesced call codes it in place on the GPU (rsmi_coalesce.cpp) instead
+// of through the engine's staging and a copy back
 uint8_t* block_scratch(size_t bytes) {
-    static thread_local std::unique_ptr<uint8_t[]> p;
-    static thread_local size_t cap = 0;
-    if (bytes > cap) {
-        p.reset(new (std::nothrow) uint8_t[bytes]);
-        cap = p ? bytes : 0;
-    }
-    return p.get();
+    static thread_local PinnedBuf buf;
+    return buf.reserve(bytes);
 }
-}  // namespace
 
 namespace {
 std::mutex g_ctx_mu;
@@ -133,6 +128,16 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
 
 Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw) const {
     return EncodeDataWithCrcs(data, shards, raw, nullptr);
+}
+
+Status Erasure::EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const {
+    if (data.empty()) return Status::Ok();  // erasure.go:52-54
+    int rc;
+    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    if (!c) return rsmi_status(rc);
+    rc = raw ? rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat, raw, raw32)
+             : rsmi_encode_block_coalesced(c, data.data(), data.size(), flat, nullptr);
+    return rsmi_status(rc);
 }
 
 Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw,

@@ -51,6 +51,9 @@ private:
 // thread, kept for the thread's life, and cut their batches to at most kStagingBytes.
 constexpr size_t kStagingBytes = size_t(64) << 20;
 PinnedBuf& thread_staging();
+// The calling thread's page-locked scratch for one block's rows (single-block encodes and
+// reconstructs), separate from thread_staging; grown on demand, contents not cleared.
+uint8_t* block_scratch(size_t bytes);
 inline size_t staging_blocks(size_t block_bytes) {
     return block_bytes >= kStagingBytes ? 1 : kStagingBytes / block_bytes;
 }
@@ -67,6 +70,11 @@ public:
     // ... and, when raw32 is not null, R32(shard) for the mutcask value checksum (CRC-32)
     Status EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw,
                               std::vector<uint32_t>* raw32) const;
+    // EncodeData into one caller buffer of (k+m) * ShardSize() bytes, shard i at i * ShardSize():
+    // the Go slices Split returns alias one buffer, so the shards need no copies of their own.
+    // raw / raw32 (k+m entries each, may be null): R(shard) / R32(shard) as EncodeDataWithCrcs.
+    // flat should be page-locked (block_scratch): a lone call is then coded in place.
+    Status EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const;
     Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
     Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;
     int64_t ShardSize() const { return ceil_frac(block_size_, data_blocks_); }

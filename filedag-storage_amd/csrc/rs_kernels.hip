@@ -430,6 +430,13 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint32_t blk = u / upb;
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
     const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
+#if RSMI_FUSED_COOP && RSMI_FUSED_IDLE_EXIT
+    // A block's last unit may hold fewer tiles than waves (RS(10,4) 256 KiB: 26 tiles, the 7th
+    // unit has 2): its idle waves end here instead of holding their slots until the unit's
+    // barrier.  s_barrier waits only on the workgroup's waves that have not ended, and the
+    // read-out below sums and reads out over the nt active waves only.
+    if (wid >= nt) return;
+#endif
     const uint8_t* ib = in + uint64_t(blk) * in_bs;
     uint8_t* ob = out + uint64_t(blk) * out_bs;
 
@@ -706,8 +713,16 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #pragma unroll
     for (int a = 0; a < NACC; a++) s_red[wid][a][lane] = cacc[a];
     __syncthreads();
+#if RSMI_FUSED_IDLE_EXIT
+    for (int a = int(wid); a < NACC; a += int(nt)) {  // only the nt active waves wrote counts
+        mfma_v4f c = s_red[0][a][lane];
+        for (uint32_t w = 1; w < nt; w++) c += s_red[w][a][lane];
+        record(a, c);
+    }
+#else
     for (int a = int(wid); a < NACC; a += kWG / kWave)
         record(a, s_red[0][a][lane] + s_red[1][a][lane] + s_red[2][a][lane] + s_red[3][a][lane]);
+#endif
 #if RSMI_FUSED_INLINE_COMBINE
     // The block's last unit to finish combines its records into R(row) (no second launch).  Each
     // workgroup publishes its record (fence, then one atomic increment of the block's counter);

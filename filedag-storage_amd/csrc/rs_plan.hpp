@@ -64,6 +64,9 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #ifndef RSMI_FUSED_UNIT
 #define RSMI_FUSED_UNIT 4
 #endif
+#ifndef RSMI_FUSED_IDLE_EXIT  // 1: a unit's workgroup lets its waves without a tile end at once
+#define RSMI_FUSED_IDLE_EXIT 0
+#endif
 #ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
 #define RSMI_FUSED_COOP 1
 #endif

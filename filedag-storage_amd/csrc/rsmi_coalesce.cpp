@@ -31,6 +31,26 @@ void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     const std::string& key = rq[0]->key;
     const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
+    // A lone request whose shard buffer is page-locked (the host mirror's block scratch) is coded
+    // in place: the host paths run it as one zero-copy kernel on that buffer, so neither the
+    // staging copy in nor the n*S copy back out happens (per-block DagNode.Put / degraded Get)
+    if (nb == 1 && host_alias(rq[0]->out, n * S)) {
+        rsmi_ctx::CoalReq& r = *rq[0];
+        if (key[0] == 'E') {
+            std::memcpy(r.out, r.block, r.B);
+            std::memset(r.out + r.B, 0, k * S - r.B);  // Split zero-padding
+            r.rc = encode_host_impl(c, r.out, n * S, r.out + k * S, n * S, S, 1, r.raw, r.raw32);
+        } else {
+            const char* f = key.c_str() + key.find(':') + 1;
+            std::vector<uint8_t> present(n), want(n);
+            for (size_t i = 0; i < n; i++) {
+                present[i] = uint8_t(f[i] == '1');
+                want[i] = uint8_t(f[n + i] == '1');
+            }
+            r.rc = reconstruct_host_impl(c, r.out, n * S, S, 1, present.data(), want.data());
+        }
+        return;
+    }
     uint8_t* h = coal_stage(c, nb * n * S);
     if (!h) {
         for (size_t j = 0; j < nb; j++) rq[j]->rc = RSMI_ERR_DEVICE;

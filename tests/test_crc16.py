@@ -335,6 +335,53 @@ def test_coalesced_encode_lone_caller_and_errors():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (16, 4, 4194304), (4, 2, 6), (10, 4, 4099)])
+def test_coalesced_lone_call_in_place_on_page_locked_buffer(k, m, B):
+    """A lone coalesced encode or reconstruct whose shard buffer is page-locked (the host
+    mirror's block scratch, DagNode.Put / a degraded Get, node.go:358-408 / :277-326) is coded
+    in place by one zero-copy kernel instead of through the engine's staging: shards, raw
+    CRC-16s and the rebuilt rows equal the oracle's, rows not asked for stay untouched."""
+    import ctypes
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    block = bytes(np.random.default_rng(B + k).integers(0, 256, size=B, dtype=np.uint8))
+    want = orc.split(k, m, block)
+    want[k:] = orc.encode(k, m, want[:k])
+    p = L.rsmi_host_alloc(n * S)
+    assert p
+    try:
+        out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p))
+        out[:] = 0xA5  # stale bytes: the padding and parity must be written, not assumed zero
+        raw = (ctypes.c_uint32 * n)()
+        with rsmi.Codec(k, m) as c:
+            src = bytearray(block)
+            assert L.rsmi_encode_block_coalesced(c._h, ctypes.addressof((ctypes.c_char * B).from_buffer(src)), B, p,
+                                                 raw) == 0
+            assert np.array_equal(out.reshape(n, S), want)
+            for r in range(n):
+                assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(want[r].tobytes())
+            assert c.stat("coalesced_batches") == 1
+            for lost, data_only in (([0], True), ([1, n - 1] if m >= 2 else [n - 1], False)):
+                sh = out.reshape(n, S)
+                sh[:] = want
+                for r in lost:
+                    sh[r] = 0xEE
+                present = (ctypes.c_uint8 * n)(*[0 if r in lost else 1 for r in range(n)])
+                assert L.rsmi_reconstruct_coalesced(c._h, p, S, present, 1 if data_only else 0) == 0
+                for r in range(n):
+                    if r in lost and (r < k or not data_only):
+                        assert np.array_equal(sh[r], want[r]), (lost, r)
+                    elif r in lost:
+                        assert (sh[r] == 0xEE).all()
+                    else:
+                        assert np.array_equal(sh[r], want[r])
+    finally:
+        L.rsmi_host_free(p)
+
+
+@pytest.mark.gpu
 def test_coalesced_host_fault_reports_err_host():
     """A coalesced batch whose executor throws std::bad_alloc (option "inject_host_fault") fails
     its requests with RSMI_ERR_HOST, the status the boundary gives host-resource exceptions

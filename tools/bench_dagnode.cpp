@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <thread>
 
 #include "../filedag-storage_amd/csrc/host/dagnode.hpp"
@@ -58,12 +59,28 @@ int main(int argc, char** argv) {
     const double putbh = secs(t0);
     d->SetGpuChecksums(true);
     d->Put("warm", blocks[0]);
+    // per-phase host time of the legs the GPU / CPU codec comparison is about (DagNode phases:
+    // fetch, stage, codec, put; summed over threads)
+    std::string phases;
+    auto phase_json = [&](const char* leg, double wall) {
+        const auto p = d->PhaseSeconds();
+        char buf[256];
+        std::snprintf(buf, sizeof buf, "%s\"%s\": {\"wall\": %.4f, \"fetch\": %.4f, \"stage\": %.4f, \"codec\": %.4f, \"put\": %.4f}",
+                      phases.empty() ? "" : ", ", leg, wall, p[0], p[1], p[2], p[3]);
+        phases += buf;
+        d->ResetPhases();
+    };
+    d->SetPhaseTiming(true);
+    d->ResetPhases();
     t0 = clk::now();
     for (int i = 0; i < N; i++) d->Put(keys[i], blocks[i]);
     const double put1 = secs(t0);
+    phase_json("put", put1);
     t0 = clk::now();
     d->PutMany(keys, blocks);
     const double putb = secs(t0);
+    phase_json("putmany", putb);
+    d->SetPhaseTiming(false);
     // Put from 16 threads at once: the per-block encodes coalesce into GPU batches
     const int T = 16;
     long c0 = 0, b0 = 0;
@@ -153,9 +170,13 @@ int main(int argc, char** argv) {
     const double rep1 = secs(t0);
     dn[size_t(rj)]->server().Wipe();
     size_t rep = 0;
+    d->SetPhaseTiming(true);
+    d->ResetPhases();
     t0 = clk::now();
     d->RepairDataNodeBatched(0, rj, 256, &rep);
     const double repb = secs(t0);
+    phase_json("repair_batched", repb);
+    d->SetPhaseTiming(false);
     // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
     // entry (cask.go:73-79).  Put / PutMany with the entry CRC-16 from the GPU pass and the
     // value CRC-32 from each datanode (the default), against the datanodes computing both, and
@@ -223,5 +244,10 @@ int main(int argc, char** argv) {
     std::printf("\"k\": %d, \"m\": %d, \"B\": %zu, \"N\": %d, \"put\": %.3f, \"putmany\": %.3f, \"put_threads\": %.3f, "
                 "\"get\": %.3f, \"getmany\": %.3f, \"get_threads\": %.3f, \"repair\": %.3f, \"repair_batched\": %.3f}\n",
                 k, m, B, N, gib / put1, gib / putb, gib / putT, gib / get1, gib / getb, gib / getT, gib / rep1, gib / repb);
+#ifdef FAKE_RSMI_FAST
+    std::printf("PHASES {\"codec\": \"cpu\", \"k\": %d, \"m\": %d, \"B\": %zu, %s}\n", k, m, B, phases.c_str());
+#else
+    std::printf("PHASES {\"codec\": \"gpu\", \"k\": %d, \"m\": %d, \"B\": %zu, %s}\n", k, m, B, phases.c_str());
+#endif
     return 0;
 }

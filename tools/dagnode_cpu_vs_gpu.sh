@@ -9,13 +9,16 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 OUT=gpurun_out/dagnode_cmp.jsonl
 : > $OUT
+: > gpurun_out/dn_phases.jsonl
 for shape in "2 1 262144 512" "10 4 262144 512" "16 4 4194304 64"; do
   for rep in 1 2 3; do
     timeout -k 10 300 ./tools/build/bench_dagnode $shape > gpurun_out/dn_gpu.log 2>&1 || { echo "gpu bench $shape failed"; tail gpurun_out/dn_gpu.log; exit 1; }
     grep '^RESULT ' gpurun_out/dn_gpu.log | sed 's/^RESULT //' >> $OUT
+    grep '^PHASES ' gpurun_out/dn_gpu.log | sed 's/^PHASES //' >> gpurun_out/dn_phases.jsonl
     timeout -k 10 300 ./tools/build/bench_dagnode_cpu $shape > gpurun_out/dn_cpu.log 2>&1 || { echo "cpu bench $shape failed"; tail gpurun_out/dn_cpu.log; exit 1; }
     grep '^RESULT ' gpurun_out/dn_cpu.log | sed 's/^RESULT //' >> $OUT
+    grep '^PHASES ' gpurun_out/dn_cpu.log | sed 's/^PHASES //' >> gpurun_out/dn_phases.jsonl
     echo "$shape run $rep done"
   done
 done
-python3 tools/dagnode_table.py $OUT
+python3 tools/dagnode_table.py $OUT gpurun_out/dn_phases.jsonl

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Median and spread (min-max) of tools/dagnode_cpu_vs_gpu.sh's RESULT lines, GPU codec beside
-CPU codec, per shape and Dag Node leg (GiB/s of block payload)."""
+CPU codec, per shape and Dag Node leg (GiB/s of block payload); with a second file of PHASES
+lines, the median per-phase host time (ms: fetch / stage / codec / put, summed over threads, and
+the leg's wall time) of the legs that report them."""
 import json
 import statistics
 import sys
@@ -8,6 +10,26 @@ import sys
 LEGS = [("put", "Put, per block"), ("putmany", "PutMany"), ("put_threads", "Put, 16 threads"),
         ("get", "Get, per block (1 lost shard)"), ("getmany", "GetMany"), ("get_threads", "Get, 16 threads"),
         ("repair", "RepairDataNode"), ("repair_batched", "RepairDataNodeBatched")]
+
+
+def phases(path):
+    rows = [json.loads(l) for l in open(path) if l.strip()]
+    shapes = []
+    for r in rows:
+        if (r["k"], r["m"], r["B"]) not in shapes:
+            shapes.append((r["k"], r["m"], r["B"]))
+    for k, m, B in shapes:
+        print(f"\nRS({k},{m}) {B // 1024} KiB: per-phase host time, ms, median of runs (summed over threads)")
+        print("| leg | codec | wall | fetch | stage | codec call | datanode puts |")
+        print("|---|---|---|---|---|---|---|")
+        for leg in ("put", "putmany", "repair_batched"):
+            for codec in ("gpu", "cpu"):
+                v = [r[leg] for r in rows if r["codec"] == codec and (r["k"], r["m"], r["B"]) == (k, m, B) and leg in r]
+                if not v:
+                    continue
+                med = {f: 1e3 * statistics.median(x[f] for x in v) for f in ("wall", "fetch", "stage", "codec", "put")}
+                print(f"| {leg} | {codec} | {med['wall']:.1f} | {med['fetch']:.1f} | {med['stage']:.1f} | "
+                      f"{med['codec']:.1f} | {med['put']:.1f} |")
 
 
 def main(path):
@@ -39,3 +61,5 @@ def main(path):
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/dagnode_cmp.jsonl")
+    if len(sys.argv) > 2:
+        phases(sys.argv[2])

@@ -13,16 +13,29 @@ import statistics
 import sys
 
 
+def label(name):
+    """The label rsmi_last_kernel reports for the coding kernels (rs_fast_kernel<K, MT, NT, WPS,
+    UA, CRC> -> rs_fast_kernel<K=..,MT=..,NT=..>[,UA][,CRC]); every other rsmi:: kernel (the fused
+    matrix-core encode + CRC-16, the combine kernels, the rows passes, repitch) by its name and
+    template arguments; None for kernels outside the library (torch's generators)."""
+    m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", name)
+    if m:
+        return f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (
+            ",UA" if m.group(5) == "true" else "") + (",CRC" if m.group(6) == "true" else "")
+    m = re.search(r"rsmi::(\w+)(<[^>]*>)?", name)
+    if not m:
+        return None
+    return m.group(1) + (m.group(2) or "").replace(" ", "")
+
+
 def per_kernel(path, counter):
     d = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "rs_fast_kernel" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter:
             continue
-        # rs_fast_kernel<K, MT, NT, WPS, UA, CRC> -> the label rsmi_last_kernel reports
-        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", r["Kernel_Name"])
-        key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (",UA" if m.group(5) == "true" else "") + (
-            ",CRC" if m.group(6) == "true" else "")
-        d.setdefault(key, []).append(float(r["Counter_Value"]))
+        key = label(r["Kernel_Name"])
+        if key:
+            d.setdefault(key, []).append(float(r["Counter_Value"]))
     return {k: statistics.mean(v) for k, v in d.items()}
 
 
