@@ -376,6 +376,17 @@ static void test_repair_datanode(bool batched) {
         auto want = oracle_shards(k, m, blocks[i]);
         CHECK(stored_shard(*c.dn[6], keys[i]) == want[6]);
     }
+    // a target that fails its writes: the first failing flush's error comes back (the next
+    // window's fetch, running ahead on a helper thread, only read), and nothing counts as repaired
+    if (batched) {
+        c.dn[6]->server().Wipe();
+        c.dn[6]->SetOffline(true);
+        size_t rep2 = 99;
+        Status s = c.node->RepairDataNodeBatched(0, 6, 4, &rep2);
+        CHECK(!s.ok() && s.err.find("rpc error") == 0);
+        CHECK(rep2 == 99);  // not written on failure
+        c.dn[6]->SetOffline(false);
+    }
     // bad indexes (data_recovery.go:17-22)
     CHECK(c.node->RepairDataNode(n, 0).err == "index greater than max index of nodes");
     CHECK(c.node->RepairDataNode(0, n).err == "repair index greater than max index of nodes");
