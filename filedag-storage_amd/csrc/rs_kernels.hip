@@ -649,6 +649,45 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             for (int j = 0; j < MT; j++)
     #pragma unroll
                 for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
+            // the output rows' stores (RSMI_FUSED_STORE_FIRST: issued before the output rows' CRC
+            // work, so they drain while it runs instead of after it)
+            auto store_out = [&]() {
+                if (UA && ch < cpb) {
+        #pragma unroll
+                    for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
+                } else if (!UA && ch < cpb) {
+                    const uint32_t boff = ch * 16u;
+                    if (boff + 16u <= S) {
+        #pragma unroll
+                        for (int j = 0; j < MT; j++) {
+                            const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                            if constexpr (NT == 1)
+                                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                            else
+                                *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                        }
+                    } else {
+                        // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+        #pragma unroll
+                        for (int j = 0; j < MT; j++) {
+                            uint8_t* p = ob + out_off[j] + boff;
+        #pragma unroll
+                            for (int w = 0; w < 4; w++) {
+                                const uint32_t val = acc[j][w];
+                                const uint32_t o = boff + 4u * w;
+                                if (o + 4u <= S) {
+                                    *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                                } else if (o < S) {
+                                    p[4 * w] = uint8_t(val);
+                                    if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                                    if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                                }
+                            }
+                        }
+                    }
+                }
+            };
+            if (RSMI_FUSED_STORE_FIRST) store_out();
             // the output rows: bit form by bit form, even rows before odd ones, so consecutive MFMAs
             // go to different accumulators wherever two output rows do not share one; PX: pair by
             // pair (accumulator K / 2 + h), each pair first reading out the pair two before it
@@ -689,40 +728,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                 }
             }
 
-            if (UA && ch < cpb) {
-    #pragma unroll
-                for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
-            } else if (!UA && ch < cpb) {
-                const uint32_t boff = ch * 16u;
-                if (boff + 16u <= S) {
-    #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-                        if constexpr (NT == 1)
-                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
-                        else
-                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
-                    }
-                } else {
-                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
-    #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        uint8_t* p = ob + out_off[j] + boff;
-    #pragma unroll
-                        for (int w = 0; w < 4; w++) {
-                            const uint32_t val = acc[j][w];
-                            const uint32_t o = boff + 4u * w;
-                            if (o + 4u <= S) {
-                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
-                            } else if (o < S) {
-                                p[4 * w] = uint8_t(val);
-                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
-                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
-                            }
-                        }
-                    }
-                }
-            }
+            if (!RSMI_FUSED_STORE_FIRST) store_out();
             if (UA && fix) {
                 // an opaque base: the reloads must not be merged with the row loop's loads (that
                 // would keep every row's window live through the tile)

@@ -12,12 +12,12 @@ for i in 1 2; do
   python3 -c "import json; j=json.load(open('gpurun_out/r04a/ua_split_$i.json')); print('split: encode', j['roofline']['achieved'], 'reconstruct', j['reconstruct']['achieved_GBs'], j['reconstruct']['kernel'], j['verify']['verified'])"
 done
 # the fused variants must be bit-exact before they are timed
-for v in v_px v_pxi; do
+for v in v_px v_pxi v_pxis; do
   RSMI_LIB=$PWD/tools/build/$v/lib/librsmi.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_crc16.py -k "fused or dev_crc" > gpurun_out/r04a/pytest_$v.log 2>&1 || { echo "pytest $v failed"; tail -30 gpurun_out/r04a/pytest_$v.log; exit 1; }
   echo "$v: $(tail -1 gpurun_out/r04a/pytest_$v.log)"
 done
 for rep in 1 2; do
-  for lib in "" tools/build/v_idle/lib/librsmi.so tools/build/v_px/lib/librsmi.so tools/build/v_pxi/lib/librsmi.so; do
+  for lib in "" tools/build/v_idle/lib/librsmi.so tools/build/v_px/lib/librsmi.so tools/build/v_pxi/lib/librsmi.so tools/build/v_pxis/lib/librsmi.so; do
     RSMI_LIB=${lib:+$PWD/$lib} timeout -k 10 200 python tools/fusedab.py >> gpurun_out/r04a/fused_ab.txt 2>gpurun_out/r04a/fused_ab.err || { echo "fusedab failed"; tail gpurun_out/r04a/fused_ab.err; exit 1; }
     RSMI_LIB=${lib:+$PWD/$lib} FUSED_SHAPE=16,4,256,4194304 timeout -k 10 200 python tools/fusedab.py >> gpurun_out/r04a/fused_ab.txt 2>>gpurun_out/r04a/fused_ab.err || { echo "fusedab failed"; tail gpurun_out/r04a/fused_ab.err; exit 1; }
   done
