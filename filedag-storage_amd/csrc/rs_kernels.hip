@@ -437,8 +437,13 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     // read-out below sums and reads out over the nt active waves only.
     if (wid >= nt) return;
 #endif
+#ifndef RSMI_DIAG_CACHED
     const uint8_t* ib = in + uint64_t(blk) * in_bs;
     uint8_t* ob = out + uint64_t(blk) * out_bs;
+#else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only
+    const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
+    uint8_t* ob = out + uint64_t(blk & 15) * out_bs;
+#endif
 
 #ifdef RSMI_FUSED_RING  // diagnostic: rows in flight
     constexpr int P = K < RSMI_FUSED_RING ? K : RSMI_FUSED_RING;
