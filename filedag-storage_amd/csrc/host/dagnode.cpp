@@ -124,6 +124,21 @@ void DagNode::fan_keys(int count, const std::function<void(int)>& f) {
         for (int i = 0; i < count; i++) f(i);
 }
 
+void DagNode::copy_bytes(uint8_t* dst, const uint8_t* src, size_t n) {
+    // a lone caller's bulk copies into page-locked staging run on the idle fan-out pool (one core
+    // copies ~10-20 GB/s, a few together saturate far more of the socket's bandwidth)
+    constexpr size_t kPart = size_t(64) << 10;
+    const int parts = int(std::min<size_t>(4, n / kPart));
+    if (parts < 2 || !parallel_ || !fan_ || active_.load() > 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    fan_->run(parts, [&](int t) {
+        const size_t a = n * size_t(t) / size_t(parts), b = n * size_t(t + 1) / size_t(parts);
+        std::memcpy(dst + a, src + a, b - a);
+    });
+}
+
 DagNode::~DagNode() { Close(); }
 
 void DagNode::Close() {
@@ -264,8 +279,23 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     uint8_t* flat = block.empty() ? nullptr : block_scratch(size_t(n) * S);
     if (!block.empty() && !flat) return Status::Error("out of host memory");
     std::vector<uint32_t> raw(gpu_checksums_ && !block.empty() ? size_t(n) : 0), raw32(want32 ? size_t(n) : 0);
-    s = enc.EncodeDataFlat(block, flat, raw.empty() ? nullptr : raw.data(), raw32.empty() ? nullptr : raw32.data());
-    if (!s.ok()) return s;
+    if (!block.empty() && active_.load() <= 1) {
+        // a lone caller (nothing to coalesce with): Split into the page-locked buffer here, the
+        // copy spread over the idle fan-out pool, then one zero-copy kernel codes it in place
+        const size_t k = size_t(config_.data_blocks);
+        copy_bytes(flat, block.data(), block.size());
+        std::memset(flat + block.size(), 0, k * S - block.size());  // Split zero-padding
+        int rc;
+        rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+        if (!ctx) return rsmi_status(rc);
+        rc = raw.empty() ? rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1)
+                         : rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1,
+                                                       raw.data(), raw32.empty() ? nullptr : raw32.data());
+        if (rc) return rsmi_status(rc);
+    } else {
+        s = enc.EncodeDataFlat(block, flat, raw.empty() ? nullptr : raw.data(), raw32.empty() ? nullptr : raw32.data());
+        if (!s.ok()) return s;
+    }
     phase_add(Phase::Codec, t0);
     const auto t1 = PhaseClock::now();
     const int wq = EntryQuorum().second;
@@ -529,24 +559,77 @@ void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>
     }
 }
 
+// A lone caller's degraded read: DecodeDataBlocks (erasure.go:70-83) with the survivors copied
+// into the page-locked block scratch over the fan-out pool, the missing data rows rebuilt there
+// in place by one zero-copy kernel, and the block (the first BlockSize bytes of the k data rows,
+// node.go:311-319) taken straight from it.  *done = false leaves the call to the per-shard path:
+// nothing to decode, or shard lengths that are not the block's shard size; every error the
+// per-shard path would return (rsmi_check_shards, the decode) is returned the same way.
+Status DagNode::decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done) {
+    *done = false;
+    const int k = config_.data_blocks, n = int(f.shards.size());
+    if (n != int(nodes_.size())) return Status::Ok();
+    bool any_empty = false, all_empty = true, data_missing = false;
+    for (int i = 0; i < n; i++) {
+        any_empty |= f.shards[i].empty();
+        all_empty &= f.shards[i].empty();
+        data_missing |= i < k && f.shards[i].empty();
+    }
+    if (!any_empty || all_empty || !data_missing) return Status::Ok();  // no decode runs
+    std::vector<size_t> lens(static_cast<size_t>(n));
+    std::vector<uint8_t> present(static_cast<size_t>(n));
+    for (int i = 0; i < n; i++) {
+        lens[i] = f.shards[i].size();
+        present[i] = f.shards[i].empty() ? 0 : 1;
+    }
+    size_t S2 = 0;
+    int rc = rsmi_check_shards(n, lens.data(), 1, &S2);
+    if (rc) return rsmi_status(rc);
+    if (S2 != S || S == 0) return Status::Ok();
+    int np = 0;
+    for (int i = 0; i < n; i++) np += present[i];
+    if (np < k) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);
+    rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+    if (!ctx) return rsmi_status(rc);
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
+    // the survivors the decode reads (the first k present) are the only rows it needs
+    for (int i = 0, used = 0; i < n && used < k; i++)
+        if (present[i]) {
+            copy_bytes(flat + size_t(i) * S, f.shards[i].data(), S);
+            used++;
+        }
+    rc = rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), 1);
+    if (rc) return rsmi_status(rc);
+    const size_t bs = size_t(f.meta.block_size);
+    block->assign(flat, flat + std::min(bs, size_t(k) * S));
+    block->resize(bs);
+    *done = true;
+    return Status::Ok();
+}
+
 Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  // node.go:277-326
     Erasure enc;
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, f.meta.block_size, &enc, device_);
     if (!s.ok()) return s;
-    s = enc.DecodeDataBlocks(f.shards);
-    if (!s.ok()) return s;
     const size_t S = size_t(enc.ShardSize());
-    // the first k shards concatenated and truncated to BlockSize (node.go:311-319), copied
-    // once (no zero fill of the whole block first)
-    const size_t bs = size_t(f.meta.block_size);
-    block->clear();
-    block->reserve(bs);
-    for (int i = 0; i < config_.data_blocks && block->size() < bs; i++) {
-        const size_t take = std::min(bs - block->size(), std::min(S, f.shards[i].size()));
-        block->insert(block->end(), f.shards[i].begin(), f.shards[i].begin() + long(take));
-        if (take < S && block->size() < bs) block->resize(std::min(bs, block->size() + (S - take)), 0);
+    bool done = false;
+    if (active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok())) return s;
+    if (!done) {
+        s = enc.DecodeDataBlocks(f.shards);
+        if (!s.ok()) return s;
+        // the first k shards concatenated and truncated to BlockSize (node.go:311-319), copied
+        // once (no zero fill of the whole block first)
+        const size_t bs = size_t(f.meta.block_size);
+        block->clear();
+        block->reserve(bs);
+        for (int i = 0; i < config_.data_blocks && block->size() < bs; i++) {
+            const size_t take = std::min(bs - block->size(), std::min(S, f.shards[i].size()));
+            block->insert(block->end(), f.shards[i].begin(), f.shards[i].begin() + long(take));
+            if (take < S && block->size() < bs) block->resize(std::min(bs, block->size() + (S - take)), 0);
+        }
+        block->resize(bs);
     }
-    block->resize(bs);
     if (!f.repair.empty()) {  // the shards move into the task: `f` is spent after this
         const int32_t bs = f.meta.block_size;
         std::lock_guard<std::mutex> g(q_mu_);
@@ -860,6 +943,9 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
         if (!GetSize(key, &size).ok()) continue;
         std::vector<Bytes> shards;
         if (!fetch_for_repair(key, to, &shards).ok()) continue;
+        bool done = false;
+        if (active_.load() == 0 && (s = repair_row_in_place(key, size, shards, to, &done), !s.ok())) return s;
+        if (done) continue;
         Erasure enc;
         s = Erasure::New(config_.data_blocks, config_.parity_blocks, size, &enc, device_);
         if (!s.ok()) return s;
@@ -868,6 +954,63 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
         s = nodes_[to].client->Put(key, encode_meta(size), shards[to]);
         if (!s.ok()) return s;
     }
+    return Status::Ok();
+}
+
+// RepairDataNode's per-key rebuild and write (data_recovery.go:95-106) for a lone caller: the k
+// survivors the decode reads are copied into the page-locked block scratch over the fan-out pool,
+// only the repaired node's row is rebuilt there in place (with its checksums when the Put
+// carries sender checksums, as RepairDataNodeBatched's), and the datanode gets a view of it.
+// *done = false leaves the key to the per-shard path (an empty block, shard lengths that are not
+// the block's shard size); the decode's errors are returned as the per-shard path returns them.
+Status DagNode::repair_row_in_place(const std::string& key, int size, const std::vector<Bytes>& shards, int to,
+                                    bool* done) {
+    *done = false;
+    const int k = config_.data_blocks, n = int(nodes_.size());
+    if (size <= 0 || int(shards.size()) != n) return Status::Ok();
+    const size_t S = rsmi_shard_size(size_t(size), k);
+    std::vector<size_t> lens(static_cast<size_t>(n));
+    std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
+    for (int i = 0; i < n; i++) {
+        lens[i] = shards[i].size();
+        present[i] = shards[i].empty() ? 0 : 1;
+    }
+    size_t S2 = 0;
+    int rc = rsmi_check_shards(n, lens.data(), 1, &S2);
+    if (rc) return rsmi_status(rc);
+    if (S2 != S || present[to]) return Status::Ok();
+    int np = 0;
+    for (int i = 0; i < n; i++) np += present[i];
+    if (np < k) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);
+    required[to] = 1;
+    rsmi_ctx* ctx = shared_context(k, config_.parity_blocks, device_, &rc);
+    if (!ctx) return rsmi_status(rc);
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
+    for (int i = 0, used = 0; i < n && used < k; i++)
+        if (present[i]) {
+            copy_bytes(flat + size_t(i) * S, shards[i].data(), S);
+            used++;
+        }
+    DataNodeClient& target = *nodes_[to].client;
+    const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
+    std::vector<uint32_t> r16(gpu_checksums_ ? size_t(n) : 0), r32(want32 ? size_t(n) : 0);
+    rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, 1, present.data(),
+                                                                required.data(), r16.data(), want32 ? r32.data() : nullptr)
+                        : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), required.data());
+    if (rc) return rsmi_status(rc);
+    const Bytes meta = encode_meta(size);
+    const ByteView row(flat + size_t(to) * S, S);
+    Status s;
+    if (!gpu_checksums_) {
+        s = target.Put(key, meta, row);
+    } else {
+        const uint16_t c16 = entry_checksum(meta, S, r16[size_t(to)]);
+        s = want32 ? target.PutWithChecksums(key, meta, row, c16, value_checksum(meta, S, c16, r32[size_t(to)]))
+                   : target.PutWithChecksum(key, meta, row, c16);
+    }
+    if (!s.ok()) return s;
+    *done = true;
     return Status::Ok();
 }
 

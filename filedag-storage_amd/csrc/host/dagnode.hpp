@@ -161,6 +161,8 @@ private:
     void verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>& st, const std::vector<char>& skip,
                         std::vector<char>* bad);
     Status finish_get(const std::string& key, Fetched& f, Bytes* block);
+    Status decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done);
+    Status repair_row_in_place(const std::string& key, int size, const std::vector<Bytes>& shards, int to, bool* done);
     Status get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online);
     Status repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,
                         const std::vector<int>& indexes);
@@ -189,6 +191,8 @@ private:
     std::atomic<size_t> last_shard_{0};   // shard size of the latest Put / Get (for GetMeta)
     std::unique_ptr<FanOut> fan_;
     void fan(int count, const std::function<void(int)>& f, size_t shard_bytes);
+    // memcpy, spread over the fan-out pool for a lone caller's large copies
+    void copy_bytes(uint8_t* dst, const uint8_t* src, size_t n);
     // whole-key tasks (GetMany): on the pool for a lone caller, whatever the shard size
     void fan_keys(int count, const std::function<void(int)>& f);
     struct Active {  // counts a caller for the fan-out policy
