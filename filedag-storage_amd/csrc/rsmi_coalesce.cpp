@@ -25,30 +25,76 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
     return c->h_coal;
 }
 
+// A group whose requests' shard buffers are page-locked, coded where they lie (see
+// run_coalesced_group).  Encode: each block is Split into its own buffer first (the caller's
+// block is pageable), outside the context lock.
+int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S) {
+    const size_t k = size_t(c->k), n = size_t(c->n);
+    const std::string& key = rq[0]->key;
+    const bool enc = key[0] == 'E';
+    bool want16 = false, want32 = false;
+    if (enc)
+        for (size_t j = 0; j < nb; j++) {
+            std::memcpy(rq[j]->out, rq[j]->block, rq[j]->B);
+            std::memset(rq[j]->out + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
+            want16 |= rq[j]->raw != nullptr;
+            want32 |= rq[j]->raw32 != nullptr;
+        }
+    std::vector<uint8_t> present(n), want(n);
+    if (!enc) {
+        const char* f = key.c_str() + key.find(':') + 1;
+        for (size_t i = 0; i < n; i++) {
+            present[i] = uint8_t(f[i] == '1');
+            want[i] = uint8_t(f[n + i] == '1');
+        }
+    }
+    std::vector<uint32_t> r16(want16 ? nb * n : 0), r32(want32 ? nb * n : 0);
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIP_TRY(hipSetDevice(c->device));
+        std::shared_ptr<Plan> plan;
+        int rc = enc ? encode_plan(c, plan) : reconstruct_plan(c, present.data(), want.data(), plan);
+        if (rc) return rc;
+        if (want16 && (rc = reserve(c->d_crc, c->crc_cap, nb * n * 4))) return rc;
+        if (want32 && (rc = reserve(c->d_crc32, c->crc32_cap, nb * n * 4))) return rc;
+        hipStream_t st = c->staging[0].stream;
+        for (size_t j = 0; j < nb; j++) {
+            uint8_t* dev = host_alias(rq[j]->out, n * S);
+            if (!dev) return RSMI_ERR_DEVICE;
+            if (enc)
+                rc = launch_encode_rows(c, *plan, dev, n * S, dev + k * S, n * S, S, 1,
+                                        want16 ? reinterpret_cast<uint32_t*>(c->d_crc) + j * n : nullptr,
+                                        want32 ? reinterpret_cast<uint32_t*>(c->d_crc32) + j * n : nullptr, st);
+            else
+                rc = launch_plan(c, *plan, dev, S, n * S, dev, S, n * S, S, 1, st);
+            if (rc) return rc;
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        if (want16) HIP_TRY(hipMemcpy(r16.data(), c->d_crc, nb * n * 4, hipMemcpyDeviceToHost));
+        if (want32) HIP_TRY(hipMemcpy(r32.data(), c->d_crc32, nb * n * 4, hipMemcpyDeviceToHost));
+    }
+    for (size_t j = 0; j < nb; j++) {
+        if (rq[j]->raw) std::memcpy(rq[j]->raw, r16.data() + j * n, n * 4);
+        if (rq[j]->raw32) std::memcpy(rq[j]->raw32, r32.data() + j * n, n * 4);
+    }
+    return RSMI_OK;
+}
+
 // One group of a coalesced batch: same request key, i.e. same kind and shard size (and,
 // for reconstruct, the same survivor pattern and requested rows).
 void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     const std::string& key = rq[0]->key;
     const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
-    // A lone request whose shard buffer is page-locked (the host mirror's block scratch) is coded
-    // in place: the host paths run it as one zero-copy kernel on that buffer, so neither the
-    // staging copy in nor the n*S copy back out happens (per-block DagNode.Put / degraded Get)
-    if (nb == 1 && host_alias(rq[0]->out, n * S)) {
-        rsmi_ctx::CoalReq& r = *rq[0];
-        if (key[0] == 'E') {
-            std::memcpy(r.out, r.block, r.B);
-            std::memset(r.out + r.B, 0, k * S - r.B);  // Split zero-padding
-            r.rc = encode_host_impl(c, r.out, n * S, r.out + k * S, n * S, S, 1, r.raw, r.raw32);
-        } else {
-            const char* f = key.c_str() + key.find(':') + 1;
-            std::vector<uint8_t> present(n), want(n);
-            for (size_t i = 0; i < n; i++) {
-                present[i] = uint8_t(f[i] == '1');
-                want[i] = uint8_t(f[n + i] == '1');
-            }
-            r.rc = reconstruct_host_impl(c, r.out, n * S, S, 1, present.data(), want.data());
-        }
+    // Requests whose shard buffers are all page-locked (the host mirror's block scratch) are coded
+    // in place: one zero-copy launch per request on the context's stream and one synchronisation
+    // for the group, so neither the staging copy in nor the n*S copy back out happens (per-block
+    // DagNode.Put and degraded Gets from many threads)
+    bool pinned = true;
+    for (size_t j = 0; j < nb && pinned; j++) pinned = host_alias(rq[j]->out, n * S) != nullptr;
+    if (pinned) {
+        const int rc = run_coalesced_in_place(c, rq, nb, S);
+        for (size_t j = 0; j < nb; j++) rq[j]->rc = rc;
         return;
     }
     uint8_t* h = coal_stage(c, nb * n * S);

@@ -143,6 +143,32 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
     return RSMI_OK;
 }
 
+// The encode of nblocks blocks whose rows lie at in / out (device addresses: device memory or
+// aliases of page-locked host memory), stream-ordered, no synchronisation: R(row) of every row
+// into d16[b*n + r] (the CRC fused into the encode where the plan allows it, else a separate
+// pass over the rows) and R32(row) into d32, either may be null (device buffers, b*n + r).
+int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
+                       size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st) {
+    const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
+    int rc;
+    if (d16 && S >= 16 && k <= 16 && m <= 4) {
+        if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, d16, st))) return rc;
+    } else {
+        if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
+        if (d16) {
+            HIP_TRY(hipMemsetAsync(d16, 0, nblocks * n * 4, st));
+            if ((rc = launch_crc(c, in, S, in_bs, uint32_t(k), S, nblocks, d16, n, st, false))) return rc;
+            if ((rc = launch_crc(c, out, S, out_bs, uint32_t(m), S, nblocks, d16 + k, n, st, false))) return rc;
+        }
+    }
+    if (d32) {
+        HIP_TRY(hipMemsetAsync(d32, 0, nblocks * n * 4, st));
+        if ((rc = launch_crc32(c, in, S, in_bs, uint32_t(k), S, nblocks, d32, n, st))) return rc;
+        if ((rc = launch_crc32(c, out, S, out_bs, uint32_t(m), S, nblocks, d32 + k, n, st))) return rc;
+    }
+    return RSMI_OK;
+}
+
 int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                             size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;

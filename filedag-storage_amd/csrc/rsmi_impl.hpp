@@ -190,7 +190,10 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
                              size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                     size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
+int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
+                       size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
+int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S);
 void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb);
 void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch);
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req);

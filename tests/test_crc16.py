@@ -382,6 +382,75 @@ def test_coalesced_lone_call_in_place_on_page_locked_buffer(k, m, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (16, 4, 1048576 + 14), (2, 1, 4099)])
+def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B):
+    """Concurrent coalesced encodes and degraded reconstructs (DagNode.Put / Get from many
+    goroutines, node.go:358-408, :277-326) whose shard buffers are each page-locked: the group is
+    coded where the buffers lie, one zero-copy launch per request and one synchronisation, with
+    no staging.  Every shard, raw CRC-16 and rebuilt row equals the oracle's, and the calls did
+    coalesce."""
+    import ctypes
+    import threading
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    T = 12
+    rng = np.random.default_rng(B)
+    blocks = [bytes(rng.integers(0, 256, size=B, dtype=np.uint8)) for _ in range(T)]
+    want = []
+    for b in blocks:
+        w = orc.split(k, m, b)
+        w[k:] = orc.encode(k, m, w[:k])
+        want.append(w)
+    ptrs = [L.rsmi_host_alloc(n * S) for _ in range(T)]
+    assert all(ptrs)
+    try:
+        views = [np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S) for p in ptrs]
+        raws = [(ctypes.c_uint32 * n)() for _ in range(T)]
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_us", 3000)
+            c.set_option("coalesce_max", T)
+            srcs = [bytearray(b) for b in blocks]
+            rcs = [None] * T
+
+            def enc(t):
+                rcs[t] = L.rsmi_encode_block_coalesced(
+                    c._h, ctypes.addressof((ctypes.c_char * B).from_buffer(srcs[t])), B, ptrs[t], raws[t])
+
+            th = [threading.Thread(target=enc, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert rcs == [0] * T
+            assert c.stat("coalesced_batches") < c.stat("coalesced_calls") == T
+            for t in range(T):
+                assert np.array_equal(views[t], want[t]), t
+                for r in range(n):
+                    assert rsmi.crc16_entry(b"", raws[t][r], S) == orc.crc16_ibm(want[t][r].tobytes()), (t, r)
+            lost = [0, k] if m >= 2 else [0]
+            present = (ctypes.c_uint8 * n)(*[0 if r in lost else 1 for r in range(n)])
+            for t in range(T):
+                views[t][lost] = 0xEE
+
+            def rec(t):
+                rcs[t] = L.rsmi_reconstruct_coalesced(c._h, ptrs[t], S, present, 0)
+
+            th = [threading.Thread(target=rec, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert rcs == [0] * T
+            for t in range(T):
+                assert np.array_equal(views[t], want[t]), t
+    finally:
+        for p in ptrs:
+            L.rsmi_host_free(p)
+
+
+@pytest.mark.gpu
 def test_coalesced_host_fault_reports_err_host():
     """A coalesced batch whose executor throws std::bad_alloc (option "inject_host_fault") fails
     its requests with RSMI_ERR_HOST, the status the boundary gives host-resource exceptions
