@@ -430,17 +430,11 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint32_t blk = u / upb;
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
     const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
-#if RSMI_FUSED_COOP && RSMI_FUSED_IDLE_EXIT
-    // A block's last unit may hold fewer tiles than waves (RS(10,4) 256 KiB: 26 tiles, the 7th
-    // unit has 2): its idle waves end here instead of holding their slots until the unit's
-    // barrier.  s_barrier waits only on the workgroup's waves that have not ended, and the
-    // read-out below sums and reads out over the nt active waves only.
-    if (wid >= nt) return;
-#endif
 #ifndef RSMI_DIAG_CACHED
     const uint8_t* ib = in + uint64_t(blk) * in_bs;
     uint8_t* ob = out + uint64_t(blk) * out_bs;
-#else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only
+#else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only, so
+       // the launch time is the kernel's own issue time
     const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
     uint8_t* ob = out + uint64_t(blk & 15) * out_bs;
 #endif
@@ -456,35 +450,9 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #pragma unroll
     for (int j = 0; j < MT; j++) out_off[j] = uint64_t(plan->out_row[j]) * out_rs;
 
-    // PX (RSMI_FUSED_PX, aligned layouts with K even): a tile's counts of each accumulator's two
-    // shards are turned into their parities as soon as the pair's MFMAs are done (per tile the
-    // counts stay below 2^11, so bits 0 and 12 are exact), into one record byte per accumulator
-    // packed four to a dword (pk); the tiles of a unit then combine by XOR, since the parity of a
-    // sum is the XOR of the parities.  Two accumulators rotate over the pairs instead of NACC
-    // living through the tile (28 -> 8 VGPRs for RS(10,4)), and the workgroup's reduction moves
-    // NACC bytes per lane through LDS instead of NACC f32x4.
-    constexpr bool PX = RSMI_FUSED_PX && !UA && K % 2 == 0;
-    constexpr int NPK = (NACC + 3) / 4;
-    mfma_v4f cacc[PX ? 2 : NACC];
+    mfma_v4f cacc[NACC];
 #pragma unroll
-    for (int a = 0; a < (PX ? 2 : NACC); a++) cacc[a] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
-    uint32_t pk[NPK];
-#pragma unroll
-    for (int i = 0; i < NPK; i++) pk[i] = 0;
-    // accumulator a's record byte: bits 0-3 / 4-7 = parity of element e of shard 2a / 2a + 1
-    auto parity_byte = [](const mfma_v4f& c) -> uint32_t {
-        uint32_t y = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) y |= (uint32_t(c[e]) & 0x1001u) << e;
-        return (y | (y >> 8)) & 0xFFu;
-    };
-    // PX: accumulator a's parities into pk, and its slot cleared for the pair two ahead
-    auto readout = [&](int a) {
-        if constexpr (PX) {
-            pk[a / 4] ^= parity_byte(cacc[a & 1]) << (8 * (a % 4));
-            cacc[a & 1] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
-        }
-    };
+    for (int a = 0; a < NACC; a++) cacc[a] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
 
 #if RSMI_FUSED_COOP
     static_assert(kFusedUnitTiles == kWG / kWave, "one tile per wave of the unit's workgroup");
@@ -543,7 +511,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #endif
         // one MFMA: bit form q of row r's chunk x into the row's accumulator
         auto crc_mfma = [&](const u32x4& x, int r, int q) {
-            mfma_v4f& acc = cacc[PX ? (r / 2) & 1 : r / 2];
+            mfma_v4f& acc = cacc[r / 2];
 #if defined(RSMI_FUSED_DIAG) && RSMI_FUSED_DIAG == 3  // diagnostic: no CRC work at all
             return;
 #endif
@@ -572,7 +540,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         // keep the MFMAs where they are issued: the accumulators are only read after the tile
         // loop, so without an anchor the MFMAs sink to the loop's end and every row's bit forms
         // stay live
-        auto anchor = [&](int r) { asm volatile("" : "+v"(cacc[PX ? (r / 2) & 1 : r / 2])); };
+        auto anchor = [&](int r) { asm volatile("" : "+v"(cacc[r / 2])); };
         // the tile's body; UA: the row's last tile with S % 16 != 0 moves its last window to its
         // chunk position (a separate copy, so the common tiles carry none of it)
         auto tile_body = [&]() {
@@ -599,9 +567,6 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                 u32x4 T[5];
     #pragma unroll
                 for (int f = 0; f < 5; f++) T[f] = Tn[f];
-                // PX: pair c / 2 takes the slot of pair c / 2 - 2, whose last MFMA issued two rows
-                // of GF work ago
-                if (PX && c % 2 == 0 && c >= 4) readout(c / 2 - 2);
     #pragma unroll
                 for (int w = 0; w < 4; w++) {
                     const uint32_t x = u4get(v[slot], w);
@@ -654,72 +619,16 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             for (int j = 0; j < MT; j++)
     #pragma unroll
                 for (int w = 0; w < 4; w++) asm volatile("" : "+v"(acc[j][w]));
-            // the output rows' stores (RSMI_FUSED_STORE_FIRST: issued before the output rows' CRC
-            // work, so they drain while it runs instead of after it)
-            auto store_out = [&]() {
-                if (UA && ch < cpb) {
-        #pragma unroll
-                    for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
-                } else if (!UA && ch < cpb) {
-                    const uint32_t boff = ch * 16u;
-                    if (boff + 16u <= S) {
-        #pragma unroll
-                        for (int j = 0; j < MT; j++) {
-                            const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-                            if constexpr (NT == 1)
-                                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
-                            else
-                                *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
-                        }
-                    } else {
-                        // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
-        #pragma unroll
-                        for (int j = 0; j < MT; j++) {
-                            uint8_t* p = ob + out_off[j] + boff;
-        #pragma unroll
-                            for (int w = 0; w < 4; w++) {
-                                const uint32_t val = acc[j][w];
-                                const uint32_t o = boff + 4u * w;
-                                if (o + 4u <= S) {
-                                    *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
-                                } else if (o < S) {
-                                    p[4 * w] = uint8_t(val);
-                                    if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
-                                    if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
-                                }
-                            }
-                        }
-                    }
-                }
-            };
-            if (RSMI_FUSED_STORE_FIRST) store_out();
             // the output rows: bit form by bit form, even rows before odd ones, so consecutive MFMAs
-            // go to different accumulators wherever two output rows do not share one; PX: pair by
-            // pair (accumulator K / 2 + h), each pair first reading out the pair two before it
-            if constexpr (PX) {
+            // go to different accumulators wherever two output rows do not share one
     #pragma unroll
-                for (int h = 0; h < (MT + 1) / 2; h++) {
-                    if (K / 2 + h >= 2) readout(K / 2 + h - 2);
+            for (int q = 0; q < 4; q++)
     #pragma unroll
-                    for (int q = 0; q < 4; q++)
+                for (int h = 0; h < 2; h++)
     #pragma unroll
-                        for (int j = 2 * h; j < 2 * h + 2 && j < MT; j++)
-                            crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
-                    anchor(K + 2 * h);
-                }
-                // the last two pairs
-                if (NACC >= 2) readout(NACC - 2);
-                readout(NACC - 1);
-            } else {
+                    for (int j = h; j < MT; j += 2) crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
     #pragma unroll
-                for (int q = 0; q < 4; q++)
-    #pragma unroll
-                    for (int h = 0; h < 2; h++)
-    #pragma unroll
-                        for (int j = h; j < MT; j += 2) crc_mfma(u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]}, K + j, q);
-    #pragma unroll
-                for (int j = 0; j < MT; j++) anchor(K + j);
-            }
+            for (int j = 0; j < MT; j++) anchor(K + j);
             // UA: every row's last window went in unshifted; correct the output rows' counts here
             // and the input rows' after the stores (reloaded: a shifted copy of every row in flight
             // would not fit the registers)
@@ -733,7 +642,40 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                 }
             }
 
-            if (!RSMI_FUSED_STORE_FIRST) store_out();
+            if (UA && ch < cpb) {
+    #pragma unroll
+                for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
+            } else if (!UA && ch < cpb) {
+                const uint32_t boff = ch * 16u;
+                if (boff + 16u <= S) {
+    #pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                        if constexpr (NT == 1)
+                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                        else
+                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                    }
+                } else {
+                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+    #pragma unroll
+                    for (int j = 0; j < MT; j++) {
+                        uint8_t* p = ob + out_off[j] + boff;
+    #pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const uint32_t val = acc[j][w];
+                            const uint32_t o = boff + 4u * w;
+                            if (o + 4u <= S) {
+                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                            } else if (o < S) {
+                                p[4 * w] = uint8_t(val);
+                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                            }
+                        }
+                    }
+                }
+            }
             if (UA && fix) {
                 // an opaque base: the reloads must not be merged with the row loop's loads (that
                 // would keep every row's window live through the tile)
@@ -757,37 +699,12 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 
     // parities -> the unit's record: byte (accumulator a, lane slot), bits i / 4 + i = element i's
     // parity of shard 2 a / 2 a + 1 (bits 0 and 12 of the exact count)
-    auto store_rec = [&](int a, uint32_t byte) {
-        crc_rec[(uint64_t(u) * NACC + a) * kWave + (lane & 15u) * 4u + (lane >> 4)] = uint8_t(byte);
+    auto record = [&](int a, const mfma_v4f& c) {
+        uint32_t y = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) y |= (uint32_t(c[e]) & 0x1001u) << e;
+        crc_rec[(uint64_t(u) * NACC + a) * kWave + (lane & 15u) * 4u + (lane >> 4)] = uint8_t(y | (y >> 8));
     };
-    auto record = [&](int a, const mfma_v4f& c) { store_rec(a, parity_byte(c)); };
-    if constexpr (PX) {
-#if RSMI_FUSED_COOP
-        // the unit's tiles meet by XOR of their packed parity bytes
-        __shared__ uint32_t s_px[PX ? kWG / kWave : 1][PX ? NPK : 1][kWave];
-#pragma unroll
-        for (int i = 0; i < NPK; i++) s_px[wid][i][lane] = pk[i];
-        __syncthreads();
-#if RSMI_FUSED_IDLE_EXIT
-        const uint32_t nw = nt;
-#else
-        const uint32_t nw = kWG / kWave;
-#endif
-        if (wid == 0) {
-#pragma unroll
-            for (int i = 0; i < NPK; i++) {
-                uint32_t x = s_px[0][i][lane];
-                for (uint32_t w = 1; w < nw; w++) x ^= s_px[w][i][lane];
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    if (4 * i + b < NACC) store_rec(4 * i + b, x >> (8 * b));
-            }
-        }
-#else
-#pragma unroll
-        for (int a = 0; a < NACC; a++) store_rec(a, pk[a / 4] >> (8 * (a % 4)));
-#endif
-    } else {
 #if RSMI_FUSED_COOP
     // the unit's four tiles meet in LDS (count sums stay below 2^24: exact), and wave w reads out
     // accumulators w, w + 4, ..., so no wave is left with the whole unit's tail
@@ -795,16 +712,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #pragma unroll
     for (int a = 0; a < NACC; a++) s_red[wid][a][lane] = cacc[a];
     __syncthreads();
-#if RSMI_FUSED_IDLE_EXIT
-    for (int a = int(wid); a < NACC; a += int(nt)) {  // only the nt active waves wrote counts
-        mfma_v4f c = s_red[0][a][lane];
-        for (uint32_t w = 1; w < nt; w++) c += s_red[w][a][lane];
-        record(a, c);
-    }
-#else
     for (int a = int(wid); a < NACC; a += kWG / kWave)
         record(a, s_red[0][a][lane] + s_red[1][a][lane] + s_red[2][a][lane] + s_red[3][a][lane]);
-#endif
 #if RSMI_FUSED_INLINE_COMBINE
     // The block's last unit to finish combines its records into R(row) (no second launch).  Each
     // workgroup publishes its record (fence, then one atomic increment of the block's counter);
@@ -829,7 +738,6 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #pragma unroll
     for (int a = 0; a < NACC; a++) record(a, cacc[a]);
 #endif
-    }
 }
 
 

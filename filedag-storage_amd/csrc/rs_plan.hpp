@@ -64,15 +64,6 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #ifndef RSMI_FUSED_UNIT
 #define RSMI_FUSED_UNIT 4
 #endif
-#ifndef RSMI_FUSED_PX  // 1: per-tile parity read-out, units combined by XOR (rs_fused_mfma_kernel)
-#define RSMI_FUSED_PX 0
-#endif
-#ifndef RSMI_FUSED_STORE_FIRST  // 1: the fused kernel stores its output rows before their CRC work
-#define RSMI_FUSED_STORE_FIRST 0
-#endif
-#ifndef RSMI_FUSED_IDLE_EXIT  // 1: a unit's workgroup lets its waves without a tile end at once
-#define RSMI_FUSED_IDLE_EXIT 0
-#endif
 #ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
 #define RSMI_FUSED_COOP 1
 #endif
