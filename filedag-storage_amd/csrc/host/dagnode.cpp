@@ -613,8 +613,8 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
     Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, f.meta.block_size, &enc, device_);
     if (!s.ok()) return s;
     const size_t S = size_t(enc.ShardSize());
-    bool done = false;
-    if (active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok())) return s;
+    bool done = f.assembled;  // GetMany's batch decode already wrote the block
+    if (!done && active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok())) return s;
     if (!done) {
         s = enc.DecodeDataBlocks(f.shards);
         if (!s.ok()) return s;
@@ -783,12 +783,15 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                             redo_after[q] = 1;
                     }
                 }
+                // each block straight from the staging (its k data rows are the Split buffer: the
+                // first BlockSize bytes, node.go:311-319), without copying the rebuilt rows into
+                // the key's shards first; a key to be fetched again keeps nothing from here
                 fan_keys(int(nb), [&](int j) {
-                    for (int c = 0; c < k; c++)
-                        if (!present[c]) {
-                            const uint8_t* row = flat + (j * n + c) * S;
-                            fs[g.second[b0 + j]].shards[c].assign(row, row + S);
-                        }
+                    const size_t q = g.second[b0 + j];
+                    if (redo_after[q]) return;
+                    const uint8_t* base = flat + size_t(j) * n * S;
+                    (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
+                    fs[q].assembled = true;
                 });
             }
         }

@@ -152,6 +152,7 @@ private:
         // deferred verification (GetMany): the accepted shards' entry metas and stored checksums
         std::vector<Bytes> metas;
         std::vector<DataNodeClient::Stored> stored;
+        bool assembled = false;  // GetMany: the block was taken from the batch decode's staging
     };
     // defer_verify: with GPU-verified reads on, accept the first wave's shards unchecked and keep
     // their stored checksums in f, for one batched check across many keys (verify_fetched)
