@@ -127,8 +127,10 @@ void DagNode::fan_keys(int count, const std::function<void(int)>& f) {
 void DagNode::copy_bytes(uint8_t* dst, const uint8_t* src, size_t n) {
     // a lone caller's bulk copies into page-locked staging run on the idle fan-out pool (one core
     // copies ~10-20 GB/s, a few together saturate far more of the socket's bandwidth)
-    constexpr size_t kPart = size_t(64) << 10;
-    const int parts = int(std::min<size_t>(4, n / kPart));
+    // only for copies large enough to repay waking pool threads (a 256 KiB block copies in
+    // ~15 us on one core, about what the hand-off costs)
+    constexpr size_t kPart = size_t(256) << 10, kMin = size_t(1) << 20;
+    const int parts = n < kMin ? 1 : int(std::min<size_t>(8, n / kPart));
     if (parts < 2 || !parallel_ || !fan_ || active_.load() > 1) {
         std::memcpy(dst, src, n);
         return;
@@ -279,7 +281,7 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     uint8_t* flat = block.empty() ? nullptr : block_scratch(size_t(n) * S);
     if (!block.empty() && !flat) return Status::Error("out of host memory");
     std::vector<uint32_t> raw(gpu_checksums_ && !block.empty() ? size_t(n) : 0), raw32(want32 ? size_t(n) : 0);
-    if (!block.empty() && active_.load() <= 1) {
+    if (!block.empty() && lone_paths_ && active_.load() <= 1) {
         // a lone caller (nothing to coalesce with): Split into the page-locked buffer here, the
         // copy spread over the idle fan-out pool, then one zero-copy kernel codes it in place
         const size_t k = size_t(config_.data_blocks);
@@ -614,7 +616,8 @@ Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  
     if (!s.ok()) return s;
     const size_t S = size_t(enc.ShardSize());
     bool done = f.assembled;  // GetMany's batch decode already wrote the block
-    if (!done && active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok())) return s;
+    if (!done && lone_paths_ && active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok()))
+        return s;
     if (!done) {
         s = enc.DecodeDataBlocks(f.shards);
         if (!s.ok()) return s;
@@ -947,7 +950,8 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
         std::vector<Bytes> shards;
         if (!fetch_for_repair(key, to, &shards).ok()) continue;
         bool done = false;
-        if (active_.load() == 0 && (s = repair_row_in_place(key, size, shards, to, &done), !s.ok())) return s;
+        if (lone_paths_ && active_.load() == 0 && (s = repair_row_in_place(key, size, shards, to, &done), !s.ok()))
+            return s;
         if (done) continue;
         Erasure enc;
         s = Erasure::New(config_.data_blocks, config_.parity_blocks, size, &enc, device_);
@@ -961,9 +965,9 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
 }
 
 // RepairDataNode's per-key rebuild and write (data_recovery.go:95-106) for a lone caller: the k
-// survivors the decode reads are copied into the page-locked block scratch over the fan-out pool,
-// only the repaired node's row is rebuilt there in place (with its checksums when the Put
-// carries sender checksums, as RepairDataNodeBatched's), and the datanode gets a view of it.
+// survivors the decode reads are copied into the page-locked block scratch, only the repaired
+// node's row is rebuilt there in place, and the datanode gets a view of it with a plain Put (the
+// datanode's own carry-less CRC of one row costs less than a GPU checksum pass and its read-back).
 // *done = false leaves the key to the per-shard path (an empty block, shard lengths that are not
 // the block's shard size); the decode's errors are returned as the per-shard path returns them.
 Status DagNode::repair_row_in_place(const std::string& key, int size, const std::vector<Bytes>& shards, int to,
@@ -995,23 +999,9 @@ Status DagNode::repair_row_in_place(const std::string& key, int size, const std:
             copy_bytes(flat + size_t(i) * S, shards[i].data(), S);
             used++;
         }
-    DataNodeClient& target = *nodes_[to].client;
-    const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
-    std::vector<uint32_t> r16(gpu_checksums_ ? size_t(n) : 0), r32(want32 ? size_t(n) : 0);
-    rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, 1, present.data(),
-                                                                required.data(), r16.data(), want32 ? r32.data() : nullptr)
-                        : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), required.data());
+    rc = rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), required.data());
     if (rc) return rsmi_status(rc);
-    const Bytes meta = encode_meta(size);
-    const ByteView row(flat + size_t(to) * S, S);
-    Status s;
-    if (!gpu_checksums_) {
-        s = target.Put(key, meta, row);
-    } else {
-        const uint16_t c16 = entry_checksum(meta, S, r16[size_t(to)]);
-        s = want32 ? target.PutWithChecksums(key, meta, row, c16, value_checksum(meta, S, c16, r32[size_t(to)]))
-                   : target.PutWithChecksum(key, meta, row, c16);
-    }
+    Status s = nodes_[to].client->Put(key, encode_meta(size), ByteView(flat + size_t(to) * S, S));
     if (!s.ok()) return s;
     *done = true;
     return Status::Ok();

@@ -129,6 +129,12 @@ public:
     // busy) and shards of at least this many bytes (in-process datanode calls on small
     // shards cost less than a thread hand-off).  Default 128 KiB (tools/bench_dagnode).
     void SetFanoutMinBytes(size_t v) { fanout_min_ = v; }
+    // A lone caller's per-block Put, degraded Get and per-key RepairDataNode code the block in
+    // place in the page-locked block scratch (Split copy, one zero-copy kernel, the datanodes or
+    // the block reading views of it) instead of through Erasure's shard vectors and the engine's
+    // group commit.  On by default; the stored entries and returned blocks are identical either
+    // way (off: tools/bench_dagnode's A/B legs).
+    void SetLoneCallerPaths(bool v) { lone_paths_ = v; }
     std::pair<int, int> EntryQuorum() const;  // (read, write)
     size_t RepairQueueLen();
     // Per-phase host time of Put / PutMany / RepairDataNodeBatched (diagnostic, off by default):
@@ -187,6 +193,7 @@ private:
     void verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas, const std::vector<Bytes>& data,
                      const std::vector<DataNodeClient::Stored>& stored, std::vector<Status>& got);
     bool parallel_ = true;
+    bool lone_paths_ = true;
     size_t fanout_min_ = size_t(128) << 10;
     std::atomic<int> active_{0};          // caller threads inside the public calls
     std::atomic<size_t> last_shard_{0};   // shard size of the latest Put / Get (for GetMeta)

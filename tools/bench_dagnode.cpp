@@ -81,6 +81,13 @@ int main(int argc, char** argv) {
     const double putb = secs(t0);
     phase_json("putmany", putb);
     d->SetPhaseTiming(false);
+    // the same per-block Puts with the lone-caller path off (Erasure's shard vectors and the
+    // group commit, as in round 3): a same-box A/B of that path
+    d->SetLoneCallerPaths(false);
+    t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Put(keys[i], blocks[i]);
+    const double put1n = secs(t0);
+    d->SetLoneCallerPaths(true);
     // Put from 16 threads at once: the per-block encodes coalesce into GPU batches
     const int T = 16;
     long c0 = 0, b0 = 0;
@@ -112,6 +119,11 @@ int main(int argc, char** argv) {
     t0 = clk::now();
     for (int i = 0; i < N; i++) d->Get(keys[i], &got);
     const double get1 = secs(t0);
+    d->SetLoneCallerPaths(false);
+    t0 = clk::now();
+    for (int i = 0; i < N; i++) d->Get(keys[i], &got);
+    const double get1n = secs(t0);
+    d->SetLoneCallerPaths(true);
     std::vector<Bytes> gm;
     std::vector<Status> st;
     double getb = 0;
@@ -168,6 +180,12 @@ int main(int argc, char** argv) {
     t0 = clk::now();
     d->RepairDataNode(0, rj);
     const double rep1 = secs(t0);
+    dn[size_t(rj)]->server().Wipe();
+    d->SetLoneCallerPaths(false);
+    t0 = clk::now();
+    d->RepairDataNode(0, rj);
+    const double rep1n = secs(t0);
+    d->SetLoneCallerPaths(true);
     dn[size_t(rj)]->server().Wipe();
     size_t rep = 0;
     d->SetPhaseTiming(true);
@@ -242,8 +260,10 @@ int main(int argc, char** argv) {
     std::printf("RESULT {\"codec\": \"gpu\", ");
 #endif
     std::printf("\"k\": %d, \"m\": %d, \"B\": %zu, \"N\": %d, \"put\": %.3f, \"putmany\": %.3f, \"put_threads\": %.3f, "
-                "\"get\": %.3f, \"getmany\": %.3f, \"get_threads\": %.3f, \"repair\": %.3f, \"repair_batched\": %.3f}\n",
-                k, m, B, N, gib / put1, gib / putb, gib / putT, gib / get1, gib / getb, gib / getT, gib / rep1, gib / repb);
+                "\"get\": %.3f, \"getmany\": %.3f, \"get_threads\": %.3f, \"repair\": %.3f, \"repair_batched\": %.3f, "
+                "\"put_nolone\": %.3f, \"get_nolone\": %.3f, \"repair_nolone\": %.3f}\n",
+                k, m, B, N, gib / put1, gib / putb, gib / putT, gib / get1, gib / getb, gib / getT, gib / rep1, gib / repb,
+                gib / put1n, gib / get1n, gib / rep1n);
 #ifdef FAKE_RSMI_FAST
     std::printf("PHASES {\"codec\": \"cpu\", \"k\": %d, \"m\": %d, \"B\": %zu, %s}\n", k, m, B, phases.c_str());
 #else

@@ -9,7 +9,9 @@ import sys
 
 LEGS = [("put", "Put, per block"), ("putmany", "PutMany"), ("put_threads", "Put, 16 threads"),
         ("get", "Get, per block (1 lost shard)"), ("getmany", "GetMany"), ("get_threads", "Get, 16 threads"),
-        ("repair", "RepairDataNode"), ("repair_batched", "RepairDataNodeBatched")]
+        ("repair", "RepairDataNode"), ("repair_batched", "RepairDataNodeBatched"),
+        ("put_nolone", "Put, per block, lone-caller path off"), ("get_nolone", "Get, per block, lone-caller path off"),
+        ("repair_nolone", "RepairDataNode, lone-caller path off")]
 
 
 def phases(path):
@@ -49,7 +51,8 @@ def main(path):
         for key, name in LEGS:
             cells, med = [], {}
             for codec in ("gpu", "cpu"):
-                v = [r[key] for r in rows if r["codec"] == codec and (r["k"], r["m"], r["B"], r["N"]) == (k, m, B, N)]
+                v = [r[key] for r in rows if r["codec"] == codec and (r["k"], r["m"], r["B"], r["N"]) == (k, m, B, N)
+                     and key in r]
                 if v:
                     med[codec] = statistics.median(v)
                     cells.append(f"{med[codec]:.2f} [{min(v):.2f}-{max(v):.2f}] ({len(v)})")
