@@ -10,6 +10,8 @@
 #include <random>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../include/rsmi.h"
 
 using clk = std::chrono::steady_clock;
@@ -49,6 +51,26 @@ int main() {
         const double r_pin = median_us([&] { return rsmi_reconstruct(c, pout, S, present.data(), 1); });
         std::vector<uint32_t> raw(n);
         const double ec_pg = median_us([&] { return rsmi_encode_block_crc(c, blk.data(), B, out.data(), raw.data()); });
+        // the lone DagNode.Put's codec call: Split already in the page-locked (k+m)*S buffer,
+        // one in-place encode with every shard's CRC-16
+        std::memcpy(pout, blk.data(), B);
+        const double ec_inplace = median_us([&] {
+            return rsmi_encode_batch_host_crcs(c, pout, n * S, pout + k * S, n * S, S, 1, raw.data(), nullptr);
+        });
+        // what the engine pays per pointer lookup (hipPointerGetAttributes) on page-locked and
+        // pageable memory
+        const double attr_pin = median_us([&] {
+            hipPointerAttribute_t a{};
+            return hipPointerGetAttributes(&a, pout) == hipSuccess ? RSMI_OK : RSMI_ERR_DEVICE;
+        }, 1000);
+        const double attr_pg = median_us([&] {
+            hipPointerAttribute_t a{};
+            (void)hipPointerGetAttributes(&a, out.data());
+            (void)hipGetLastError();
+            return RSMI_OK;
+        }, 1000);
+        std::printf("B=%8zu  encode in place + CRC-16 (lone Put) %8.1f us pinned | hipPointerGetAttributes %.2f us "
+                    "pinned, %.2f us pageable\n", B, ec_inplace, attr_pin, attr_pg);
         std::printf("B=%8zu  encode_block %8.1f us pageable %8.1f us pinned | reconstruct(1 lost) %8.1f us pageable "
                     "%8.1f us pinned  (%.2f / %.2f GiB/s pageable) | encode_block_crc %8.1f us pageable\n",
                     B, e_pg, e_pin, r_pg, r_pin, B / e_pg / 1073.741824, B / r_pg / 1073.741824, ec_pg);
