@@ -388,7 +388,9 @@ __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uin
 // lane alone (the counts only matter mod 2), for the output rows from registers and for the input
 // rows from a reload, so the common tiles carry none of it.  Workgroups take XCD-contiguous units,
 // as the UA coding kernels do.
-template <int K, int MT, int NT, int WPS, bool UA = false>
+// INL (small launches, a block of a few units): the block's last unit to finish combines its
+// records into R(row) itself, so the call needs no second launch (below).
+template <int K, int MT, int NT, int WPS, bool UA = false, bool INL = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
                                                               const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                               uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -714,26 +716,29 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     __syncthreads();
     for (int a = int(wid); a < NACC; a += kWG / kWave)
         record(a, s_red[0][a][lane] + s_red[1][a][lane] + s_red[2][a][lane] + s_red[3][a][lane]);
-#if RSMI_FUSED_INLINE_COMBINE
-    // The block's last unit to finish combines its records into R(row) (no second launch).  Each
-    // workgroup publishes its record (fence, then one atomic increment of the block's counter);
-    // atomicInc wraps the counter back to 0 at the block's last unit, so the counters are ready
-    // for the next launch without a memset.
-    __threadfence();
-    __syncthreads();
-    __shared__ uint32_t s_last;
-    if (threadIdx.x == 0) s_last = atomicInc(ctr + blk, upb - 1) == upb - 1 ? 1u : 0u;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    __shared__ uint32_t s_p4[kCrcP4Words];
-    for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
-    __syncthreads();
-    const uint8_t* rb = crc_rec + uint64_t(blk) * upb * NACC * kWave;
-    for (uint32_t p = wid; p < uint32_t(NSH + 3) / 4; p += kWG / kWave)
-        crc16_combine_rows(reinterpret_cast<const uint16_t*>(s_p4), rb, upb, NACC, NSH, sh, raw + uint64_t(blk) * NSH,
-                           p, lane);
-#endif
+    if constexpr (INL) {
+        // The block's last unit to finish combines its records into R(row) (no second launch).
+        // Each workgroup publishes its record (fence, then one atomic increment of the block's
+        // counter); atomicInc wraps the counter back to 0 at the block's last unit, so the
+        // counters are ready for the next launch without a memset.  The agent-scope release writes
+        // back the XCD's L2 (the 8 XCDs' L2s are not coherent with each other): per unit of a
+        // 4096-block launch that cost 25x the separate combine (8.2 ms against 0.33), so only
+        // launches of a few units take this form (rsmi_crc.cpp, kFusedInlineUnits).
+        __threadfence();
+        __syncthreads();
+        __shared__ uint32_t s_last;
+        if (threadIdx.x == 0) s_last = atomicInc(ctr + blk, upb - 1) == upb - 1 ? 1u : 0u;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        __shared__ uint32_t s_p4[INL ? kCrcP4Words : 1];
+        for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
+        __syncthreads();
+        const uint8_t* rb = crc_rec + uint64_t(blk) * upb * NACC * kWave;
+        for (uint32_t p = wid; p < uint32_t(NSH + 3) / 4; p += kWG / kWave)
+            crc16_combine_rows(reinterpret_cast<const uint16_t*>(s_p4), rb, upb, NACC, NSH, sh,
+                               raw + uint64_t(blk) * NSH, p, lane);
+    }
 #else
 #pragma unroll
     for (int a = 0; a < NACC; a++) record(a, cacc[a]);
@@ -1382,6 +1387,15 @@ static void fill_km(FastKernelTable& t) {
     t.fused_ua[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true>);
 }
 
+// the in-kernel combine for small launches, for the encode shapes of the BASELINE configs (other
+// shapes take the two-launch form)
+template <int K, int MT>
+static void fill_inl(FastKernelTable& t) {
+    constexpr int NT = auto_nt(K, MT);
+    t.fused_inl[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, false, true>);
+    t.fused_ua_inl[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true, true>);
+}
+
 template <int K>
 static void fill_k(FastKernelTable& t) {
     fill_km<K, 1>(t);
@@ -1403,6 +1417,10 @@ const FastKernelTable& fast_kernels() {
         fill_k<10>(x);
         fill_k<12>(x);
         fill_k<16>(x);
+        fill_inl<2, 1>(x);
+        fill_inl<4, 2>(x);
+        fill_inl<10, 4>(x);
+        fill_inl<16, 4>(x);
         return x;
     }();
     return t;

@@ -36,6 +36,8 @@ struct FastKernelTable {
     void* ua_crc[17][kMaxMT + 1];
     void* fused[17][kMaxMT + 1];     // aligned, the CRC-16 folded on the matrix cores (rs_fused_mfma_kernel)
     void* fused_ua[17][kMaxMT + 1];  // the same on unaligned-window layouts (S >= 16)
+    void* fused_inl[17][kMaxMT + 1];     // fused with the combine in the kernel (small launches;
+    void* fused_ua_inl[17][kMaxMT + 1];  // null: the two-launch form)
 };
 
 const FastKernelTable& fast_kernels();
@@ -67,13 +69,12 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #ifndef RSMI_FUSED_COOP  // 1: a workgroup codes a unit (one tile per wave); 0: one wave codes a unit
 #define RSMI_FUSED_COOP 1
 #endif
-// 1 (with COOP, diagnostic): each block's last unit combines its records in the fused kernel.
-// Measured 8.2 ms instead of ~0.33 ms: the agent-scope release each unit needs before its
-// counter increment writes back its XCD's L2 (the 8 XCDs' L2s are not coherent with each
-// other), so the separate combine launch (0, the default) stays.
-#ifndef RSMI_FUSED_INLINE_COMBINE
-#define RSMI_FUSED_INLINE_COMBINE 0
+// launches of at most this many units combine their records in the fused kernel (one launch
+// instead of two; larger ones keep the separate combine, see rs_fused_mfma_kernel INL)
+#ifndef RSMI_FUSED_INLINE_UNITS
+#define RSMI_FUSED_INLINE_UNITS 64
 #endif
+constexpr uint32_t kFusedInlineUnits = RSMI_FUSED_INLINE_UNITS;
 // fused encode + CRC on the matrix cores: tiles per wave (one unit), 1, 2 or 4 (the two-shard
 // accumulators stay exact up to 4 tiles)
 constexpr int kFusedUnitTiles = RSMI_FUSED_UNIT;

@@ -180,7 +180,11 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
         const uint64_t e = uint64_t(((int64_t(S) - int64_t(upb) * unit_bytes) % int64_t(kCrcOrder) + kCrcOrder) % kCrcOrder);
         Crc16Shift sh;
         for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), e);
-        constexpr bool inline_combine = RSMI_FUSED_COOP && RSMI_FUSED_INLINE_COMBINE;
+        // a launch of a few units (the per-block calls of DagNode.Put) combines in the kernel: one
+        // launch instead of two; big ones keep the separate combine (rs_fused_mfma_kernel INL)
+        void* inl_fn = aligned ? fast_kernels().fused_inl[tile.K][tile.MT] : fast_kernels().fused_ua_inl[tile.K][tile.MT];
+        const bool inline_combine = RSMI_FUSED_COOP && inl_fn && nblocks * upb <= kFusedInlineUnits;
+        if (inline_combine) fn = inl_fn;
         // per-block unit counters of the inline combine: zeroed once when allocated, and every
         // launch leaves them at zero again (atomicInc wraps at the block's last unit)
         if (inline_combine && c->fctr_cap < nblocks) {
@@ -221,8 +225,8 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         }
         char buf[96];
-        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s", tile.K, tile.MT,
-                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA");
+        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s%s", tile.K, tile.MT,
+                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA", inline_combine ? ",INL" : "");
         c->last_kernel = buf;
         return hip_status(hipGetLastError());
     }

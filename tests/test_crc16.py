@@ -585,6 +585,49 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opts):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (4, 2, 262144), (16, 4, 4194304), (10, 4, 1048576)])
+@pytest.mark.parametrize("layout", ["pitched", "split"])
+def test_fused_inline_combine_small_launches(k, m, B, layout):
+    """A fused encode + CRC-16 launch of at most kFusedInlineUnits (64) units -- DagNode.Put's
+    per-block call, node.go:358-408 with server.go:57-80's checksum -- combines its records in
+    the kernel (",INL": the block's last unit, found by a per-block counter that wraps back to
+    zero) instead of a second launch.  Repeated launches (the counters must be back at zero),
+    1..N blocks, and a launch just past the limit (the two-launch form) all give the oracle's
+    parity and R(row)."""
+    import torch
+
+    n = k + m
+    S = (B + k - 1) // k
+    tpb = ((S + 15) // 16 + 63) // 64
+    upb = (tpb + 3) // 4
+    rs = rsmi.recommended_pitch(S) if layout == "pitched" else S
+    nb_max = 64 // upb
+    for nb in sorted({1, 2, max(1, nb_max), nb_max + 1}):
+        data = np.random.default_rng(nb + S).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+        host = np.zeros((nb, n, rs), dtype=np.uint8)
+        host[:, :k, :S] = data
+        want = orc.encode_fast(k, m, data)
+        with rsmi.Codec(k, m) as c:
+            for rep in range(3):
+                d = torch.from_numpy(host.reshape(-1).copy()).cuda()
+                raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+                base = d.data_ptr()
+                c.encode_batch_dev_crc(base, rs, n * rs, base + k * rs, rs, n * rs, S, nb, raw.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                kern = c.last_kernel()
+                assert kern.startswith("rs_fused_mfma_kernel"), kern
+                assert (",INL" in kern) == (nb * upb <= 64), (nb, kern)
+                got = d.cpu().numpy().reshape(nb, n, rs)
+                assert np.array_equal(got[:, k:, :S], want), (nb, rep)
+                r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+                for b in range(nb):
+                    rows = list(data[b]) + list(want[b])
+                    for i in range(n):
+                        assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (nb, rep, b, i)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m,S,nb,lost,pinned", [(10, 4, 26215, 24, [0], True), (10, 4, 26215, 24, [3, 11], False),
                                                   (10, 4, 26215, 9, [2, 5, 7, 9], True), (4, 2, 65536, 8, [1], True),
                                                   (16, 4, 4097, 5, [0, 15], True), (3, 2, 7, 6, [1], True),
