@@ -406,6 +406,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #ifdef RSMI_FUSED_WSTAGE  // diagnostic: the weights staged in LDS by every workgroup (16 KiB)
     __shared__ u32x4 s_w[kCrcFWWords / 4];
 #endif
+    // INL: the combine's power tables, staged with the coding tables (off the combine's path)
+    __shared__ uint32_t s_p4[INL ? kCrcP4Words : 1];
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
@@ -414,6 +416,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         const u32x4* w = reinterpret_cast<const u32x4*>(crc_tbl + kCrcFWOff);
         for (int i = threadIdx.x; i < kCrcFWWords / 4; i += kWG) s_w[i] = w[i];
 #endif
+        if constexpr (INL)
+            for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
     }
     __syncthreads();
 
@@ -455,6 +459,50 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     mfma_v4f cacc[NACC];
 #pragma unroll
     for (int a = 0; a < NACC; a++) cacc[a] = mfma_v4f{0.f, 0.f, 0.f, 0.f};
+
+    // the output rows of one tile: the lane's chunk ch (UA: its window at byte win)
+    auto store_out = [&](uint32_t ch, uint32_t win, const uint32_t (&acc)[MT][4]) {
+        if (UA && ch < cpb) {
+#pragma unroll
+            for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
+        } else if (!UA && ch < cpb) {
+            const uint32_t boff = ch * 16u;
+            if (boff + 16u <= S) {
+#pragma unroll
+                for (int j = 0; j < MT; j++) {
+                    const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+                    if constexpr (NT == 1)
+                        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
+                    else
+                        *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
+                }
+            } else {
+                // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
+#pragma unroll
+                for (int j = 0; j < MT; j++) {
+                    uint8_t* p = ob + out_off[j] + boff;
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const uint32_t val = acc[j][w];
+                        const uint32_t o = boff + 4u * w;
+                        if (o + 4u <= S) {
+                            *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
+                        } else if (o < S) {
+                            p[4 * w] = uint8_t(val);
+                            if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
+                            if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
+                        }
+                    }
+                }
+            }
+        }
+    };
+    // INL: the output rows are stored after the unit's record is published, so the publish's
+    // release waits for the record alone, not for the rows' writes (over PCIe when the call
+    // codes page-locked host memory in place); one tile per wave (COOP) keeps them in registers
+    constexpr bool kDefer = INL && RSMI_FUSED_COOP && RSMI_FUSED_INL_DEFER;
+    uint32_t dacc[kDefer ? MT : 1][4];
+    uint32_t dch = ~0u, dwin = 0u;
 
 #if RSMI_FUSED_COOP
     static_assert(kFusedUnitTiles == kWG / kWave, "one tile per wave of the unit's workgroup");
@@ -644,39 +692,15 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                 }
             }
 
-            if (UA && ch < cpb) {
+            if constexpr (kDefer) {
     #pragma unroll
-                for (int j = 0; j < MT; j++) st16u<NT == 1>(ob + out_off[j] + win, u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]});
-            } else if (!UA && ch < cpb) {
-                const uint32_t boff = ch * 16u;
-                if (boff + 16u <= S) {
+                for (int j = 0; j < MT; j++)
     #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-                        if constexpr (NT == 1)
-                            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(ob + out_off[j]) + ch);
-                        else
-                            *(reinterpret_cast<u32x4*>(ob + out_off[j]) + ch) = o;
-                    }
-                } else {
-                    // the row's last, partial chunk (1..15 bytes): whole dwords, then bytes
-    #pragma unroll
-                    for (int j = 0; j < MT; j++) {
-                        uint8_t* p = ob + out_off[j] + boff;
-    #pragma unroll
-                        for (int w = 0; w < 4; w++) {
-                            const uint32_t val = acc[j][w];
-                            const uint32_t o = boff + 4u * w;
-                            if (o + 4u <= S) {
-                                *reinterpret_cast<uint32_t*>(p + 4 * w) = val;
-                            } else if (o < S) {
-                                p[4 * w] = uint8_t(val);
-                                if (o + 1u < S) p[4 * w + 1] = uint8_t(val >> 8);
-                                if (o + 2u < S) p[4 * w + 2] = uint8_t(val >> 16);
-                            }
-                        }
-                    }
-                }
+                    for (int w = 0; w < 4; w++) dacc[j][w] = acc[j][w];
+                dch = ch;
+                dwin = win;
+            } else {
+                store_out(ch, win, acc);
             }
             if (UA && fix) {
                 // an opaque base: the reloads must not be merged with the row loop's loads (that
@@ -724,15 +748,27 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         // back the XCD's L2 (the 8 XCDs' L2s are not coherent with each other): per unit of a
         // 4096-block launch that cost 25x the separate combine (8.2 ms against 0.33), so only
         // launches of a few units take this form (rsmi_crc.cpp, kFusedInlineUnits).
-        __threadfence();
-        __syncthreads();
-        __shared__ uint32_t s_last;
-        if (threadIdx.x == 0) s_last = atomicInc(ctr + blk, upb - 1) == upb - 1 ? 1u : 0u;
-        __syncthreads();
-        if (!s_last) return;
-        __threadfence();
-        __shared__ uint32_t s_p4[INL ? kCrcP4Words : 1];
-        for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
+        // A block of one unit needs none of it: its own workgroup wrote every record.
+#ifndef RSMI_DIAG_INL_NOFENCE  // diagnostic (wrong R for blocks of several units): the publish's cost
+        if (upb > 1u) {
+            __threadfence();
+            __syncthreads();
+            __shared__ uint32_t s_last;
+            if (threadIdx.x == 0) s_last = atomicInc(ctr + blk, upb - 1) == upb - 1 ? 1u : 0u;
+            __syncthreads();
+            if (!s_last) {
+                if constexpr (kDefer) if (dch != ~0u) store_out(dch, dwin, dacc);
+                return;
+            }
+            __threadfence();
+        }
+#else
+        if (u - blk * upb != upb - 1u) {
+            if constexpr (kDefer) if (dch != ~0u) store_out(dch, dwin, dacc);
+            return;
+        }
+#endif
+        if constexpr (kDefer) if (dch != ~0u) store_out(dch, dwin, dacc);
         __syncthreads();
         const uint8_t* rb = crc_rec + uint64_t(blk) * upb * NACC * kWave;
         for (uint32_t p = wid; p < uint32_t(NSH + 3) / 4; p += kWG / kWave)

@@ -75,6 +75,10 @@ constexpr int kCrcTableWords = kCrcFWOff + kCrcFWWords;
 #define RSMI_FUSED_INLINE_UNITS 64
 #endif
 constexpr uint32_t kFusedInlineUnits = RSMI_FUSED_INLINE_UNITS;
+// 1: such launches store the output rows after the unit's record is published (0: before it)
+#ifndef RSMI_FUSED_INL_DEFER
+#define RSMI_FUSED_INL_DEFER 1
+#endif
 // fused encode + CRC on the matrix cores: tiles per wave (one unit), 1, 2 or 4 (the two-shard
 // accumulators stay exact up to 4 tiles)
 constexpr int kFusedUnitTiles = RSMI_FUSED_UNIT;

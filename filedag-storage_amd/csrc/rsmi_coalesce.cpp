@@ -69,9 +69,14 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
                 rc = launch_plan(c, *plan, dev, S, n * S, dev, S, n * S, S, 1, st);
             if (rc) return rc;
         }
+        const uint32_t *h16, *h32;
+        if ((rc = readback(c, want16 ? reinterpret_cast<const uint32_t*>(c->d_crc) : nullptr,
+                           want32 ? reinterpret_cast<const uint32_t*>(c->d_crc32) : nullptr, nb * n * 4, st, h16,
+                           h32)))
+            return rc;
         HIP_TRY(hipStreamSynchronize(st));
-        if (want16) HIP_TRY(hipMemcpy(r16.data(), c->d_crc, nb * n * 4, hipMemcpyDeviceToHost));
-        if (want32) HIP_TRY(hipMemcpy(r32.data(), c->d_crc32, nb * n * 4, hipMemcpyDeviceToHost));
+        if (want16) std::memcpy(r16.data(), h16, nb * n * 4);
+        if (want32) std::memcpy(r32.data(), h32, nb * n * 4);
     }
     for (size_t j = 0; j < nb; j++) {
         if (rq[j]->raw) std::memcpy(rq[j]->raw, r16.data() + j * n, n * 4);

@@ -368,9 +368,13 @@ int rsmi_crc_rows_host(rsmi_ctx* c, const uint8_t* rows, size_t row_stride, size
         if ((rc = launch_crc32(c, dev, stride, stride, 1, S, nrows, reinterpret_cast<uint32_t*>(c->d_crc32), 1, st)))
             return rc;
     }
+    const uint32_t *h16, *h32;
+    if ((rc = readback(c, raw16_out ? reinterpret_cast<const uint32_t*>(c->d_crc) : nullptr,
+                       raw32_out ? reinterpret_cast<const uint32_t*>(c->d_crc32) : nullptr, sz, st, h16, h32)))
+        return rc;
     HIP_TRY(hipStreamSynchronize(st));
-    if (raw16_out) HIP_TRY(hipMemcpy(raw16_out, c->d_crc, sz, hipMemcpyDeviceToHost));
-    if (raw32_out) HIP_TRY(hipMemcpy(raw32_out, c->d_crc32, sz, hipMemcpyDeviceToHost));
+    if (raw16_out) std::memcpy(raw16_out, h16, sz);
+    if (raw32_out) std::memcpy(raw32_out, h32, sz);
     return RSMI_OK;
 } catch (...) {
     return rsmi::impl::exception_status();

@@ -75,6 +75,36 @@ uint8_t* small_stage(rsmi_ctx* c, size_t need) {
     return c->h_small;
 }
 
+// Row CRCs (device buffers d16 / d32, sz bytes each, either may be null) to the host: a copy
+// kernel per buffer into the context's page-locked read-back area, in stream order, so they
+// arrive with the call's own stream synchronisation instead of a blocking hipMemcpy after it (a second
+// round trip).  h16 / h32 are where they land; read them after that synchronisation.
+int readback(rsmi_ctx* c, const uint32_t* d16, const uint32_t* d32, size_t sz, hipStream_t st, const uint32_t*& h16,
+             const uint32_t*& h32) {
+    h16 = h32 = nullptr;
+    if (!sz || (!d16 && !d32)) return RSMI_OK;
+    if (c->h_raw_cap < 2 * sz) {
+        if (c->h_raw) (void)hipHostFree(c->h_raw);
+        c->h_raw = nullptr;
+        c->h_raw_cap = 0;
+        const size_t cap = std::max<size_t>(2 * sz, 64 << 10);
+        HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&c->h_raw), cap));
+        c->h_raw_cap = cap;
+    }
+    uint8_t* dev = host_alias(c->h_raw, 2 * sz);
+    if (!dev) return RSMI_ERR_DEVICE;
+    int rc;
+    if (d16) {
+        if ((rc = repitch(dev, sz, reinterpret_cast<const uint8_t*>(d16), sz, sz, 1, st))) return rc;
+        h16 = reinterpret_cast<const uint32_t*>(c->h_raw);
+    }
+    if (d32) {
+        if ((rc = repitch(dev + sz, sz, reinterpret_cast<const uint8_t*>(d32), sz, sz, 1, st))) return rc;
+        h32 = reinterpret_cast<const uint32_t*>(c->h_raw + sz);
+    }
+    return RSMI_OK;
+}
+
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
                         size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
@@ -325,9 +355,11 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
     uint32_t* d32 = raw32 ? reinterpret_cast<uint32_t*>(c->d_crc32) : nullptr;
     if ((raw16 || raw32) && (rc = launch_rebuilt_crcs(c, dev, S, dbs, S, nblocks, present, want, d16, d32, st)))
         return rc;
+    const uint32_t *h16, *h32;
+    if ((rc = readback(c, d16, d32, raw_sz, st, h16, h32))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
-    if (raw16) HIP_TRY(hipMemcpy(raw16, d16, raw_sz, hipMemcpyDeviceToHost));
-    if (raw32) HIP_TRY(hipMemcpy(raw32, d32, raw_sz, hipMemcpyDeviceToHost));
+    if (raw16) std::memcpy(raw16, h16, raw_sz);
+    if (raw32) std::memcpy(raw32, h32, raw_sz);
     if (hs)
         for (size_t b = 0; b < nblocks; b++)
             for (size_t i = 0; i < n; i++)
@@ -578,12 +610,12 @@ int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t bloc
             hipStream_t st = c->staging[0].stream;
             uint32_t* d = reinterpret_cast<uint32_t*>(c->d_crc);
             rc = launch_plan_crc(c, *plan, dev, S, block_stride, dev, S, block_stride, S, nblocks, d, st);
+            const uint32_t *all = nullptr, *unused;
+            if (rc == RSMI_OK) rc = readback(c, d, nullptr, nblocks * nsh * 4, st, all, unused);
             if (rc == RSMI_OK) {
                 HIP_TRY(hipStreamSynchronize(st));
-                std::vector<uint32_t> all(nblocks * nsh);
-                HIP_TRY(hipMemcpy(all.data(), d, all.size() * 4, hipMemcpyDeviceToHost));
                 for (size_t b = 0; b < nblocks; b++)
-                    std::memcpy(raw16_in + b * k, all.data() + b * nsh, k * 4);
+                    std::memcpy(raw16_in + b * k, all + b * nsh, k * 4);
                 return RSMI_OK;
             }
             if (rc != RSMI_ERR_INVALID_ARG) return rc;

@@ -107,6 +107,8 @@ struct rsmi_ctx {
     long opt_small_bytes = 2L << 20;  // host calls up to this many shard bytes run zero-copy
     uint8_t* h_small = nullptr;       // page-locked staging of small calls (pageable callers)
     size_t h_small_cap = 0;
+    uint8_t* h_raw = nullptr;  // page-locked landing area of row CRCs read back by kernel (readback)
+    size_t h_raw_cap = 0;
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;
@@ -164,6 +166,8 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
             hipStream_t stream);
 uint8_t* host_alias(void* p, size_t len);
 uint8_t* small_stage(rsmi_ctx* c, size_t need);
+int readback(rsmi_ctx* c, const uint32_t* d16, const uint32_t* d32, size_t sz, hipStream_t st, const uint32_t*& h16,
+             const uint32_t*& h32);
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,
                         size_t S, size_t nblocks, uint32_t* raw_out, uint32_t* raw32_out = nullptr);
 int encode_host_impl(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,

@@ -585,15 +585,16 @@ def test_encode_batch_dev_crc_fused(k, m, S, nb, layout, opts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (4, 2, 262144), (16, 4, 4194304), (10, 4, 1048576)])
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (4, 2, 262144), (16, 4, 4194304), (10, 4, 1048576),
+                                   (10, 4, 4096), (16, 4, 65536), (10, 4, 65536)])
 @pytest.mark.parametrize("layout", ["pitched", "split"])
 def test_fused_inline_combine_small_launches(k, m, B, layout):
     """A fused encode + CRC-16 launch of at most kFusedInlineUnits (64) units -- DagNode.Put's
     per-block call, node.go:358-408 with server.go:57-80's checksum -- combines its records in
     the kernel (",INL": the block's last unit, found by a per-block counter that wraps back to
-    zero) instead of a second launch.  Repeated launches (the counters must be back at zero),
-    1..N blocks, and a launch just past the limit (the two-launch form) all give the oracle's
-    parity and R(row)."""
+    zero; blocks of one unit, 4 KiB and 64 KiB RS(16,4), skip the counter) instead of a second
+    launch.  Repeated launches (the counters must be back at zero), 1..N blocks, and a launch just
+    past the limit (the two-launch form) all give the oracle's parity and R(row)."""
     import torch
 
     n = k + m
@@ -625,6 +626,70 @@ def test_fused_inline_combine_small_launches(k, m, B, layout):
                     rows = list(data[b]) + list(want[b])
                     for i in range(n):
                         assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (nb, rep, b, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_calls_crc_readback(pinned):
+    """Host calls that read the row CRCs back by kernel into the context's page-locked area (no
+    blocking copy after the sync), twice on one context: encode with both CRCs, the rows-CRC
+    call, the verified reconstruct and the rows rebuild with CRCs all equal the oracle, over
+    page-locked and pageable shards (DagNode.Put / Get / RepairDataNode, node.go:358-408,
+    :220-326, data_recovery.go:16-112)."""
+    k, m, S, nb = 10, 4, 26215, 3
+    n = k + m
+    data = np.random.default_rng(7 * pinned).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+    full = np.concatenate([data, orc.encode_fast(k, m, data)], axis=1)
+    r16 = [[orc.crc16_ibm(full[b, r].tobytes()) for r in range(n)] for b in range(nb)]
+    r32 = [[orc.crc32_ieee(full[b, r].tobytes()) for r in range(n)] for b in range(nb)]
+    ptr = rsmi.lib().rsmi_host_alloc(nb * n * S) if pinned else None
+    try:
+        sh = (np.ctypeslib.as_array((ctypes.c_uint8 * (nb * n * S)).from_address(ptr)).reshape(nb, n, S)
+              if pinned else np.empty((nb, n, S), dtype=np.uint8))
+        with rsmi.Codec(k, m) as c:
+            for rounds in range(2):
+                sh[:] = 0
+                sh[:, :k] = data
+                a16 = np.zeros((nb, n), dtype=np.uint32)
+                a32 = np.zeros((nb, n), dtype=np.uint32)
+                c.encode_batch_host_crcs_ptr(sh.ctypes.data, n * S, sh.ctypes.data + k * S, n * S, S, nb,
+                                             a16.ctypes.data, a32.ctypes.data)
+                assert np.array_equal(sh, full)
+                for b in range(nb):
+                    for r in range(n):
+                        assert rsmi.crc16_entry(b"", int(a16[b, r]), S) == r16[b][r], (b, r)
+                        assert rsmi.crc32_entry(b"", int(a32[b, r]), S) == r32[b][r], (b, r)
+                c16 = np.zeros(nb * n, dtype=np.uint32)
+                c32 = np.zeros(nb * n, dtype=np.uint32)
+                c.crc_rows_host_ptr(sh.ctypes.data, S, nb * n, S, c16.ctypes.data, c32.ctypes.data)
+                for b in range(nb):
+                    for r in range(n):
+                        assert rsmi.crc16_entry(b"", int(c16[b * n + r]), S) == r16[b][r], (b, r)
+                        assert rsmi.crc32_entry(b"", int(c32[b * n + r]), S) == r32[b][r], (b, r)
+                lost = [2, 11]
+                present = [i not in lost for i in range(n)]
+                sh[:, lost] = 0
+                v16 = np.zeros((nb, k), dtype=np.uint32)
+                c.reconstruct_batch_host_verify_ptr(sh.ctypes.data, n * S, S, nb, present, False, v16.ctypes.data)
+                assert np.array_equal(sh, full)
+                used = [i for i in range(n) if present[i]][:k]
+                for b in range(nb):
+                    for j, r in enumerate(used):
+                        assert rsmi.crc16_entry(b"", int(v16[b, j]), S) == r16[b][r], (b, j)
+                sh[:, lost] = 0
+                e16 = np.zeros((nb, n), dtype=np.uint32)
+                e32 = np.zeros((nb, n), dtype=np.uint32)
+                c.reconstruct_rows_batch_host_crcs_ptr(sh.ctypes.data, n * S, S, nb, present,
+                                                       [i in lost for i in range(n)], e16.ctypes.data, e32.ctypes.data)
+                assert np.array_equal(sh, full)
+                for b in range(nb):
+                    for r in lost:
+                        assert rsmi.crc16_entry(b"", int(e16[b, r]), S) == r16[b][r], (b, r)
+                        assert rsmi.crc32_entry(b"", int(e32[b, r]), S) == r32[b][r], (b, r)
+            del sh
+    finally:
+        if pinned:
+            rsmi.lib().rsmi_host_free(ptr)
 
 
 @pytest.mark.gpu

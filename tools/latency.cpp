@@ -1,7 +1,10 @@
 // latency.cpp -- per-block call latency of the C-ABI (the Dag Node's per-key Put / Get seam,
 // erasure.go:51-93): rsmi_encode_block and a 1-lost-shard rsmi_reconstruct, from pageable
 // (std::vector, like Go slices over cgo) and page-locked (rsmi_host_alloc) buffers.
-// Diagnostic; prints microseconds per call (median of 200).
+// Diagnostic; prints microseconds per call (median of 200); block sizes
+// may be given as arguments.  --sched-spin sets
+// hipDeviceScheduleSpin before the first HIP call (the runtime's polling wait), for comparison:
+// level with the default (profiles/r04/f), as was the engine polling its stream.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -31,11 +34,21 @@ static double median_us(F f, int iters = 200) {
     return t[t.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
     const int k = 10, m = 4, n = k + m;
+    std::vector<size_t> sizes;  // block sizes given on the command line, else the default list
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "--sched-spin")) {
+            if (hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) return 3;
+            std::printf("hipDeviceScheduleSpin\n");
+        } else {
+            sizes.push_back(std::strtoull(argv[i], nullptr, 10));
+        }
+    }
+    if (sizes.empty()) sizes = {4096, 65536, 262144, 1048576, 4194304};
     rsmi_ctx* c = nullptr;
     if (rsmi_open(k, m, 0, &c) != RSMI_OK) return 2;
-    for (size_t B : {size_t(4096), size_t(65536), size_t(262144), size_t(1048576), size_t(4194304)}) {
+    for (size_t B : sizes) {
         const size_t S = rsmi_shard_size(B, k);
         std::mt19937 r(1);
         std::vector<uint8_t> blk(B), out(n * S);
@@ -59,6 +72,11 @@ int main() {
         });
         // what the engine pays per pointer lookup (hipPointerGetAttributes) on page-locked and
         // pageable memory
+        // the rows-CRC call of GetMany's verify / RepairDataNode (both CRCs of the n rows)
+        std::vector<uint32_t> r32(n);
+        const double crc_rows = median_us([&] {
+            return rsmi_crc_rows_host(c, pout, S, n, S, raw.data(), r32.data());
+        });
         const double attr_pin = median_us([&] {
             hipPointerAttribute_t a{};
             return hipPointerGetAttributes(&a, pout) == hipSuccess ? RSMI_OK : RSMI_ERR_DEVICE;
@@ -69,14 +87,24 @@ int main() {
             (void)hipGetLastError();
             return RSMI_OK;
         }, 1000);
-        std::printf("B=%8zu  encode in place + CRC-16 (lone Put) %8.1f us pinned | hipPointerGetAttributes %.2f us "
-                    "pinned, %.2f us pageable\n", B, ec_inplace, attr_pin, attr_pg);
+        std::printf("B=%8zu  encode in place + CRC-16 (lone Put) %8.1f us pinned | CRC-16 + CRC-32 of the rows "
+                    "%8.1f us pinned | hipPointerGetAttributes %.2f us pinned, %.2f us pageable\n",
+                    B, ec_inplace, crc_rows, attr_pin, attr_pg);
         std::printf("B=%8zu  encode_block %8.1f us pageable %8.1f us pinned | reconstruct(1 lost) %8.1f us pageable "
                     "%8.1f us pinned  (%.2f / %.2f GiB/s pageable) | encode_block_crc %8.1f us pageable\n",
                     B, e_pg, e_pin, r_pg, r_pin, B / e_pg / 1073.741824, B / r_pg / 1073.741824, ec_pg);
         rsmi_host_free(pblk);
         rsmi_host_free(pout);
     }
+    // what the rows-CRC read-back replaced: a blocking copy of a few result words after the sync
+    void* d = nullptr;
+    if (hipMalloc(&d, 4096) != hipSuccess) return 5;
+    std::vector<uint8_t> h(256);
+    const double d2h = median_us([&] {
+        return hipMemcpy(h.data(), d, 56, hipMemcpyDeviceToHost) == hipSuccess ? RSMI_OK : RSMI_ERR_DEVICE;
+    });
+    std::printf("hipMemcpy device->pageable host, 56 B: %.1f us\n", d2h);
+    (void)hipFree(d);
     rsmi_close(c);
     return 0;
 }
