@@ -40,6 +40,30 @@ constexpr int rows_in_flight() {
     return K < cap ? K : cap;
 }
 
+// A table copied into LDS in two steps: its words are loaded into registers at the kernel's
+// start and written to LDS (then one barrier) once the wave's first rows are in flight, so the
+// table's latency and the rows' overlap instead of adding up (a per-block call over PCIe is
+// latency-bound, tools/latency.cpp).  Every thread of the workgroup takes part.
+template <int N>
+struct LdsTable {
+    static constexpr int kPer = (N + kWG - 1) / kWG;
+    uint32_t r[kPer];
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ src) {
+#pragma unroll
+        for (int i = 0; i < kPer; i++) {
+            const int x = int(threadIdx.x) + i * kWG;
+            r[i] = x < N ? src[x] : 0u;
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* dst) const {
+#pragma unroll
+        for (int i = 0; i < kPer; i++) {
+            const int x = int(threadIdx.x) + i * kWG;
+            if (x < N) dst[x] = r[i];
+        }
+    }
+};
+
 // K inputs, MT (<= 4) outputs, one 16-byte chunk per lane per row.
 // NT: cache policy, 1 = nontemporal loads and stores (write-heavy tiles), 2 = nontemporal
 // loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.
@@ -408,18 +432,26 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #endif
     // INL: the combine's power tables, staged with the coding tables (off the combine's path)
     __shared__ uint32_t s_p4[INL ? kCrcP4Words : 1];
-    {
-        const uint32_t* src = plan->tbl;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
-        for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+    // the tables; INL (latency-bound launches): written to LDS once the wave's first rows are in
+    // flight (stage, below), else at once
+    LdsTable<K * kColDwords> lt;
+    lt.load(plan->tbl);
+    LdsTable<INL ? kCrcP4Words : 1> lp;
+    if constexpr (INL) lp.load(crc_tbl + kCrcP4Off);
+    __builtin_amdgcn_sched_barrier(0);
+    bool staged = false;  // wave-uniform: every wave passes the staging barrier exactly once
+    auto stage = [&]() {
+        if (staged) return;
+        lt.store(reinterpret_cast<uint32_t*>(s_tbl));
+        if constexpr (INL) lp.store(s_p4);
 #ifdef RSMI_FUSED_WSTAGE
         const u32x4* w = reinterpret_cast<const u32x4*>(crc_tbl + kCrcFWOff);
         for (int i = threadIdx.x; i < kCrcFWWords / 4; i += kWG) s_w[i] = w[i];
 #endif
-        if constexpr (INL)
-            for (int i = threadIdx.x; i < kCrcP4Words; i += kWG) s_p4[i] = crc_tbl[kCrcP4Off + i];
-    }
-    __syncthreads();
+        __syncthreads();
+        staged = true;
+    };
+    if constexpr (!INL) stage();
 
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -432,7 +464,10 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #else
     const uint32_t u = blockIdx.x * (kWG / kWave) + wid;
 #endif
-    if (u >= nunits) return;
+    if (u >= nunits) {
+        stage();
+        return;
+    }
     const uint32_t blk = u / upb;
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
     const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
@@ -604,6 +639,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             u32x4 v[P];
     #pragma unroll
             for (int c = 0; c < P; c++) v[c] = load_col(c);
+            stage();
             uint32_t acc[MT][4], pend[MT][4];
             uint32_t tb = 0;
             asm volatile("" : "+v"(tb));
@@ -722,6 +758,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
         };
         tile_body();
     }
+    stage();  // waves without a tile (the unit's last tiles past the row's end)
 
     // parities -> the unit's record: byte (accumulator a, lane slot), bits i / 4 + i = element i's
     // parity of shard 2 a / 2 a + 1 (bits 0 and 12 of the exact count)
