@@ -13,6 +13,7 @@
 #include <random>
 #include <vector>
 
+#include <emmintrin.h>
 #include <hip/hip_runtime_api.h>
 
 #include "../include/rsmi.h"
@@ -32,6 +33,24 @@ static double median_us(F f, int iters = 200) {
     }
     std::sort(t.begin(), t.end());
     return t[t.size() / 2];
+}
+
+// n bytes with streaming (non-temporal) stores: dst lands in memory, not in this core's cache
+static void copy_nt(uint8_t* dst, const uint8_t* src, size_t n) {
+    size_t i = 0;
+    while (i < n && (reinterpret_cast<uintptr_t>(dst + i) & 15)) dst[i] = src[i], i++;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    for (; i < n; i++) dst[i] = src[i];
+    _mm_sfence();
 }
 
 int main(int argc, char** argv) {
@@ -70,6 +89,29 @@ int main(int argc, char** argv) {
         const double ec_inplace = median_us([&] {
             return rsmi_encode_batch_host_crcs(c, pout, n * S, pout + k * S, n * S, S, 1, raw.data(), nullptr);
         });
+        // the lone Put's whole codec phase: the Split copy of a block that is not in cache (one
+        // of 512 distinct blocks, like tools/bench_dagnode) into the page-locked scratch, then
+        // the in-place call; the copy with plain and with streaming stores
+        {
+            const size_t nblk = 512;
+            std::vector<uint8_t> many(nblk * B);
+            for (size_t i = 0; i < many.size(); i += 64) many[i] = uint8_t(i >> 6);
+            size_t it = 0;
+            auto put_phase = [&](bool nt, bool call) {
+                return median_us([&] {
+                    const uint8_t* src = many.data() + (it++ % nblk) * B;
+                    if (nt) copy_nt(pout, src, B);
+                    else std::memcpy(pout, src, B);
+                    std::memset(pout + B, 0, k * S - B);
+                    return call ? rsmi_encode_batch_host_crcs(c, pout, n * S, pout + k * S, n * S, S, 1, raw.data(), nullptr)
+                                : RSMI_OK;
+                });
+            };
+            const double cp = put_phase(false, false), cpn = put_phase(true, false);
+            const double ph = put_phase(false, true), phn = put_phase(true, true);
+            std::printf("B=%8zu  Split copy %.1f us (streaming %.1f) | copy + in-place encode + CRC-16 %.1f us "
+                        "(streaming copy %.1f)\n", B, cp, cpn, ph, phn);
+        }
         // what the engine pays per pointer lookup (hipPointerGetAttributes) on page-locked and
         // pageable memory
         // the rows-CRC call of GetMany's verify / RepairDataNode (both CRCs of the n rows)
