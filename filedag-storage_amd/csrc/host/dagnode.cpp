@@ -2,8 +2,6 @@
 // dag/node/dagnode/node.go, data_recovery.go and error.go.
 #include "dagnode.hpp"
 
-#include <emmintrin.h>
-
 #include <algorithm>
 #include <cstring>
 #include <future>
@@ -126,51 +124,23 @@ void DagNode::fan_keys(int count, const std::function<void(int)>& f) {
         for (int i = 0; i < count; i++) f(i);
 }
 
-namespace {
-// n bytes with streaming stores: the copy lands in memory rather than in this core's cache, so
-// it skips the read-for-ownership of the destination, and the GPU's zero-copy reads of it over
-// PCIe find no dirty lines to snoop (tools/latency.cpp: a 4 MiB Split copy + in-place encode
-// 278-297 -> 252-255 us, 1 MiB 88-93 -> 78-83 us; level at 256 KiB, so used from 1 MiB)
-void copy_streaming(uint8_t* dst, const uint8_t* src, size_t n) {
-    size_t i = 0;
-    while (i < n && (reinterpret_cast<uintptr_t>(dst + i) & 15)) {
-        dst[i] = src[i];
-        i++;
-    }
-    for (; i + 64 <= n; i += 64) {
-        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
-        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
-        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
-    }
-    for (; i < n; i++) dst[i] = src[i];
-    _mm_sfence();  // the streaming stores are visible before the codec call reads them
-}
-}  // namespace
 
 void DagNode::copy_bytes(uint8_t* dst, const uint8_t* src, size_t n) {
     // a lone caller's bulk copies into page-locked staging run on the idle fan-out pool (one core
     // copies ~10-20 GB/s, a few together saturate far more of the socket's bandwidth)
     // only for copies large enough to repay waking pool threads (a 256 KiB block copies in
-    // ~15 us on one core, about what the hand-off costs); from 1 MiB with streaming stores
+    // ~15 us on one core, about what the hand-off costs); streaming stores from 1 MiB
+    // (copy_to_staging), also in each part
     constexpr size_t kPart = size_t(256) << 10, kMin = size_t(1) << 20;
     const int parts = n < kMin ? 1 : int(std::min<size_t>(8, n / kPart));
-    auto copy = [](uint8_t* d, const uint8_t* s, size_t len) {
-        if (len >= kMin / 8) copy_streaming(d, s, len);
-        else std::memcpy(d, s, len);
-    };
     if (parts < 2 || !parallel_ || !fan_ || active_.load() > 1) {
-        if (n >= kMin) copy_streaming(dst, src, n);
-        else std::memcpy(dst, src, n);
+        copy_to_staging(dst, src, n);
         return;
     }
     fan_->run(parts, [&](int t) {
         const size_t a = n * size_t(t) / size_t(parts), b = n * size_t(t + 1) / size_t(parts);
-        copy(dst + a, src + a, b - a);
+        if (b - a >= kMin / 8) copy_streaming(dst + a, src + a, b - a);
+        else std::memcpy(dst + a, src + a, b - a);
     });
 }
 

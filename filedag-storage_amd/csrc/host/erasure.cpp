@@ -1,6 +1,8 @@
 // erasure.cpp -- see erasure.hpp.
 #include "erasure.hpp"
 
+#include <emmintrin.h>
+
 #include <memory>
 
 #include <cstring>
@@ -11,6 +13,31 @@
 
 namespace rsmi {
 namespace host {
+
+void copy_streaming(uint8_t* dst, const uint8_t* src, size_t n) {
+    size_t i = 0;
+    while (i < n && (reinterpret_cast<uintptr_t>(dst + i) & 15)) {
+        dst[i] = src[i];
+        i++;
+    }
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    for (; i < n; i++) dst[i] = src[i];
+    _mm_sfence();  // the streaming stores are visible before the codec call reads them
+}
+
+void copy_to_staging(uint8_t* dst, const uint8_t* src, size_t n) {
+    if (n >= (size_t(1) << 20)) copy_streaming(dst, src, n);
+    else std::memcpy(dst, src, n);
+}
 
 Status rsmi_status(int rc) {
     switch (rc) {
@@ -120,7 +147,8 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
-    rc = rsmi_encode_block_coalesced(c, data.data(), data.size(), flat, nullptr);
+    copy_to_staging(flat, data.data(), data.size());  // Split's copy, on this thread
+    rc = rsmi_encode_block_coalesced(c, flat, data.size(), flat, nullptr);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++) (*shards)[i].assign(flat + i * S, flat + (i + 1) * S);
     return Status::Ok();
@@ -135,8 +163,10 @@ Status Erasure::EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, 
     int rc;
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
-    rc = raw ? rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat, raw, raw32)
-             : rsmi_encode_block_coalesced(c, data.data(), data.size(), flat, nullptr);
+    // Split's copy on this thread (concurrent callers copy in parallel), then coded in place
+    copy_to_staging(flat, data.data(), data.size());
+    rc = raw ? rsmi_encode_block_coalesced_crcs(c, flat, data.size(), flat, raw, raw32)
+             : rsmi_encode_block_coalesced(c, flat, data.size(), flat, nullptr);
     return rsmi_status(rc);
 }
 
@@ -155,7 +185,8 @@ Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards
     if (!flat) return Status::Error("out of host memory");
     raw->assign(size_t(n), 0);
     if (raw32) raw32->assign(size_t(n), 0);
-    rc = rsmi_encode_block_coalesced_crcs(c, data.data(), data.size(), flat, raw->data(),
+    copy_to_staging(flat, data.data(), data.size());  // Split's copy, on this thread
+    rc = rsmi_encode_block_coalesced_crcs(c, flat, data.size(), flat, raw->data(),
                                           raw32 ? raw32->data() : nullptr);
     if (rc) return rsmi_status(rc);
     for (int i = 0; i < n; i++) (*shards)[i].assign(flat + i * S, flat + (i + 1) * S);
@@ -183,11 +214,15 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
     if (np == n || (data_only && dp == data_blocks_)) return Status::Ok();
     rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
-    // [][]byte -> one contiguous buffer for the C-ABI (missing rows: don't-care bytes)
+    // [][]byte -> one contiguous buffer for the C-ABI: the first k present rows, the only ones the
+    // decode reads (upstream reconstruct(); missing and later rows: don't-care bytes)
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
-    for (int i = 0; i < n; i++)
-        if (present[i]) std::memcpy(flat + size_t(i) * S, shards[i].data(), S);
+    for (int i = 0, used = 0; i < n && used < data_blocks_; i++)
+        if (present[i]) {
+            copy_to_staging(flat + size_t(i) * S, shards[i].data(), S);
+            used++;
+        }
     // coalesced: concurrent degraded Gets usually miss the same node's shard, so they batch
     rc = rsmi_reconstruct_coalesced(c, flat, S, present.data(), data_only ? 1 : 0);
     if (rc) return rsmi_status(rc);

@@ -54,6 +54,12 @@ PinnedBuf& thread_staging();
 // The calling thread's page-locked scratch for one block's rows (single-block encodes and
 // reconstructs), separate from thread_staging; grown on demand, contents not cleared.
 uint8_t* block_scratch(size_t bytes);
+// n bytes into page-locked staging on the calling thread; from 1 MiB with streaming stores, which
+// skip the destination's read-for-ownership and leave no dirty lines for the GPU's zero-copy
+// reads to snoop (tools/latency.cpp: a 4 MiB Split copy + in-place encode 278-297 -> 252-255 us;
+// level at 256 KiB)
+void copy_to_staging(uint8_t* dst, const uint8_t* src, size_t n);
+void copy_streaming(uint8_t* dst, const uint8_t* src, size_t n);  // always streaming stores
 inline size_t staging_blocks(size_t block_bytes) {
     return block_bytes >= kStagingBytes ? 1 : kStagingBytes / block_bytes;
 }
@@ -73,7 +79,8 @@ public:
     // EncodeData into one caller buffer of (k+m) * ShardSize() bytes, shard i at i * ShardSize():
     // the Go slices Split returns alias one buffer, so the shards need no copies of their own.
     // raw / raw32 (k+m entries each, may be null): R(shard) / R32(shard) as EncodeDataWithCrcs.
-    // flat should be page-locked (block_scratch): a lone call is then coded in place.
+    // flat should be page-locked (block_scratch): the block is Split into it on the calling
+    // thread, and the call (alone or in a coalesced group) codes it in place.
     Status EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const;
     Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
     Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;

@@ -27,7 +27,9 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
 
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
 // run_coalesced_group).  Encode: each block is Split into its own buffer first (the caller's
-// block is pageable), outside the context lock.
+// block is pageable), outside the context lock -- unless the caller Split it there itself
+// (block == out), as the host mirror does, so the copies run on the callers' threads in
+// parallel instead of one after another on the executor's.
 int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S) {
     const size_t k = size_t(c->k), n = size_t(c->n);
     const std::string& key = rq[0]->key;
@@ -35,7 +37,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
     bool want16 = false, want32 = false;
     if (enc)
         for (size_t j = 0; j < nb; j++) {
-            std::memcpy(rq[j]->out, rq[j]->block, rq[j]->B);
+            if (rq[j]->block != rq[j]->out) std::memcpy(rq[j]->out, rq[j]->block, rq[j]->B);
             std::memset(rq[j]->out + rq[j]->B, 0, k * S - rq[j]->B);  // Split zero-padding
             want16 |= rq[j]->raw != nullptr;
             want32 |= rq[j]->raw32 != nullptr;

@@ -156,7 +156,10 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
  * group commit turns those calls into GPU batches.  The caller that finds no batch running
  * executes every block queued so far (waiting up to option "coalesce_us" for more, default
  * 0; at most "coalesce_max" blocks, default 256) and wakes the others; blocks arriving
- * meanwhile form the next batch.  A lone caller never waits on anyone. */
+ * meanwhile form the next batch.  A lone caller never waits on anyone.  block may be
+ * shards_out itself: the caller has already copied the block to the start of shards_out
+ * (Split's copy, done on the caller's own thread), and the engine zero-pads and encodes it in
+ * place; any other overlap of block and shards_out is not allowed. */
 int rsmi_encode_block_coalesced(rsmi_ctx* ctx, const uint8_t* block, size_t B, uint8_t* shards_out,
                                 uint32_t* raw_out);
 

@@ -136,8 +136,8 @@ void run_batch(rsmi_ctx* c, std::vector<Req*>& batch) {
     for (Req* r : batch) {
         if (r->encode) {
             const size_t S = r->S, k = size_t(c->k), n = size_t(c->n);
-            std::memset(r->out, 0, n * S);
-            std::memcpy(r->out, r->block, r->B);
+            if (r->block != r->out) std::memcpy(r->out, r->block, r->B);  // block == out: Split by the caller
+            std::memset(r->out + r->B, 0, n * S - r->B);
             r->rc = encode_one(c, r->out, r->out + k * S, S);
             for (size_t i = 0; i < n && r->rc == RSMI_OK; i++) {
                 if (r->raw16) r->raw16[i] = r16(r->out + i * S, S);

@@ -382,13 +382,40 @@ def test_coalesced_lone_call_in_place_on_page_locked_buffer(k, m, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (4, 2, 4099), (16, 4, 4194304)])
+def test_coalesced_encode_split_by_caller_pageable(k, m, B):
+    """rsmi_encode_block_coalesced with block == shards_out on pageable memory (the staging path
+    of a coalesced group): the block at the start of the buffer is zero-padded and encoded, over
+    stale bytes, with R(shard) of every shard, equal to the oracle."""
+    import ctypes
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    block = np.random.default_rng(B + 3).integers(0, 256, size=B, dtype=np.uint8)
+    want = orc.split(k, m, bytes(block))
+    want[k:] = orc.encode(k, m, want[:k])
+    buf = np.full(n * S, 0xA5, dtype=np.uint8)
+    buf[:B] = block
+    raw = (ctypes.c_uint32 * n)()
+    with rsmi.Codec(k, m) as c:
+        assert L.rsmi_encode_block_coalesced(c._h, buf.ctypes.data, B, buf.ctypes.data, raw) == 0
+    assert np.array_equal(buf.reshape(n, S), want)
+    for r in range(n):
+        assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(want[r].tobytes()), r
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (16, 4, 1048576 + 14), (2, 1, 4099)])
-def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B):
+@pytest.mark.parametrize("split_by_caller", [False, True])
+def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B, split_by_caller):
     """Concurrent coalesced encodes and degraded reconstructs (DagNode.Put / Get from many
     goroutines, node.go:358-408, :277-326) whose shard buffers are each page-locked: the group is
     coded where the buffers lie, one zero-copy launch per request and one synchronisation, with
-    no staging.  Every shard, raw CRC-16 and rebuilt row equals the oracle's, and the calls did
-    coalesce."""
+    no staging.  split_by_caller: each caller has copied its block to the start of its buffer
+    and passes the buffer as the block too (include/rsmi.h: block == shards_out), as the host
+    mirror does, over stale bytes in the padding and parity.  Every shard, raw CRC-16 and
+    rebuilt row equals the oracle's, and the calls did coalesce."""
     import ctypes
     import threading
 
@@ -413,10 +440,15 @@ def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B):
             c.set_option("coalesce_max", T)
             srcs = [bytearray(b) for b in blocks]
             rcs = [None] * T
+            if split_by_caller:
+                for t in range(T):
+                    flat = views[t].reshape(-1)
+                    flat[:] = 0xA5
+                    flat[:B] = np.frombuffer(blocks[t], dtype=np.uint8)
 
             def enc(t):
-                rcs[t] = L.rsmi_encode_block_coalesced(
-                    c._h, ctypes.addressof((ctypes.c_char * B).from_buffer(srcs[t])), B, ptrs[t], raws[t])
+                src = ptrs[t] if split_by_caller else ctypes.addressof((ctypes.c_char * B).from_buffer(srcs[t]))
+                rcs[t] = L.rsmi_encode_block_coalesced(c._h, src, B, ptrs[t], raws[t])
 
             th = [threading.Thread(target=enc, args=(t,)) for t in range(T)]
             for x in th:
