@@ -106,6 +106,7 @@ Status DagNode::New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNo
     d->slots_.assign(kClusterSlots / 8, 0);
     for (auto& c : clients) d->nodes_.push_back(StorageNode{c, false});
     d->fan_.reset(new FanOut(int(n) - 1));  // the calling thread runs one share itself
+    warm_contexts(cfg.data_blocks, cfg.parity_blocks, device);  // the codec contexts, before the first call
     *out = std::move(d);
     return Status::Ok();
 }

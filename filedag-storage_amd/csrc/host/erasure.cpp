@@ -5,11 +5,13 @@
 
 #include <memory>
 
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <new>
 #include <tuple>
+#include <vector>
 
 namespace rsmi {
 namespace host {
@@ -102,7 +104,21 @@ uint8_t* block_scratch(size_t bytes) {
 
 namespace {
 std::mutex g_ctx_mu;
-std::map<std::tuple<int, int, int>, rsmi_ctx*> g_ctx_cache;  // lives for the process
+std::map<std::tuple<int, int, int, int>, rsmi_ctx*> g_ctx_cache;  // (k, m, device, lane); lives for the process
+
+rsmi_ctx* lane_context(int k, int m, int device, int lane, int* rc) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    auto key = std::make_tuple(k, m, device, lane);
+    auto it = g_ctx_cache.find(key);
+    if (it != g_ctx_cache.end()) {
+        *rc = RSMI_OK;
+        return it->second;
+    }
+    rsmi_ctx* c = nullptr;
+    *rc = rsmi_open(k, m, device, &c);
+    if (*rc == RSMI_OK) g_ctx_cache[key] = c;
+    return c;
+}
 }  // namespace
 
 void release_shared_contexts() {
@@ -111,20 +127,34 @@ void release_shared_contexts() {
     g_ctx_cache.clear();
 }
 
-rsmi_ctx* shared_context(int k, int m, int device, int* rc) {
-    auto& mu = g_ctx_mu;
-    auto& cache = g_ctx_cache;
-    std::lock_guard<std::mutex> g(mu);
-    auto key = std::make_tuple(k, m, device);
-    auto it = cache.find(key);
-    if (it != cache.end()) {
-        *rc = RSMI_OK;
-        return it->second;
+rsmi_ctx* shared_context(int k, int m, int device, int* rc) { return lane_context(k, m, device, 0, rc); }
+
+rsmi_ctx* call_context(int k, int m, int device, int* rc) {
+    static std::atomic<unsigned> next{0};
+    thread_local const int lane = int(next.fetch_add(1) % unsigned(kCallLanes));
+    return lane_context(k, m, device, lane, rc);
+}
+
+void warm_contexts(int k, int m, int device) {
+    const size_t B = size_t(64) * size_t(k);  // S = 64: the fused encode + CRC-16 path
+    const size_t S = rsmi_shard_size(B, k);
+    std::vector<uint8_t> block(B, 1), out(size_t(k + m) * S);
+    std::vector<uint32_t> raw(size_t(k + m));
+    for (int lane = 0; lane < kCallLanes; lane++) {
+        int rc;
+        rsmi_ctx* c = lane_context(k, m, device, lane, &rc);
+        if (c) (void)rsmi_encode_block_coalesced_crcs(c, block.data(), B, out.data(), raw.data(), nullptr);
     }
-    rsmi_ctx* c = nullptr;
-    *rc = rsmi_open(k, m, device, &c);
-    if (*rc == RSMI_OK) cache[key] = c;
-    return c;
+}
+
+long lane_stat(int k, int m, int device, const char* key) {
+    long v = 0;
+    for (int lane = 0; lane < kCallLanes; lane++) {
+        int rc;
+        rsmi_ctx* c = lane_context(k, m, device, lane, &rc);
+        if (c) v += rsmi_get_stat(c, key);
+    }
+    return v;
 }
 
 Status Erasure::New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device) {
@@ -142,7 +172,7 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     shards->assign(size_t(n), Bytes());
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     uint8_t* flat = block_scratch(size_t(n) * S);
@@ -161,7 +191,7 @@ Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards,
 Status Erasure::EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const {
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     // Split's copy on this thread (concurrent callers copy in parallel), then coded in place
     copy_to_staging(flat, data.data(), data.size());
@@ -178,7 +208,7 @@ Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards
     if (raw32) raw32->clear();
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     uint8_t* flat = block_scratch(size_t(n) * S);
@@ -212,7 +242,7 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
             if (i < data_blocks_) dp++;
         }
     if (np == n || (data_only && dp == data_blocks_)) return Status::Ok();
-    rsmi_ctx* c = shared_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
     if (!c) return rsmi_status(rc);
     // [][]byte -> one contiguous buffer for the C-ABI: the first k present rows, the only ones the
     // decode reads (upstream reconstruct(); missing and later rows: don't-care bytes)

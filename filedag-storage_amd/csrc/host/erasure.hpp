@@ -24,6 +24,19 @@ int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
 // Process-wide context per (k, m, device): NewErasure runs per block in the reference
 // (node.go:277,376) but the matrix / device plans are built once.
 rsmi_ctx* shared_context(int k, int m, int device, int* rc);
+// Per-block calls from concurrent threads (Erasure's encodes and reconstructs) spread over
+// kCallLanes contexts per (k, m, device), one per calling thread in turn; lane 0 is the shared
+// context.  A context runs one host call at a time (a launch and a wait), and the GPU has room
+// for several such latency-bound calls at once (tools/latency.cpp --threads, 16 threads of
+// RS(10,4) 256 KiB coalesced encodes: 8.3 GiB/s on one context, 18.7 on four).
+constexpr int kCallLanes = 4;
+rsmi_ctx* call_context(int k, int m, int device, int* rc);
+// rsmi_get_stat summed over the lanes of (k, m, device) (the coalescing counters)
+long lane_stat(int k, int m, int device, const char* key);
+// Bring up every lane's device resources (streams, plans, CRC tables) with one tiny encode each,
+// so the first concurrent calls do not pay for them (a Dag Node does this when it starts);
+// errors are left to the real calls, which fail loudly.
+void warm_contexts(int k, int m, int device);
 // Close every shared context (process shutdown, with no call in flight).
 void release_shared_contexts();
 

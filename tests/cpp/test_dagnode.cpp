@@ -733,7 +733,7 @@ static void test_concurrent_puts() {
     int rc;
     rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
     CHECK(ctx != nullptr);
-    const long calls0 = rsmi_get_stat(ctx, "coalesced_calls"), batches0 = rsmi_get_stat(ctx, "coalesced_batches");
+    const long calls0 = lane_stat(k, m, 0, "coalesced_calls"), batches0 = lane_stat(k, m, 0, "coalesced_batches");
     std::vector<std::thread> th;
     std::vector<Status> st(size_t(T * per));
     for (int t = 0; t < T; t++)
@@ -741,8 +741,8 @@ static void test_concurrent_puts() {
             for (int j = 0; j < per; j++) st[size_t(t * per + j)] = c.node->Put(keys[t * per + j], blocks[t * per + j]);
         });
     for (auto& x : th) x.join();
-    const long calls = rsmi_get_stat(ctx, "coalesced_calls") - calls0;
-    const long batches = rsmi_get_stat(ctx, "coalesced_batches") - batches0;
+    const long calls = lane_stat(k, m, 0, "coalesced_calls") - calls0;
+    const long batches = lane_stat(k, m, 0, "coalesced_batches") - batches0;
     // a Put that finds no other caller in flight takes the lone path (no group commit), so
     // every Put is either coalesced or lone, and the concurrent ones coalesce
     CHECK(calls >= 1 && calls <= T * per);
@@ -751,7 +751,7 @@ static void test_concurrent_puts() {
     // degraded Gets from the same threads with data shard 2's node down: one erasure
     // pattern, so the per-key reconstructs coalesce; every block must come back intact
     c.dn[2]->SetOffline(true);
-    const long rc0 = rsmi_get_stat(ctx, "coalesced_calls"), rb0 = rsmi_get_stat(ctx, "coalesced_batches");
+    const long rc0 = lane_stat(k, m, 0, "coalesced_calls"), rb0 = lane_stat(k, m, 0, "coalesced_batches");
     std::vector<Bytes> got(size_t(T * per));
     std::vector<Status> gst(size_t(T * per));
     th.clear();
@@ -761,7 +761,7 @@ static void test_concurrent_puts() {
         });
     for (auto& x : th) x.join();
     c.dn[2]->SetOffline(false);
-    const long rcalls = rsmi_get_stat(ctx, "coalesced_calls") - rc0, rbatches = rsmi_get_stat(ctx, "coalesced_batches") - rb0;
+    const long rcalls = lane_stat(k, m, 0, "coalesced_calls") - rc0, rbatches = lane_stat(k, m, 0, "coalesced_batches") - rb0;
     CHECK(rcalls >= 1 && rcalls <= T * per);
     std::printf("concurrent degraded gets: %ld reconstructs in %ld GPU batches\n", rcalls, rbatches);
     for (int i = 0; i < T * per; i++) {

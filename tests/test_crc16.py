@@ -406,13 +406,15 @@ def test_coalesced_encode_split_by_caller_pageable(k, m, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (16, 4, 1048576 + 14), (2, 1, 4099)])
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (16, 4, 1048576 + 14), (2, 1, 4099), (4, 2, 262144)])
 @pytest.mark.parametrize("split_by_caller", [False, True])
 def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B, split_by_caller):
     """Concurrent coalesced encodes and degraded reconstructs (DagNode.Put / Get from many
     goroutines, node.go:358-408, :277-326) whose shard buffers are each page-locked: the group is
     coded where the buffers lie, one zero-copy launch per request and one synchronisation, with
-    no staging.  split_by_caller: each caller has copied its block to the start of its buffer
+    no staging (an encode group with CRC-16s: one launch over a table of the blocks' bases,
+    aligned for RS(4,2) 256 KiB, unaligned windows otherwise).  split_by_caller: each caller has
+    copied its block to the start of its buffer
     and passes the buffer as the block too (include/rsmi.h: block == shards_out), as the host
     mirror does, over stale bytes in the padding and parity.  Every shard, raw CRC-16 and
     rebuilt row equals the oracle's, and the calls did coalesce."""

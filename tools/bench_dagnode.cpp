@@ -99,8 +99,8 @@ int main(int argc, char** argv) {
     int rc;
     rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
     if (ctx) {
-        c0 = rsmi_get_stat(ctx, "coalesced_calls");
-        b0 = rsmi_get_stat(ctx, "coalesced_batches");
+        c0 = lane_stat(k, m, 0, "coalesced_calls");
+        b0 = lane_stat(k, m, 0, "coalesced_batches");
     }
     t0 = clk::now();
     {
@@ -112,8 +112,8 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
     }
     const double putT = secs(t0);
-    const long calls = ctx ? rsmi_get_stat(ctx, "coalesced_calls") - c0 : 0;
-    const long batches = ctx ? rsmi_get_stat(ctx, "coalesced_batches") - b0 : 0;
+    const long calls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - c0 : 0;
+    const long batches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - b0 : 0;
     // CRC + framing alone (the datanode's byte-serial CPU loop), for context
     t0 = clk::now();
     volatile uint16_t sink = 0;
@@ -146,7 +146,7 @@ int main(int argc, char** argv) {
         }
     }
     // degraded Get from 16 threads: the reconstructs coalesce (one erasure pattern)
-    const long gc0 = ctx ? rsmi_get_stat(ctx, "coalesced_calls") : 0, gb0 = ctx ? rsmi_get_stat(ctx, "coalesced_batches") : 0;
+    const long gc0 = ctx ? lane_stat(k, m, 0, "coalesced_calls") : 0, gb0 = ctx ? lane_stat(k, m, 0, "coalesced_batches") : 0;
     t0 = clk::now();
     {
         std::vector<std::thread> th;
@@ -158,8 +158,8 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
     }
     const double getT = secs(t0);
-    const long gcalls = ctx ? rsmi_get_stat(ctx, "coalesced_calls") - gc0 : 0;
-    const long gbatches = ctx ? rsmi_get_stat(ctx, "coalesced_batches") - gb0 : 0;
+    const long gcalls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - gc0 : 0;
+    const long gbatches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - gb0 : 0;
     // the same degraded reads with the checksums checked on the GPU instead of by each datanode
     d->SetGpuVerifiedReads(true);
     t0 = clk::now();

@@ -1,7 +1,8 @@
 // latency.cpp -- per-block call latency of the C-ABI (the Dag Node's per-key Put / Get seam,
 // erasure.go:51-93): rsmi_encode_block and a 1-lost-shard rsmi_reconstruct, from pageable
 // (std::vector, like Go slices over cgo) and page-locked (rsmi_host_alloc) buffers.
-// Diagnostic; prints microseconds per call (median of 200); block sizes
+// Diagnostic; prints microseconds per call (median of 200); --threads: coalesced groups from
+// concurrent callers (throughput); block sizes
 // may be given as arguments.  --sched-spin sets
 // hipDeviceScheduleSpin before the first HIP call (the runtime's polling wait), for comparison:
 // level with the default (profiles/r04/f), as was the engine polling its stream.
@@ -11,6 +12,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <tuple>
+#include <thread>
 #include <vector>
 
 #include <emmintrin.h>
@@ -53,7 +56,64 @@ static void copy_nt(uint8_t* dst, const uint8_t* src, size_t n) {
     _mm_sfence();
 }
 
+// T threads, each coding `calls` blocks of B bytes through rsmi_encode_block_coalesced_crcs, in
+// place in its own page-locked buffer (block == shards_out, Split by the thread): the coalesced
+// groups' throughput, GiB/s of block payload, and how many groups they formed
+static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1) {
+    // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes)
+    std::vector<rsmi_ctx*> cs(static_cast<size_t>(lanes));
+    for (auto& x : cs)
+        if (rsmi_open(k, m, 0, &x) != RSMI_OK) std::exit(2);
+    rsmi_ctx* c = cs[0];
+    const size_t n = size_t(k + m), S = rsmi_shard_size(B, k);
+    std::vector<uint8_t*> bufs(static_cast<size_t>(T));
+    std::vector<std::vector<uint8_t>> blocks(static_cast<size_t>(T), std::vector<uint8_t>(B));
+    for (int t = 0; t < T; t++) {
+        bufs[size_t(t)] = static_cast<uint8_t*>(rsmi_host_alloc(n * S));
+        for (size_t i = 0; i < B; i++) blocks[size_t(t)][i] = uint8_t(i * 31 + size_t(t));
+    }
+    auto run = [&] {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                std::vector<uint32_t> raw(n);
+                for (int i = 0; i < calls; i++) {
+                    std::memcpy(bufs[size_t(t)], blocks[size_t(t)].data(), B);
+                    if (rsmi_encode_block_coalesced_crcs(cs[size_t(t % lanes)], bufs[size_t(t)], B, bufs[size_t(t)],
+                                                         raw.data(), nullptr))
+                        std::exit(3);
+                }
+            });
+        for (auto& x : th) x.join();
+    };
+    run();  // warm: plans, staging, tables
+    auto stat = [&](const char* key) {
+        long v = 0;
+        for (auto* x : cs) v += rsmi_get_stat(x, key);
+        return v;
+    };
+    const long c0 = stat("coalesced_calls"), b0 = stat("coalesced_batches");
+    const auto a = std::chrono::steady_clock::now();
+    run();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    const long calls_n = stat("coalesced_calls") - c0, batches = stat("coalesced_batches") - b0;
+    std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s): %7.2f GiB/s, "
+                "%ld calls in %ld groups (last kernel %s)\n", k, m, B, T, calls, lanes,
+                double(T) * calls * B / sec / 1073741824.0, calls_n, batches, rsmi_last_kernel(c));
+    for (auto* p : bufs) rsmi_host_free(p);
+    for (auto* x : cs) rsmi_close(x);
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && !std::strcmp(argv[1], "--threads")) {
+        for (int lanes : {1, 2, 4})
+            for (int T : {4, 16})
+                for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
+                                   std::make_tuple(16, 4, size_t(4194304))})
+                    coalesced_threads(std::get<0>(shape), std::get<1>(shape), std::get<2>(shape), T,
+                                      std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, lanes);
+        return 0;
+    }
     const int k = 10, m = 4, n = k + m;
     std::vector<size_t> sizes;  // block sizes given on the command line, else the default list
     for (int i = 1; i < argc; i++) {
