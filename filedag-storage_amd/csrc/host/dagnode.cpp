@@ -664,10 +664,15 @@ Status DagNode::Get(const std::string& key, Bytes* block) {
         return st[0];
     }
     Active act(active_);
+    const auto t0 = PhaseClock::now();
     Fetched f;
     Status s = fetch_for_get(key, &f);
+    phase_add(Phase::Fetch, t0);
     if (!s.ok()) return s;
-    return finish_get(key, f, block);
+    const auto t1 = PhaseClock::now();
+    s = finish_get(key, f, block);  // the decode (survivors staged, codec call) and the block
+    phase_add(Phase::Codec, t1);
+    return s;
 }
 
 void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* blocks, std::vector<Status>* statuses,

@@ -102,6 +102,8 @@ int main(int argc, char** argv) {
         c0 = lane_stat(k, m, 0, "coalesced_calls");
         b0 = lane_stat(k, m, 0, "coalesced_batches");
     }
+    d->SetPhaseTiming(true);
+    d->ResetPhases();
     t0 = clk::now();
     {
         std::vector<std::thread> th;
@@ -112,6 +114,8 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
     }
     const double putT = secs(t0);
+    phase_json("put_threads", putT);
+    d->SetPhaseTiming(false);
     const long calls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - c0 : 0;
     const long batches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - b0 : 0;
     // CRC + framing alone (the datanode's byte-serial CPU loop), for context
@@ -126,10 +130,15 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; rep++)
         for (bool lone : {true, false}) {
             d->SetLoneCallerPaths(lone);
+            d->SetPhaseTiming(lone && rep == 0);
+            d->ResetPhases();
             t0 = clk::now();
             for (int i = 0; i < N; i++) d->Get(keys[i], &got);
-            (lone ? get1 : get1n) = std::min(lone ? get1 : get1n, secs(t0));
+            const double t = secs(t0);
+            if (lone && rep == 0) phase_json("get", t);
+            (lone ? get1 : get1n) = std::min(lone ? get1 : get1n, t);
         }
+    d->SetPhaseTiming(false);
     d->SetLoneCallerPaths(true);
     std::vector<Bytes> gm;
     std::vector<Status> st;
@@ -147,6 +156,8 @@ int main(int argc, char** argv) {
     }
     // degraded Get from 16 threads: the reconstructs coalesce (one erasure pattern)
     const long gc0 = ctx ? lane_stat(k, m, 0, "coalesced_calls") : 0, gb0 = ctx ? lane_stat(k, m, 0, "coalesced_batches") : 0;
+    d->SetPhaseTiming(true);
+    d->ResetPhases();
     t0 = clk::now();
     {
         std::vector<std::thread> th;
@@ -158,6 +169,8 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
     }
     const double getT = secs(t0);
+    phase_json("get_threads", getT);
+    d->SetPhaseTiming(false);
     const long gcalls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - gc0 : 0;
     const long gbatches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - gb0 : 0;
     // the same degraded reads with the checksums checked on the GPU instead of by each datanode
