@@ -414,8 +414,6 @@ __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uin
 // as the UA coding kernels do.
 // INL (small launches, a block of a few units): the block's last unit to finish combines its
 // records into R(row) itself, so the call needs no second launch (below).
-// blk_base (may be null): a table of block base addresses, for a coalesced group whose blocks
-// each lie in their own page-locked buffer (one launch for the group, rsmi_coalesce.cpp).
 template <int K, int MT, int NT, int WPS, bool UA = false, bool INL = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
                                                               const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
@@ -424,8 +422,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                                                               uint32_t upb, uint32_t nunits,
                                                               const uint32_t* __restrict__ crc_tbl,
                                                               uint8_t* __restrict__ crc_rec, uint32_t* __restrict__ ctr,
-                                                              uint32_t* __restrict__ raw, Crc16Shift sh,
-                                                              const uint64_t* __restrict__ blk_base) {
+                                                              uint32_t* __restrict__ raw, Crc16Shift sh) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     constexpr int NSH = K + MT;
     constexpr int NACC = (NSH + 1) / 2;  // two shards per accumulator
@@ -475,12 +472,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
     const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
 #ifndef RSMI_DIAG_CACHED
-    // blk_base (a coalesced group's blocks, each in its caller's own buffer): block b lies at
-    // blk_base[b], and in / out are the offsets of its input / output rows there
-    const uint8_t* ib = blk_base ? reinterpret_cast<const uint8_t*>(blk_base[blk] + reinterpret_cast<uintptr_t>(in))
-                                 : in + uint64_t(blk) * in_bs;
-    uint8_t* ob = blk_base ? reinterpret_cast<uint8_t*>(blk_base[blk] + reinterpret_cast<uintptr_t>(out))
-                           : out + uint64_t(blk) * out_bs;
+    const uint8_t* ib = in + uint64_t(blk) * in_bs;
+    uint8_t* ob = out + uint64_t(blk) * out_bs;
 #else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only, so
        // the launch time is the kernel's own issue time
     const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;

@@ -26,9 +26,8 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
 }
 
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
-// run_coalesced_group): an encode group with CRC-16s in one launch over a table of the blocks'
-// bases, otherwise one launch per request, and one synchronisation.  Encode: each block is Split into its own buffer first (the caller's
-// block is pageable), outside the context lock -- unless the caller Split it there itself
+// run_coalesced_group): one launch per request and one synchronisation.  Encode: each block is
+// Split into its own buffer first (the caller's block is pageable), outside the context lock -- unless the caller Split it there itself
 // (block == out), as the host mirror does, so the copies run on the callers' threads in
 // parallel instead of one after another on the executor's.
 int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S) {
@@ -61,37 +60,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         if (want16 && (rc = reserve(c->d_crc, c->crc_cap, nb * n * 4))) return rc;
         if (want32 && (rc = reserve(c->d_crc32, c->crc32_cap, nb * n * 4))) return rc;
         hipStream_t st = c->staging[0].stream;
-        // encode groups with the CRC-16: one launch for the whole group over a table of the
-        // blocks' bases (rs_fused_mfma_kernel blk_base), so the blocks are coded side by side
-        // instead of one small latency-bound kernel after another on the stream
-        bool tab_done = false;
-        if (enc && want16 && !want32 && nb > 1 && S >= 16 && k <= 16 && size_t(c->m) <= 4) {
-            if (c->h_tab_cap < nb) {
-                if (c->h_tab) (void)hipHostFree(c->h_tab);
-                c->h_tab = nullptr;
-                c->h_tab_cap = 0;
-                const size_t cap = std::max<size_t>(nb, 256);
-                HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&c->h_tab), cap * 8));
-                c->h_tab_cap = cap;
-            }
-            uintptr_t base_or = 0;
-            for (size_t j = 0; j < nb; j++) {
-                uint8_t* dev = host_alias(rq[j]->out, n * S);
-                if (!dev) return RSMI_ERR_DEVICE;
-                c->h_tab[j] = uint64_t(reinterpret_cast<uintptr_t>(dev));
-                base_or |= reinterpret_cast<uintptr_t>(dev);
-            }
-            const uint64_t* tab = reinterpret_cast<const uint64_t*>(host_alias(c->h_tab, nb * 8));
-            if (tab) {
-                rc = launch_plan_crc(c, *plan, nullptr, S, 0, reinterpret_cast<uint8_t*>(uintptr_t(k * S)), S, 0, S, nb,
-                                     reinterpret_cast<uint32_t*>(c->d_crc), st, tab, base_or);
-                if (rc == RSMI_OK)
-                    tab_done = true;
-                else if (rc != RSMI_ERR_INVALID_ARG)
-                    return rc;
-            }
-        }
-        for (size_t j = 0; j < nb && !tab_done; j++) {
+        for (size_t j = 0; j < nb; j++) {
             uint8_t* dev = host_alias(rq[j]->out, n * S);
             if (!dev) return RSMI_ERR_DEVICE;
             if (enc)

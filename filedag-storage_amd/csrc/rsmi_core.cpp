@@ -350,7 +350,6 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->h_coal) (void)hipHostFree(c->h_coal);
             if (c->h_small) (void)hipHostFree(c->h_small);
             if (c->h_raw) (void)hipHostFree(c->h_raw);
-            if (c->h_tab) (void)hipHostFree(c->h_tab);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
             if (c->d_chunks) (void)hipFree(c->d_chunks);

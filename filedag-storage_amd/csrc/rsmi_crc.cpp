@@ -148,22 +148,16 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
 // row j at r = K + j; device or page-locked host memory).  Needs K <= 16, one plan tile
 // (MT <= 4) and either an aligned layout or S >= 16; returns RSMI_ERR_INVALID_ARG otherwise
 // (callers then run the separate pass).
-//
-// blk_base (device-visible, may be null): block b lies at blk_base[b] and in / out are offsets
-// within it (in_bs / out_bs unused); base_or is the OR of every base address (its alignment).
-// Only the matrix-core fold takes a table; RSMI_ERR_INVALID_ARG otherwise.
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
-                    const uint64_t* blk_base, uintptr_t base_or) {
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
     if (plan.tiles.size() != 1 || plan.tiles[0].K > 16) return RSMI_ERR_INVALID_ARG;
     const DevTile& tile = plan.tiles[0];
     const size_t nsh = size_t(tile.K + tile.MT);
     const size_t cpb = (S + 15) / 16, tpb = (cpb + kWave - 1) / kWave;
     int rc;
     if ((rc = ensure_crc_tables(c))) return rc;
-    if (blk_base) in_bs = out_bs = 0;  // offsets from each block's base
     const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
-                         base_or % 16 == 0 && in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
+                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
                          in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (size_t(1) << 31);
     // unaligned-window layouts (the Split layout, page-locked host rows at pitch S): S >= 16
     const bool ua = !aligned && S >= 16 && S < (size_t(1) << 31) && in_rs >= S && out_rs >= S;
@@ -211,13 +205,8 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             uint8_t* rb = rec + b0 * rec_per_block;
             uint32_t* cb = inline_combine ? c->d_fctr + b0 : nullptr;
             uint32_t* rw = raw + b0 * nsh;
-            const uint64_t* bt = blk_base ? blk_base + b0 : nullptr;
-            if (blk_base) {
-                inb = in;
-                outb = out;
-            }
             void* args[] = {&pd,  &inb,   &outb,   &ibs, &irs, &obs, &ors, &S32, &cpb32,
-                            &tpb32, &upb32, &nunits, &tb,  &rb,  &cb,  &rw,  &sh, &bt};
+                            &tpb32, &upb32, &nunits, &tb,  &rb,  &cb,  &rw,  &sh};
             const uint32_t wgs = RSMI_FUSED_COOP ? nunits : (nunits + kWG / kWave - 1) / (kWG / kWave);
             HIP_TRY(hipLaunchKernel(fn, dim3(wgs), dim3(kWG), args, 0, st));
         }
@@ -236,13 +225,11 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         }
         char buf[96];
-        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s%s%s", tile.K, tile.MT,
-                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA", inline_combine ? ",INL" : "",
-                      blk_base ? ",TAB" : "");
+        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s%s", tile.K, tile.MT,
+                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA", inline_combine ? ",INL" : "");
         c->last_kernel = buf;
         return hip_status(hipGetLastError());
     }
-    if (blk_base) return RSMI_ERR_INVALID_ARG;
     const size_t ns2 = ((nsh + 3) / 4 + 1) / 2;
     const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * nsh * 4;
     if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;

@@ -131,8 +131,6 @@ struct rsmi_ctx {
     std::atomic<int> opt_inject_host_fault{0};  // test hook: the next coalesced batches throw std::bad_alloc
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;
-    uint64_t* h_tab = nullptr;  // page-locked block-base table of the executing group (in place)
-    size_t h_tab_cap = 0;
 };
 
 namespace rsmi {
@@ -195,8 +193,7 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                              size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
-                    const uint64_t* blk_base = nullptr, uintptr_t base_or = 0);
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
                        size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
