@@ -600,9 +600,11 @@ Status DagNode::decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
     // the survivors the decode reads (the first k present) are the only rows it needs
+    const bool stream = size_t(k) * S >= (size_t(1) << 20);  // as Erasure's staging of the survivors
     for (int i = 0, used = 0; i < n && used < k; i++)
         if (present[i]) {
-            copy_bytes(flat + size_t(i) * S, f.shards[i].data(), S);
+            if (stream && S < (size_t(1) << 20)) copy_streaming(flat + size_t(i) * S, f.shards[i].data(), S);
+            else copy_bytes(flat + size_t(i) * S, f.shards[i].data(), S);
             used++;
         }
     rc = rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), 1);

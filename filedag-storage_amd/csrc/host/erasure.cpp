@@ -248,9 +248,13 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
     // decode reads (upstream reconstruct(); missing and later rows: don't-care bytes)
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
+    // streaming stores once the k rows reach 1 MiB together (copy_to_staging's threshold is for
+    // the bytes the GPU then reads, not for one row)
+    const bool stream = size_t(data_blocks_) * S >= (size_t(1) << 20);
     for (int i = 0, used = 0; i < n && used < data_blocks_; i++)
         if (present[i]) {
-            copy_to_staging(flat + size_t(i) * S, shards[i].data(), S);
+            if (stream) copy_streaming(flat + size_t(i) * S, shards[i].data(), S);
+            else std::memcpy(flat + size_t(i) * S, shards[i].data(), S);
             used++;
         }
     // coalesced: concurrent degraded Gets usually miss the same node's shard, so they batch
