@@ -28,7 +28,8 @@ rsmi_ctx* shared_context(int k, int m, int device, int* rc);
 // kCallLanes contexts per (k, m, device), one per calling thread in turn; lane 0 is the shared
 // context.  A context runs one host call at a time (a launch and a wait), and the GPU has room
 // for several such latency-bound calls at once (tools/latency.cpp --threads, 16 threads of
-// RS(10,4) 256 KiB coalesced encodes: 8.3 GiB/s on one context, 18.7 on four).
+// RS(10,4) 256 KiB coalesced encodes: 8.3 GiB/s on one context, 15.4-18.7 on four, 18.0 on eight,
+// profiles/r04/r, y).
 constexpr int kCallLanes = 4;
 rsmi_ctx* call_context(int k, int m, int device, int* rc);
 // rsmi_get_stat summed over the lanes of (k, m, device) (the coalescing counters)
