@@ -2,6 +2,8 @@
 #include "erasure.hpp"
 
 #include <emmintrin.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <memory>
 
@@ -97,9 +99,46 @@ PinnedBuf& thread_staging() {
 // call (a 364 KB vector per Put or Get was a fresh value-initialised allocation each time), and
 // page-locked, so a lone coalesced call codes it in place on the GPU (rsmi_coalesce.cpp) instead
 // of through the engine's staging and a copy back
+namespace {
+// scratch of ended threads, by the NUMA node it was placed on (the allocating thread's), freed
+// at exit; a new thread takes one placed on its own node
+std::mutex g_scratch_mu;
+std::map<int, std::vector<std::unique_ptr<PinnedBuf>>> g_scratch_pool;
+int current_node() {
+    unsigned cpu = 0, node = 0;
+    return syscall(SYS_getcpu, &cpu, &node, nullptr) == 0 ? int(node) : 0;
+}
+struct ScratchHolder {
+    std::unique_ptr<PinnedBuf> buf;
+    int node = 0;
+    ~ScratchHolder() {
+        if (!buf) return;
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        try {
+            g_scratch_pool[node].push_back(std::move(buf));
+        } catch (...) {  // no room in the pool: the buffer is simply freed
+        }
+    }
+};
+}  // namespace
+
 uint8_t* block_scratch(size_t bytes) {
-    static thread_local PinnedBuf buf;
-    return buf.reserve(bytes);
+    static thread_local ScratchHolder h;
+    if (!h.buf) {
+        h.node = current_node();
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        auto& free = g_scratch_pool[h.node];
+        // the largest free one: it most likely already fits
+        auto best = free.end();
+        for (auto it = free.begin(); it != free.end(); ++it)
+            if (best == free.end() || (*it)->capacity() > (*best)->capacity()) best = it;
+        if (best != free.end()) {
+            h.buf = std::move(*best);
+            free.erase(best);
+        }
+    }
+    if (!h.buf) h.buf.reset(new (std::nothrow) PinnedBuf());
+    return h.buf ? h.buf->reserve(bytes) : nullptr;
 }
 
 namespace {

@@ -53,6 +53,7 @@ public:
     ~PinnedBuf() { release(); }
     uint8_t* reserve(size_t bytes);
     uint8_t* data() const { return p_; }
+    size_t capacity() const { return cap_; }
 
 private:
     void release();
@@ -66,7 +67,11 @@ private:
 constexpr size_t kStagingBytes = size_t(64) << 20;
 PinnedBuf& thread_staging();
 // The calling thread's page-locked scratch for one block's rows (single-block encodes and
-// reconstructs), separate from thread_staging; grown on demand, contents not cleared.
+// reconstructs), separate from thread_staging; grown on demand, contents not cleared.  A thread
+// that ends hands its scratch to a process-wide pool (by NUMA node), and a new thread takes one
+// placed on its own node, so short-lived callers do not page-lock fresh memory each
+// (page-locking holds the process's memory-map lock, which stalls every other thread's page
+// faults meanwhile).
 uint8_t* block_scratch(size_t bytes);
 // n bytes into page-locked staging on the calling thread; from 1 MiB with streaming stores, which
 // skip the destination's read-for-ownership and leave no dirty lines for the GPU's zero-copy
