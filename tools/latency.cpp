@@ -106,7 +106,7 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
 
 int main(int argc, char** argv) {
     if (argc > 1 && !std::strcmp(argv[1], "--threads")) {
-        for (int lanes : {1, 4, 8})
+        for (int lanes : {1, 4, 8, 16})
             for (int T : {4, 16})
                 for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
                                    std::make_tuple(16, 4, size_t(4194304))})
