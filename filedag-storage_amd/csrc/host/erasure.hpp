@@ -30,7 +30,10 @@ rsmi_ctx* shared_context(int k, int m, int device, int* rc);
 // for several such latency-bound calls at once (tools/latency.cpp --threads, 16 threads of
 // RS(10,4) 256 KiB coalesced encodes: 8.3 GiB/s on one context, 15.4-18.7 on four, 18.0 on eight,
 // profiles/r04/r, y).
-constexpr int kCallLanes = 4;
+#ifndef RSMI_HOST_CALL_LANES
+#define RSMI_HOST_CALL_LANES 4
+#endif
+constexpr int kCallLanes = RSMI_HOST_CALL_LANES;
 rsmi_ctx* call_context(int k, int m, int device, int* rc);
 // rsmi_get_stat summed over the lanes of (k, m, device) (the coalescing counters)
 long lane_stat(int k, int m, int device, const char* key);
