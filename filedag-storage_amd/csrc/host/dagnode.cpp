@@ -1035,12 +1035,31 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     // (block size, survivor pattern) -> pending keys
     std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
     DataNodeClient& target = *nodes_[to].client;
+    // The rebuilt rows of one flush go to the target on a helper thread while the next flush
+    // stages and codes into the other of two page-locked buffers (the GPU call leaves the cores
+    // free for the writes). A flush joins the previous flush's writes, in key order, before it
+    // starts its own, and every return joins them first, so the rows written, the count and the
+    // first error returned are those of the sequential loop.
+    std::future<std::vector<Status>> writing;
+    auto join_writes = [&]() -> Status {
+        if (!writing.valid()) return Status::Ok();
+        const std::vector<Status> ps = writing.get();
+        for (const Status& st : ps) {
+            if (!st.ok()) return st;
+            done++;
+        }
+        return Status::Ok();
+    };
+    int cur = 0;
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
         int rc;
         rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
-        if (!ctx) return rsmi_status(rc);
+        if (!ctx) {
+            const Status w = join_writes();
+            return w.ok() ? rsmi_status(rc) : w;
+        }
         const size_t S = rsmi_shard_size(size_t(size), k), nb = pend.size();
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
@@ -1048,8 +1067,20 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         // the fetch returns exactly the k survivors the plan reads (fetch_for_repair stops at
         // the read quorum k), and only those are staged; the rows being rebuilt are not
         const auto t0 = PhaseClock::now();
-        uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
-        if (!flat) return Status::Error("out of host memory");
+        // the two buffers are the halves of the thread's staging (kept warm by the batch calls);
+        // it only grows after the writes reading the other half are joined
+        PinnedBuf& st = thread_staging();
+        const size_t bytes = nb * size_t(n) * S;
+        if (st.capacity() < 2 * bytes) {
+            const Status w = join_writes();
+            if (!w.ok()) return w;
+        }
+        uint8_t* base = st.reserve(2 * bytes);
+        if (!base) {
+            const Status w = join_writes();
+            return w.ok() ? Status::Error("out of host memory") : w;
+        }
+        uint8_t* flat = base + (cur ? st.capacity() / 2 : 0);
         fan_keys(int(nb), [&](int j) {
             for (int i = 0; i < n; i++)
                 if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, pend[j].shards[i].data(), S);
@@ -1065,29 +1096,33 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                             : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(),
                                                                required.data());
         phase_add(Phase::Codec, t1);
+        const Status w = join_writes();
+        if (!w.ok()) return w;
         if (rc) return rsmi_status(rc);
-        const Bytes meta = encode_meta(size);
         // the rebuilt rows go to the target concurrently, each as a view of the staging buffer;
-        // outcomes are taken in key order
-        const auto t2 = PhaseClock::now();
-        std::vector<Status> ps(nb);
-        fan_keys(int(nb), [&](int j) {
-            const ByteView shard(flat + (size_t(j) * n + size_t(to)) * S, S);
-            if (!gpu_checksums_) {
-                ps[j] = target.Put(pend[j].key, meta, shard);
-                return;
-            }
-            const uint16_t c16 = entry_checksum(meta, S, r16[size_t(j) * n + size_t(to)]);
-            ps[j] = want32 ? target.PutWithChecksums(pend[j].key, meta, shard, c16,
-                                                     value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
-                           : target.PutWithChecksum(pend[j].key, meta, shard, c16);
-        });
-        phase_add(Phase::Put, t2);
-        for (size_t j = 0; j < nb; j++) {
-            if (!ps[j].ok()) return ps[j];
-            done++;
-        }
+        // outcomes are taken in key order by the next join
+        std::vector<std::string> wkeys(nb);
+        for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[j].key);
         pend.clear();
+        writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size),
+                                                  wkeys = std::move(wkeys), r16 = std::move(r16), r32 = std::move(r32)] {
+            const auto t2 = PhaseClock::now();
+            std::vector<Status> ps(wkeys.size());
+            fan_keys(int(wkeys.size()), [&](int j) {
+                const ByteView shard(flat + (size_t(j) * n + size_t(to)) * S, S);
+                if (!gpu_checksums_) {
+                    ps[j] = target.Put(wkeys[j], meta, shard);
+                    return;
+                }
+                const uint16_t c16 = entry_checksum(meta, S, r16[size_t(j) * n + size_t(to)]);
+                ps[j] = want32 ? target.PutWithChecksums(wkeys[j], meta, shard, c16,
+                                                         value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
+                               : target.PutWithChecksum(wkeys[j], meta, shard, c16);
+            });
+            phase_add(Phase::Put, t2);
+            return ps;
+        });
+        cur ^= 1;
         return Status::Ok();
     };
     // Each key's checks and fetch (the target's GetMeta, the meta quorum, the k-of-n fetch) run
@@ -1117,13 +1152,14 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         phase_add(Phase::Fetch, t0);
         return fr;
     };
-    // windows as large as one flush (staging-bounded by the shard size seen last), at most batch
+    // windows as large as one flush (half the staging, for the double buffer, by the shard size
+    // seen last), at most batch
     size_t window = std::min<size_t>(batch, 16);
     auto next_window = [&](const std::vector<Fetch>& fr) {
         for (auto& f : fr)
             if (f.use && f.size > 0)
                 window = std::max<size_t>(
-                    1, std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(f.size), k))));
+                    1, std::min(batch, staging_blocks(2 * size_t(n) * rsmi_shard_size(size_t(f.size), k))));
     };
     std::future<std::vector<Fetch>> ahead;
     size_t c0 = 0, nk = std::min(window, keys.size());
@@ -1138,6 +1174,8 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
             const int size = fr[q].size;
             std::vector<Bytes>& shards = fr[q].shards;
             if (size <= 0) {  // empty block: the per-key path's error behaviour (ErrShardNoData)
+                s = join_writes();
+                if (!s.ok()) return s;
                 Erasure enc;
                 s = Erasure::New(k, m, size, &enc, device_);
                 if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
@@ -1149,7 +1187,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
             auto gk = std::make_pair(size, pat);
             auto& pend = groups[gk];
             pend.push_back(Pending{key, std::move(shards)});
-            if (pend.size() >= std::min(batch, staging_blocks(size_t(n) * rsmi_shard_size(size_t(size), k)))) {
+            if (pend.size() >= std::min(batch, staging_blocks(2 * size_t(n) * rsmi_shard_size(size_t(size), k)))) {
                 s = flush(gk, pend);
                 if (!s.ok()) return s;
             }
@@ -1162,6 +1200,8 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         s = flush(g.first, g.second);
         if (!s.ok()) return s;
     }
+    s = join_writes();
+    if (!s.ok()) return s;
     if (repaired) *repaired = done;
     return Status::Ok();
 }
