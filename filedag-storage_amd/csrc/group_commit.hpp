@@ -2,14 +2,16 @@
 // (rsmi_coalesce.cpp; plain C++, so tests/cpp runs it under ThreadSanitizer without a device).
 //
 // DagNode.Put hands the engine one block per call (node.go:358-408) from many goroutines at
-// once.  A caller that finds no batch executing becomes the executor: it takes every request
-// queued so far (optionally waiting up to wait_us for the queue to reach cap), runs them as one
-// batch through exec(batch) with the lock released, marks them done and wakes the others.
-// Requests that arrive while a batch runs form the next batch.  A lone caller never waits: its
-// batch is itself.  Req needs a `bool done` member, false on submission, and an `int rc`.  If
-// exec throws (std::bad_alloc from its own vectors), every request of the batch completes with
-// rc = the fail code given at construction and the executor role is released, so no current or
-// later caller waits forever; the exception does not cross the C-ABI.
+// once.  A caller whose request is still queued and that finds a free lane becomes that lane's
+// executor: it takes every request queued so far (optionally waiting up to wait_us for the queue
+// to reach cap), runs them as one batch through exec(batch, lane) with the lock released, marks
+// them done and wakes the others.  Up to `lanes` batches execute at once, each on its own lane
+// (0 .. lanes-1, distinct among the batches executing), so one batch can be launched while the
+// one before it is still coded; requests that arrive while every lane is busy form the next
+// batch.  A lone caller never waits: its batch is itself.  Req needs a `bool done` member, false
+// on submission, and an `int rc`.  If exec throws (std::bad_alloc from its own vectors), every
+// request of the batch completes with rc = the fail code given at construction and the lane is
+// released, so no current or later caller waits forever; the exception does not cross the C-ABI.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -24,20 +26,28 @@ namespace rsmi {
 template <class Req>
 class GroupCommit {
 public:
+    static constexpr int kMaxLanes = 32;
     explicit GroupCommit(int fail_rc) : fail_rc_(fail_rc) {}
     template <class Exec>
-    void submit(Req& req, size_t cap, long wait_us, Exec&& exec) {
+    void submit(Req& req, size_t cap, long wait_us, int lanes, Exec&& exec) {
         calls_++;
+        lanes = std::min(std::max(lanes, 1), kMaxLanes);
+        cap = std::max<size_t>(cap, 1);
         std::unique_lock<std::mutex> lk(mu_);
         pending_.push_back(&req);
         cv_.notify_all();  // an executor waiting out wait_us may now have enough
         while (!req.done) {
-            if (executing_) {
+            // only a caller whose own request is still queued executes: it is then certain to
+            // find work, and a caller whose request is already in a batch just waits for it
+            const bool queued = std::find(pending_.begin(), pending_.end(), &req) != pending_.end();
+            if (!queued || executing_ >= lanes) {
                 cv_.wait(lk);
                 continue;
             }
-            executing_ = true;
-            cap = std::max<size_t>(cap, 1);
+            int lane = 0;
+            while (busy_ & (uint64_t(1) << lane)) lane++;
+            busy_ |= uint64_t(1) << lane;
+            executing_++;
             if (wait_us > 0 && pending_.size() < cap)
                 cv_.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return pending_.size() >= cap; });
             const size_t take = std::min(cap, pending_.size());
@@ -50,32 +60,36 @@ public:
                     pending_[i]->done = true;
                 }
                 pending_.erase(pending_.begin(), pending_.begin() + take);
-                executing_ = false;
-                cv_.notify_all();
+                release(lane);
                 continue;
             }
             pending_.erase(pending_.begin(), pending_.begin() + take);
             lk.unlock();
             try {
-                exec(batch);
+                exec(batch, lane);
             } catch (...) {
                 for (Req* r : batch) r->rc = fail_rc_;
             }
             batches_++;
             lk.lock();
             for (Req* r : batch) r->done = true;
-            executing_ = false;
-            cv_.notify_all();
+            release(lane);
         }
     }
     uint64_t calls() const { return calls_.load(); }
     uint64_t batches() const { return batches_.load(); }
 
 private:
+    void release(int lane) {  // caller holds mu_
+        busy_ &= ~(uint64_t(1) << lane);
+        executing_--;
+        cv_.notify_all();
+    }
     std::mutex mu_;
     std::condition_variable cv_;
     std::vector<Req*> pending_;
-    bool executing_ = false;
+    int executing_ = 0;
+    uint64_t busy_ = 0;  // lanes with a batch executing
     const int fail_rc_;
     std::atomic<uint64_t> calls_{0}, batches_{0};
 };

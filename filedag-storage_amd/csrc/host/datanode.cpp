@@ -106,15 +106,20 @@ Status DataNodeServer::store(const std::string& key, const Bytes& meta, ByteView
     const size_t len = pre + size_t(kHeaderSize) + meta.size() + data.size();
     // the entry is framed straight into the value the KV keeps (a recycled buffer when one is
     // large enough; every byte is written below), outside the lock, with no second copy
+    // The smallest spare that fits, and none more than twice the entry's size: a few large
+    // displaced values are not handed to small entries, where they would stay allocated for as
+    // long as the key lives
     Value nv;
     {
         std::lock_guard<std::mutex> g(mu_);
-        for (size_t i = spare_.size(); i-- > 0;)
-            if (spare_[i].cap >= len) {
-                nv = std::move(spare_[i]);
-                spare_.erase(spare_.begin() + long(i));
-                break;
-            }
+        size_t best = spare_.size();
+        for (size_t i = 0; i < spare_.size(); i++)
+            if (spare_[i].cap >= len && spare_[i].cap <= 2 * len && (best == spare_.size() || spare_[i].cap < spare_[best].cap))
+                best = i;
+        if (best < spare_.size()) {
+            nv = std::move(spare_[best]);
+            spare_.erase(spare_.begin() + long(best));
+        }
     }
     if (!nv.p) {
         nv.p.reset(new uint8_t[len]);
@@ -130,7 +135,18 @@ Status DataNodeServer::store(const std::string& key, const Bytes& meta, ByteView
     if (pre) put_le32(nv.p.get(), value_crc ? *value_crc : crc32_ieee(e, len - pre));
     std::lock_guard<std::mutex> g(mu_);
     std::swap(kv_[key], nv);
-    if (nv.p && spare_.size() < kSpareValues) spare_.push_back(std::move(nv));
+    // a displaced value is kept for reuse while the pool has room; when it is full, the new one
+    // replaces the largest spare if it is smaller (the pool drifts towards the sizes in use)
+    if (nv.p) {
+        if (spare_.size() < kSpareValues) {
+            spare_.push_back(std::move(nv));
+        } else {
+            size_t big = 0;
+            for (size_t i = 1; i < spare_.size(); i++)
+                if (spare_[i].cap > spare_[big].cap) big = i;
+            if (spare_[big].cap > nv.cap) spare_[big] = std::move(nv);
+        }
+    }
     return Status::Ok();
 }
 

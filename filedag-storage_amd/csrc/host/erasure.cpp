@@ -175,14 +175,10 @@ rsmi_ctx* call_context(int k, int m, int device, int* rc) {
 }
 
 void warm_contexts(int k, int m, int device) {
-    const size_t B = size_t(64) * size_t(k);  // S = 64: the fused encode + CRC-16 path
-    const size_t S = rsmi_shard_size(B, k);
-    std::vector<uint8_t> block(B, 1), out(size_t(k + m) * S);
-    std::vector<uint32_t> raw(size_t(k + m));
     for (int lane = 0; lane < kCallLanes; lane++) {
         int rc;
         rsmi_ctx* c = lane_context(k, m, device, lane, &rc);
-        if (c) (void)rsmi_encode_block_coalesced_crcs(c, block.data(), B, out.data(), raw.data(), nullptr);
+        if (c) (void)rsmi_warm(c);  // the context and each of its coalescing lanes
     }
 }
 

@@ -24,14 +24,15 @@ int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
 // Process-wide context per (k, m, device): NewErasure runs per block in the reference
 // (node.go:277,376) but the matrix / device plans are built once.
 rsmi_ctx* shared_context(int k, int m, int device, int* rc);
-// Per-block calls from concurrent threads (Erasure's encodes and reconstructs) spread over
-// kCallLanes contexts per (k, m, device), one per calling thread in turn; lane 0 is the shared
-// context.  A context runs one host call at a time (a launch and a wait), and the GPU has room
-// for several such latency-bound calls at once (tools/latency.cpp --threads, 16 threads of
-// RS(10,4) 256 KiB coalesced encodes: 8.3 GiB/s on one context, 15.4-18.7 on four, 18.0 on eight,
-// profiles/r04/r, y).
+// Per-block calls from concurrent threads (Erasure's encodes and reconstructs) go to kCallLanes
+// contexts per (k, m, device), one per calling thread in turn; lane 0 is the shared context.  One
+// (the default) keeps every caller in one group-commit queue, whose batches the context codes on
+// its own coalescing lanes (option "coalesce_lanes", include/rsmi.h), so concurrent Puts become
+// a few launches over tables of blocks instead of a launch per block (round 4 spread the callers
+// over 4 contexts instead, each queue then holding ~1 block per batch: 2,048 calls in 1,744-2,048
+// groups, profiles/r04/af).
 #ifndef RSMI_HOST_CALL_LANES
-#define RSMI_HOST_CALL_LANES 4
+#define RSMI_HOST_CALL_LANES 1
 #endif
 constexpr int kCallLanes = RSMI_HOST_CALL_LANES;
 rsmi_ctx* call_context(int k, int m, int device, int* rc);

@@ -64,6 +64,16 @@ struct LdsTable {
     }
 };
 
+// Block blk's rows: at p + blk * bs, or, over a table of block bases (TB, BlockBases), at the
+// table's entry for blk plus the offset p (one scalar load from the kernel arguments per wave).
+template <bool TB, class T>
+__device__ __forceinline__ T* block_rows(const BasesArg<TB>& bases, T* p, uint32_t blk, uint64_t bs) {
+    if constexpr (TB)
+        return reinterpret_cast<T*>(uintptr_t(bases.b[blk]) + reinterpret_cast<uintptr_t>(p));
+    else
+        return p + uint64_t(blk) * bs;
+}
+
 // K inputs, MT (<= 4) outputs, one 16-byte chunk per lane per row.
 // NT: cache policy, 1 = nontemporal loads and stores (write-heavy tiles), 2 = nontemporal
 // loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.
@@ -86,13 +96,16 @@ struct LdsTable {
 // R(row).
 // Launch geometry: one tile per wave; the loop strides over further tiles only
 // when the caller caps the grid (option waves_per_cu).
-template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false>
+// TB: the blocks lie where a table of block bases says (BlockBases: a coalesced group of callers'
+// own page-locked buffers, one launch for the group); in / out are offsets from each base.
+template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false, bool TB = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
                                                        uint32_t ntiles, const uint32_t* __restrict__ crc_tbl,
-                                                       uint32_t* __restrict__ crc_rec, uint32_t* __restrict__ crc_tail) {
+                                                       uint32_t* __restrict__ crc_rec, uint32_t* __restrict__ crc_tail,
+                                                       BasesArg<TB> bases) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     constexpr int NSH = K + MT;            // CRC: shards of the block (encode plans)
     constexpr int NSL = (NSH + 3) / 4;     // CRC: rows each lane keeps (r = q mod 4)
@@ -136,8 +149,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 
     for (; t < ntiles; t += nw) {
 #ifndef RSMI_DIAG_CACHED
-        const uint8_t* ib = in + uint64_t(blk) * in_bs;
-        uint8_t* ob = out + uint64_t(blk) * out_bs;
+        const uint8_t* ib = block_rows<TB>(bases, in, blk, in_bs);
+        uint8_t* ob = block_rows<TB>(bases, out, blk, out_bs);
 #else  // diagnostic build (tools/Makefile diag-cached): tiles wrap onto the first 16
        // blocks (~7 MB, cache-resident), so the kernel's own issue rate (VALU, LDS, waits)
        // is what the launch time shows
@@ -375,10 +388,56 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 typedef int mfma_v8i __attribute__((ext_vector_type(8)));
 typedef float mfma_v4f __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t crc_pow4(const uint16_t* sQ, int i, uint32_t s);
+// A^(2^i)(s) through the nibble-sliced tables P4[i][4][16]
+__device__ __forceinline__ uint32_t crc_pow4(const uint16_t* sQ, int i, uint32_t s) {
+    const uint16_t* t = sQ + i * 64;
+    return xor3(uint32_t(t[s & 15]), uint32_t(t[16 + ((s >> 4) & 15)]), uint32_t(t[32 + ((s >> 8) & 15)])) ^
+           uint32_t(t[48 + ((s >> 12) & 15)]);
+}
+
+// R(row) of rows 4 p + g (lane l = 16 g + m: class m) of one block from its unit records
+// (rs_fused_mfma_kernel): for each unit h a lane gathers its class's 16-bit value from the
+// class's four record bytes (one dword load; the loads of 8 units are issued before their power
+// steps) and steps its running value by one unit (A^4096 for 4-tile units) before adding it; a
+// 4-level scan over the 16 classes (A^(16 * 2^j)) then leaves the row's value relative to the end
+// of the last unit in lane 15 of the group, and A^e, e = (S - that end) mod 32767 (column form),
+// moves it to the row's end.  out[r] is written once (host memory allowed).
 __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uint8_t* rec, uint32_t upb, uint32_t nacc,
                                                    uint32_t nsh, const Crc16Shift& sh, uint32_t* out, uint32_t p,
-                                                   uint32_t lane);
+                                                   uint32_t lane) {
+    const uint32_t m = lane & 15u, g = lane >> 4;
+    const uint32_t r = g + 4u * p, rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row, store nothing
+    const uint32_t sp = 4u * (rr & 1u);
+    // the class's four bytes (j = 0..3) of accumulator rr / 2 in unit h
+    const uint8_t* rb = rec + (rr >> 1) * kWave + m * 4u;
+    uint32_t acc = 0;
+    for (uint32_t h0 = 0; h0 < upb; h0 += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int hh = 0; hh < 8; hh++) {
+            const uint32_t h = h0 + hh < upb ? h0 + hh : upb - 1;
+            x[hh] = *reinterpret_cast<const uint32_t*>(rb + uint64_t(h) * nacc * kWave);
+        }
+#pragma unroll
+        for (int hh = 0; hh < 8; hh++) {
+            if (h0 + hh >= upb) break;
+            const uint32_t y = x[hh] >> sp;
+            const uint32_t v = (y & 15u) | ((y >> 4) & 0xF0u) | ((y >> 8) & 0xF00u) | ((y >> 12) & 0xF000u);
+            acc = crc_pow4(sQ, 10 + kFusedUnitLog, acc) ^ v;  // earlier units move one unit further
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
+        const uint32_t t = __shfl_up(w, 1u << j);
+        if (m >= (1u << j)) acc ^= t;
+    }
+    uint32_t y = 0;  // A^e(acc), column form
+#pragma unroll
+    for (int bit = 0; bit < 16; bit++) y ^= ((acc >> bit) & 1u) ? sh.col[bit] : 0u;
+    if (m == 15 && r < nsh) out[r] = y;
+}
+
 
 // ------------------------------------------------------------------ fused encode + CRC-16, matrix-core fold
 // DagNode.Put's device form (node.go:358-408 with server.go:57-80's checksum of every shard):
@@ -414,7 +473,9 @@ __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uin
 // as the UA coding kernels do.
 // INL (small launches, a block of a few units): the block's last unit to finish combines its
 // records into R(row) itself, so the call needs no second launch (below).
-template <int K, int MT, int NT, int WPS, bool UA = false, bool INL = false>
+// TB: over a table of block bases, as rs_fast_kernel TB (a coalesced group of DagNode.Put
+// callers' own page-locked buffers in one launch).
+template <int K, int MT, int NT, int WPS, bool UA = false, bool INL = false, bool TB = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev* __restrict__ plan,
                                                               const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                               uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
@@ -422,7 +483,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
                                                               uint32_t upb, uint32_t nunits,
                                                               const uint32_t* __restrict__ crc_tbl,
                                                               uint8_t* __restrict__ crc_rec, uint32_t* __restrict__ ctr,
-                                                              uint32_t* __restrict__ raw, Crc16Shift sh) {
+                                                              uint32_t* __restrict__ raw, Crc16Shift sh,
+                                                              BasesArg<TB> bases) {
     static_assert(NT == 1 || NT == 2, "cache policy 1 or 2");
     constexpr int NSH = K + MT;
     constexpr int NACC = (NSH + 1) / 2;  // two shards per accumulator
@@ -472,8 +534,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint32_t t0 = (u - blk * upb) * kFusedUnitTiles;
     const uint32_t nt = tpb - t0 < uint32_t(kFusedUnitTiles) ? tpb - t0 : uint32_t(kFusedUnitTiles);
 #ifndef RSMI_DIAG_CACHED
-    const uint8_t* ib = in + uint64_t(blk) * in_bs;
-    uint8_t* ob = out + uint64_t(blk) * out_bs;
+    const uint8_t* ib = block_rows<TB>(bases, in, blk, in_bs);
+    uint8_t* ob = block_rows<TB>(bases, out, blk, out_bs);
 #else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only, so
        // the launch time is the kernel's own issue time
     const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
@@ -819,6 +881,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 }
 
 
+#ifndef RSMI_TB_UNIT  // rs_kernels_tb.hip: the coding kernels above only
 // Any K (<= 256), MT <= 4, any alignment: one byte-group of 4 per lane, bytewise memory
 // access.  Correctness path for layouts the fast kernel does not accept.
 __global__ __launch_bounds__(kWG) void rs_generic_kernel(const RsPlanDev* __restrict__ plan, const uint8_t* in,
@@ -916,13 +979,6 @@ void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 // final shift accounts for).
 __device__ __forceinline__ uint32_t crc_pow(const uint16_t* sP, int i, uint32_t s) {
     return uint32_t(sP[i * 512 + (s & 0xFF)]) ^ uint32_t(sP[i * 512 + 256 + (s >> 8)]);
-}
-
-// A^(2^i)(s) through the nibble-sliced tables P4[i][4][16]
-__device__ __forceinline__ uint32_t crc_pow4(const uint16_t* sQ, int i, uint32_t s) {
-    const uint16_t* t = sQ + i * 64;
-    return xor3(uint32_t(t[s & 15]), uint32_t(t[16 + ((s >> 4) & 15)]), uint32_t(t[32 + ((s >> 8) & 15)])) ^
-           uint32_t(t[48 + ((s >> 12) & 15)]);
 }
 
 __device__ __forceinline__ uint32_t crc_nib_chunk(const uint8_t* nb, const u32x4& v) {
@@ -1278,49 +1334,6 @@ void* crc16_rows_mfma_kernel(bool aligned) {
                    : reinterpret_cast<void*>(&rs_crc16_rows_mfma_kernel<true>);
 }
 
-// R(row) of rows 4 p + g (lane l = 16 g + m: class m) of one block from its unit records
-// (rs_fused_mfma_kernel): for each unit h a lane gathers its class's 16-bit value from the
-// class's four record bytes (one dword load; the loads of 8 units are issued before their power
-// steps) and steps its running value by one unit (A^4096 for 4-tile units) before adding it; a
-// 4-level scan over the 16 classes (A^(16 * 2^j)) then leaves the row's value relative to the end
-// of the last unit in lane 15 of the group, and A^e, e = (S - that end) mod 32767 (column form),
-// moves it to the row's end.  out[r] is written once (host memory allowed).
-__device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uint8_t* rec, uint32_t upb, uint32_t nacc,
-                                                   uint32_t nsh, const Crc16Shift& sh, uint32_t* out, uint32_t p,
-                                                   uint32_t lane) {
-    const uint32_t m = lane & 15u, g = lane >> 4;
-    const uint32_t r = g + 4u * p, rr = r < nsh ? r : nsh - 1;  // idle lanes repeat a row, store nothing
-    const uint32_t sp = 4u * (rr & 1u);
-    // the class's four bytes (j = 0..3) of accumulator rr / 2 in unit h
-    const uint8_t* rb = rec + (rr >> 1) * kWave + m * 4u;
-    uint32_t acc = 0;
-    for (uint32_t h0 = 0; h0 < upb; h0 += 8) {
-        uint32_t x[8];
-#pragma unroll
-        for (int hh = 0; hh < 8; hh++) {
-            const uint32_t h = h0 + hh < upb ? h0 + hh : upb - 1;
-            x[hh] = *reinterpret_cast<const uint32_t*>(rb + uint64_t(h) * nacc * kWave);
-        }
-#pragma unroll
-        for (int hh = 0; hh < 8; hh++) {
-            if (h0 + hh >= upb) break;
-            const uint32_t y = x[hh] >> sp;
-            const uint32_t v = (y & 15u) | ((y >> 4) & 0xF0u) | ((y >> 8) & 0xF00u) | ((y >> 12) & 0xF000u);
-            acc = crc_pow4(sQ, 10 + kFusedUnitLog, acc) ^ v;  // earlier units move one unit further
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t w = crc_pow4(sQ, 4 + j, acc);  // 16 * 2^j bytes
-        const uint32_t t = __shfl_up(w, 1u << j);
-        if (m >= (1u << j)) acc ^= t;
-    }
-    uint32_t y = 0;  // A^e(acc), column form
-#pragma unroll
-    for (int bit = 0; bit < 16; bit++) y ^= ((acc >> bit) & 1u) ? sh.col[bit] : 0u;
-    if (m == 15 && r < nsh) out[r] = y;
-}
-
 // R(row) from rs_fused_mfma_kernel's unit records: a persistent grid whose waves take items
 // (block b, row group p) in turn, lane l = 16 g + m class m of row 4 p + g (the workgroup stages
 // the power tables once).  For each unit h
@@ -1444,10 +1457,49 @@ void* crc16_rows_kernel(bool aligned) {
                    : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false>);
 }
 
+#endif  // RSMI_TB_UNIT
+
 // ------------------------------------------------------------------ dispatch table
 // One kernel per (K, MT) and layout, with the cache policy of the shape (auto_cache_policy in
 // rsmi_core.cpp): nontemporal stores unless the tile reads at least 4 rows per row it writes.
 constexpr int auto_nt(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
+
+#ifdef RSMI_TB_UNIT
+// the table-of-bases forms (rs_kernels_tb.hip, its own translation unit so the build compiles it
+// beside this one): for the BASELINE shapes' encodes (K = k, MT = m) and their reconstructs of up
+// to 4 rows; other shapes code a coalesced group with one launch per block
+template <int K, int MT>
+static void fill_tb_km(FastKernelTable& t) {
+    constexpr int NT = auto_nt(K, MT);
+    t.fn_tb[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, false, true>);
+    t.ua_tb[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, false, true>);
+}
+template <int K, int MT>
+static void fill_tb_fused(FastKernelTable& t) {
+    constexpr int NT = auto_nt(K, MT);
+    t.fused_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, false, false, true>);
+    t.fused_ua_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true, false, true>);
+    t.fused_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, false, true, true>);
+    t.fused_ua_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true, true, true>);
+}
+template <int K>
+static void fill_tb_k(FastKernelTable& t) {
+    fill_tb_km<K, 1>(t);
+    fill_tb_km<K, 2>(t);
+    fill_tb_km<K, 3>(t);
+    fill_tb_km<K, 4>(t);
+}
+void fill_table_kernels(FastKernelTable& t) {
+    fill_tb_k<2>(t);
+    fill_tb_k<4>(t);
+    fill_tb_k<10>(t);
+    fill_tb_k<16>(t);
+    fill_tb_fused<2, 1>(t);
+    fill_tb_fused<4, 2>(t);
+    fill_tb_fused<10, 4>(t);
+    fill_tb_fused<16, 4>(t);
+}
+#else
 
 template <int K, int MT>
 static void fill_km(FastKernelTable& t) {
@@ -1494,11 +1546,13 @@ const FastKernelTable& fast_kernels() {
         fill_inl<4, 2>(x);
         fill_inl<10, 4>(x);
         fill_inl<16, 4>(x);
+        fill_table_kernels(x);
         return x;
     }();
     return t;
 }
 
 void* generic_kernel() { return reinterpret_cast<void*>(&rs_generic_kernel); }
+#endif  // RSMI_TB_UNIT
 
 }  // namespace rsmi

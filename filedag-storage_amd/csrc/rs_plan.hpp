@@ -1,6 +1,7 @@
 // rs_plan.hpp -- device-side coding plan shared by the host launcher and the kernels.
 #pragma once
 #include <cstdint>
+#include <type_traits>
 
 namespace rsmi {
 
@@ -26,6 +27,20 @@ struct RsPlanDev {
     uint32_t tbl[kMaxK * kColDwords];
 };
 
+// A coalesced group of blocks that each lie in their own caller's page-locked buffer (concurrent
+// DagNode.Put / Get callers, rsmi_coalesce.cpp), coded by one launch: block b's rows start at
+// b[b], and the launch's in / out pointers are offsets from there.  Passed by value, so the
+// table travels in the kernel arguments (one scalar load per wave, no copy to the device); a
+// group of more blocks takes several launches.  The kernels' table-less instantiations take
+// NoBases in its place, an unused empty argument that leaves their code unchanged.
+constexpr int kTableBlocks = 64;
+struct BlockBases {
+    uint64_t b[kTableBlocks];
+};
+struct NoBases {};
+template <bool TB>
+using BasesArg = std::conditional_t<TB, BlockBases, NoBases>;
+
 // Instantiated fast kernels, one per (K, MT) with the shape's cache policy (null when K has no
 // instantiation): aligned layouts, unaligned-window layouts, and both with the datanode CRC-16
 // of every row fused in (encode plans).
@@ -38,7 +53,16 @@ struct FastKernelTable {
     void* fused_ua[17][kMaxMT + 1];  // the same on unaligned-window layouts (S >= 16)
     void* fused_inl[17][kMaxMT + 1];     // fused with the combine in the kernel (small launches;
     void* fused_ua_inl[17][kMaxMT + 1];  // null: the two-launch form)
+    // the same over a table of block bases (BlockBases; rs_kernels_tb.hip, for the shapes of the
+    // BASELINE configs; null: one launch per block)
+    void* fn_tb[17][kMaxMT + 1];
+    void* ua_tb[17][kMaxMT + 1];
+    void* fused_tb[17][kMaxMT + 1];
+    void* fused_ua_tb[17][kMaxMT + 1];
+    void* fused_inl_tb[17][kMaxMT + 1];
+    void* fused_ua_inl_tb[17][kMaxMT + 1];
 };
+void fill_table_kernels(FastKernelTable& t);  // rs_kernels_tb.hip
 
 const FastKernelTable& fast_kernels();
 void* generic_kernel();

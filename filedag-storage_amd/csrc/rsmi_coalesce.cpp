@@ -26,8 +26,10 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
 }
 
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
-// run_coalesced_group): one launch per request and one synchronisation.  Encode: each block is
-// Split into its own buffer first (the caller's block is pageable), outside the context lock -- unless the caller Split it there itself
+// run_coalesced_group): one launch over a table of the blocks' bases for up to kTableBlocks
+// requests (BlockBases, the table kernels of the BASELINE shapes), else one launch per request,
+// and one synchronisation.  Encode: each block is Split into its own buffer first (the caller's
+// block is pageable), outside the context lock -- unless the caller Split it there itself
 // (block == out), as the host mirror does, so the copies run on the callers' threads in
 // parallel instead of one after another on the executor's.
 int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S) {
@@ -51,6 +53,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         }
     }
     std::vector<uint32_t> r16(want16 ? nb * n : 0), r32(want32 ? nb * n : 0);
+    std::vector<uint8_t*> dev(nb);
     {
         std::lock_guard<std::mutex> g(c->mu);
         HIP_TRY(hipSetDevice(c->device));
@@ -59,23 +62,51 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         if (rc) return rc;
         if (want16 && (rc = reserve(c->d_crc, c->crc_cap, nb * n * 4))) return rc;
         if (want32 && (rc = reserve(c->d_crc32, c->crc32_cap, nb * n * 4))) return rc;
+        for (size_t j = 0; j < nb; j++)
+            if (!(dev[j] = host_alias(rq[j]->out, n * S))) return RSMI_ERR_DEVICE;
         hipStream_t st = c->staging[0].stream;
-        for (size_t j = 0; j < nb; j++) {
-            uint8_t* dev = host_alias(rq[j]->out, n * S);
-            if (!dev) return RSMI_ERR_DEVICE;
-            if (enc)
-                rc = launch_encode_rows(c, *plan, dev, n * S, dev + k * S, n * S, S, 1,
-                                        want16 ? reinterpret_cast<uint32_t*>(c->d_crc) + j * n : nullptr,
-                                        want32 ? reinterpret_cast<uint32_t*>(c->d_crc32) + j * n : nullptr, st);
+        // after the first launch an error must not return before the stream is idle: the queued
+        // kernels still read and write the callers' buffers, which the callers reuse once told
+        // 
+        bool launched = false;
+        auto fail = [&](int e) {
+            if (launched) (void)hipStreamSynchronize(st);
+            return e;
+        };
+        uint32_t* d16 = want16 ? reinterpret_cast<uint32_t*>(c->d_crc) : nullptr;
+        uint32_t* d32 = want32 ? reinterpret_cast<uint32_t*>(c->d_crc32) : nullptr;
+        // the table form: in / out are offsets from each block's base ([k data | m parity] at
+        // pitch S for encode, n rows in place for reconstruct); the CRC-32 keeps a launch per block
+        bool table = nb > 1 && !want32;
+        for (size_t j0 = 0; j0 < nb && table; j0 += size_t(kTableBlocks)) {
+            const size_t cnt = std::min(size_t(kTableBlocks), nb - j0);
+            BlockBases tb;
+            for (size_t i = 0; i < cnt; i++) tb.b[i] = uint64_t(reinterpret_cast<uintptr_t>(dev[j0 + i]));
+            uint8_t* const par = reinterpret_cast<uint8_t*>(uintptr_t(k * S));  // offset of the parity rows
+            if (enc && want16)
+                rc = launch_plan_crc(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, d16 + j0 * n, st, &tb);
+            else if (enc)
+                rc = launch_plan(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, st, nullptr, &tb);
             else
-                rc = launch_plan(c, *plan, dev, S, n * S, dev, S, n * S, S, 1, st);
-            if (rc) return rc;
+                rc = launch_plan(c, *plan, nullptr, S, 0, nullptr, S, 0, S, cnt, st, nullptr, &tb);
+            if (rc == RSMI_ERR_INVALID_ARG && j0 == 0) {
+                table = false;  // no table kernel for this shape: a launch per request
+                break;
+            }
+            if (rc) return fail(rc);
+            launched = true;
+        }
+        for (size_t j = 0; j < nb && !table; j++) {
+            if (enc)
+                rc = launch_encode_rows(c, *plan, dev[j], n * S, dev[j] + k * S, n * S, S, 1, d16 ? d16 + j * n : nullptr,
+                                        d32 ? d32 + j * n : nullptr, st);
+            else
+                rc = launch_plan(c, *plan, dev[j], S, n * S, dev[j], S, n * S, S, 1, st);
+            if (rc) return fail(rc);
+            launched = true;
         }
         const uint32_t *h16, *h32;
-        if ((rc = readback(c, want16 ? reinterpret_cast<const uint32_t*>(c->d_crc) : nullptr,
-                           want32 ? reinterpret_cast<const uint32_t*>(c->d_crc32) : nullptr, nb * n * 4, st, h16,
-                           h32)))
-            return rc;
+        if ((rc = readback(c, d16, d32, nb * n * 4, st, h16, h32))) return fail(rc);
         HIP_TRY(hipStreamSynchronize(st));
         if (want16) std::memcpy(r16.data(), h16, nb * n * 4);
         if (want32) std::memcpy(r32.data(), h32, nb * n * 4);
@@ -147,11 +178,47 @@ void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
     }
 }
 
-void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
+// The context that codes lane `lane`'s batches: the context itself for lane 0, else its child
+// lane context, opened with the same k, m, device and options on first use.  nullptr with *rc
+// set when it cannot be opened.
+rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
+    *rc = RSMI_OK;
+    if (lane == 0) return c;
+    std::lock_guard<std::mutex> g(c->lanes_mu);
+    if (c->lanes.size() < size_t(lane)) c->lanes.resize(size_t(lane), nullptr);
+    rsmi_ctx*& l = c->lanes[size_t(lane - 1)];
+    if (l) return l;
+    rsmi_ctx* x = nullptr;
+    if ((*rc = rsmi_open(c->k, c->m, c->device, &x))) return nullptr;
+    {
+        std::lock_guard<std::mutex> gx(x->mu);
+        x->opt_crc16_fold = c->opt_crc16_fold;
+        x->opt_crc32_fold = c->opt_crc32_fold;
+        x->opt_fused_fold = c->opt_fused_fold;
+        x->opt_waves_per_cu = c->opt_waves_per_cu;
+        x->opt_zero_copy = c->opt_zero_copy;
+        x->opt_small_bytes = c->opt_small_bytes;
+        *rc = ensure_device(x);
+    }
+    if (*rc) {
+        rsmi_close(x);
+        return nullptr;
+    }
+    l = x;
+    return l;
+}
+
+void run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch) {
     const size_t n = size_t(c->n);
     // test hook (option "inject_host_fault"): this batch fails as a host allocation would
     for (int v = c->opt_inject_host_fault.load(); v > 0;)
         if (c->opt_inject_host_fault.compare_exchange_weak(v, v - 1)) throw std::bad_alloc();
+    int rc;
+    rsmi_ctx* x = lane_context(c, lane, &rc);
+    if (!x) {
+        for (auto* r : batch) r->rc = rc;
+        return;
+    }
     std::map<std::string, std::vector<rsmi_ctx::CoalReq*>> groups;
     for (auto* r : batch) groups[r->key].push_back(r);
     for (auto& g : groups) {
@@ -159,19 +226,19 @@ void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch) {
         const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
         const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
         for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk)
-            run_coalesced_group(c, g.second.data() + j0, std::min(chunk, g.second.size() - j0));
+            run_coalesced_group(x, g.second.data() + j0, std::min(chunk, g.second.size() - j0));
     }
+    if (x != c) set_last_kernel(c, rsmi_last_kernel(x));
 }
 
-// Queue a request and either wait for the executor or become it (group_commit.hpp).
+// Queue a request and either wait for an executor or become one (group_commit.hpp).  The device
+// check takes no lock once the context is bound, so callers queue while a batch is being coded
+// (under the lock) instead of waiting behind it.
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        int rc = ensure_device(c);
-        if (rc) return rc;
-    }
-    c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us,
-                   [c](std::vector<rsmi_ctx::CoalReq*>& batch) { run_coalesced(c, batch); });
+    int rc = ensure_device_fast(c);
+    if (rc) return rc;
+    c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us, int(c->opt_coalesce_lanes),
+                   [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { run_coalesced(c, lane, batch); });
     return req.rc;
 }
 
@@ -211,6 +278,34 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     for (int i = 0; i < c->n; i++) key.push_back(want[i] ? '1' : '0');
     rsmi_ctx::CoalReq req{nullptr, 0, shards, nullptr, nullptr, std::move(key), RSMI_OK, false};
     return coalesce(c, req);
+} catch (...) {
+    return rsmi::impl::exception_status();
+}
+
+int rsmi_warm(rsmi_ctx* c) try {
+    if (!c) return RSMI_ERR_INVALID_ARG;
+    int rc = ensure_device_fast(c);
+    if (rc) return rc;
+    // one tiny in-place encode + CRC-16 per lane (S = 64: the fused kernel), as a lone request of
+    // that lane, so each lane's context binds its streams, plan, tables and read-back area now
+    const size_t n = size_t(c->n), S = 64, B = size_t(c->k) * S;
+    uint8_t* buf = nullptr;
+    if (pinned_alloc(reinterpret_cast<void**>(&buf), n * S) != hipSuccess) {
+        (void)hipGetLastError();
+        return RSMI_ERR_DEVICE;
+    }
+    std::memset(buf, 1, B);
+    std::vector<uint32_t> raw(n);
+    for (int lane = 0; lane < int(c->opt_coalesce_lanes) && rc == RSMI_OK; lane++) {
+        rsmi_ctx* x = lane_context(c, lane, &rc);
+        if (!x) break;
+        rsmi_ctx::CoalReq req{buf, B, buf, raw.data(), nullptr, "E" + std::to_string(S) + ":", RSMI_OK, false};
+        rsmi_ctx::CoalReq* r = &req;
+        run_coalesced_group(x, &r, 1);
+        rc = req.rc;
+    }
+    (void)hipHostFree(buf);
+    return rc;
 } catch (...) {
     return rsmi::impl::exception_status();
 }

@@ -53,7 +53,31 @@ int ensure_device(rsmi_ctx* c) {
     c->staging.resize(3);
     for (auto& s : c->staging) HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     c->dev_ready = true;
+    c->dev_ready_flag.store(true, std::memory_order_release);
     return RSMI_OK;
+}
+
+int ensure_device_fast(rsmi_ctx* c) {
+    if (c->dev_ready_flag.load(std::memory_order_acquire)) return RSMI_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    return ensure_device(c);
+}
+
+void set_last_kernel(rsmi_ctx* c, const std::string& label) {
+    std::lock_guard<std::mutex> g(c->lk_mu);
+    c->last_kernel = label;
+}
+
+CrcScratch& crc_scratch(rsmi_ctx* c, hipStream_t st) {
+    for (const Staging& s : c->staging)
+        if (s.stream == st) return c->own_scratch;
+    return c->stream_scratch[st];
+}
+
+int reserve_on(uint8_t*& p, size_t& cap, size_t need, hipStream_t st) {
+    if (cap >= need) return RSMI_OK;
+    if (p) HIP_TRY(hipStreamSynchronize(st));
+    return reserve(p, cap, need);
 }
 
 // Build the device tiles for a coefficient matrix coef (rows x K) mapping input rows
@@ -178,22 +202,38 @@ const char* kernel_label(int K, int MT, int NT, bool fast) {
 // 2-row -3 %, RS(16,4) 2-row -4 %, RS(4,2) 1-row -5 %; RS(16,4) encode is a tie).
 int auto_cache_policy(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
 
+uintptr_t table_alignment(const BlockBases* tb, uint64_t nblocks) {
+    uintptr_t a = 0;
+    for (uint64_t b = 0; tb && b < nblocks; b++) a |= uintptr_t(tb->b[b]);
+    return a;
+}
+
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
-                const CrcFuse* fuse) {
+                const CrcFuse* fuse, const BlockBases* tb) {
     if (nblocks == 0 || S == 0) return RSMI_OK;
-    const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
-                         in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (uint64_t(1) << 31);
+    // tb: a table of block bases (in / out are offsets from each), one launch of at most
+    // kTableBlocks blocks, table kernels only (callers fall back to a launch per block)
+    if (tb && (nblocks > uint64_t(kTableBlocks) || fuse)) return RSMI_ERR_INVALID_ARG;
+    const uintptr_t tba = table_alignment(tb, nblocks);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(in) | tba) % 16 == 0) &&
+                         ((reinterpret_cast<uintptr_t>(out) | tba) % 16 == 0) && in_rs % 16 == 0 && in_bs % 16 == 0 &&
+                         out_rs % 16 == 0 && out_bs % 16 == 0 && in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) &&
+                         S < (uint64_t(1) << 31);
     // any other layout with rows of at least 16 bytes: the unaligned-window variant (D = 1)
     const bool ua = !aligned && S >= 16 && S < (uint64_t(1) << 31) && in_rs >= S && out_rs >= S;
     if (fuse && ((!aligned && !ua) || plan.tiles.size() != 1)) return RSMI_ERR_INVALID_ARG;  // callers fall back
                                                                                               // to the separate pass
+    if (tb)
+        for (const DevTile& t : plan.tiles)
+            if (t.K > 16 || !(aligned ? fast_kernels().fn_tb : fast_kernels().ua_tb)[t.K][t.MT] || (!aligned && !ua))
+                return RSMI_ERR_INVALID_ARG;
     for (const DevTile& t : plan.tiles) {
         const int NT = auto_cache_policy(t.K, t.MT);
         void* fn = nullptr;
         if (t.K <= 16) {
-            if (fuse) fn = ua ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().crc[t.K][t.MT];
+            if (tb) fn = aligned ? fast_kernels().fn_tb[t.K][t.MT] : fast_kernels().ua_tb[t.K][t.MT];
+            else if (fuse) fn = ua ? fast_kernels().ua_crc[t.K][t.MT] : fast_kernels().crc[t.K][t.MT];
             else if (aligned) fn = fast_kernels().fn[t.K][t.MT];
             else if (ua) fn = fast_kernels().ua[t.K][t.MT];
         }
@@ -223,14 +263,18 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 const uint64_t rec_per_block = tpb * uint64_t((((t.K + t.MT) + 3) / 4 + 1) / 2) * kWave;
                 uint32_t* crec = fuse ? fuse->rec + b0 * rec_per_block : nullptr;
                 uint32_t* ctail = fuse && fuse->tail ? fuse->tail + b0 * uint64_t(t.K + t.MT) : nullptr;
+                NoBases nob;
+                void* bases = tb ? const_cast<BlockBases*>(tb) : static_cast<void*>(&nob);
                 void* args[] = {&pd,    &inb,   &outb,   &in_bs, &in_rs, &out_bs, &out_rs, &S32,
-                                &cpb32, &tpb32, &ntiles, &ctbl,  &crec,  &ctail};
+                                &cpb32, &tpb32, &ntiles, &ctbl,  &crec,  &ctail, bases};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));
                 HIP_TRY(hipLaunchKernel(fn, dim3(uint32_t(wgs)), dim3(uint32_t(wpg * kWave)), args, 0, stream));
             }
-            c->last_kernel = kernel_label(t.K, t.MT, NT, true);
-            if (ua) c->last_kernel += ",UA";
-            if (fuse) c->last_kernel += ",CRC";
+            std::string label = kernel_label(t.K, t.MT, NT, true);
+            if (ua) label += ",UA";
+            if (fuse) label += ",CRC";
+            if (tb) label += ",TB";
+            set_last_kernel(c, label);
         } else {
             const uint64_t groups = (S + 3) / 4;
             const uint32_t gx = uint32_t(std::min<uint64_t>((groups + kWG - 1) / kWG, 4096));
@@ -238,7 +282,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             const RsPlanDev* pd = t.dev;
             void* args[] = {&pd, &in, &out, &in_bs, &in_rs, &out_bs, &out_rs, &S, &nblocks};
             HIP_TRY(hipLaunchKernel(generic_kernel(), dim3(gx, gy), dim3(kWG), args, 0, stream));
-            c->last_kernel = kernel_label(t.K, t.MT, 0, false);
+            set_last_kernel(c, kernel_label(t.K, t.MT, 0, false));
         }
     }
     return hip_status(hipGetLastError());
@@ -334,6 +378,7 @@ int rsmi_open(int k, int m, int device, rsmi_ctx** out) try {
 
 void rsmi_close(rsmi_ctx* c) {
     if (!c) return;
+    for (rsmi_ctx* l : c->lanes) rsmi_close(l);
     {
         std::lock_guard<std::mutex> g(c->mu);
         c->plans.clear();
@@ -352,8 +397,15 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->h_raw) (void)hipHostFree(c->h_raw);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
-            if (c->d_chunks) (void)hipFree(c->d_chunks);
-            if (c->d_fctr) (void)hipFree(c->d_fctr);
+            auto free_scratch = [](CrcScratch& x) {
+                if (x.d_chunks) (void)hipFree(x.d_chunks);
+                if (x.d_fctr) (void)hipFree(x.d_fctr);
+            };
+            free_scratch(c->own_scratch);
+            for (auto& e : c->stream_scratch) {
+                (void)hipStreamSynchronize(e.first);
+                free_scratch(e.second);
+            }
             if (c->d_crc32_tbl) (void)hipFree(c->d_crc32_tbl);
             if (c->d_crc32) (void)hipFree(c->d_crc32);
         }
@@ -385,7 +437,31 @@ int rsmi_decode_matrix(const rsmi_ctx* c, const uint8_t* present, uint8_t* out, 
 
 int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     if (!c || !key) return RSMI_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if ((rc = apply_option(c, key, value))) return rc;
+    }
+    // the coalescer's lane contexts code with the same options (the test hook stays with the
+    // context whose batches it fails)
+    if (std::strcmp(key, "inject_host_fault") != 0) {
+        std::lock_guard<std::mutex> g(c->lanes_mu);
+        for (rsmi_ctx* l : c->lanes) {
+            std::lock_guard<std::mutex> gl(l->mu);
+            (void)apply_option(l, key, value);
+        }
+    }
+    return RSMI_OK;
+} catch (...) {
+    return rsmi::impl::exception_status();
+}
+
+}  // extern "C"
+
+namespace rsmi {
+namespace impl {
+
+int apply_option(rsmi_ctx* c, const char* key, long value) {
     if (!std::strcmp(key, "zero_copy")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
         c->opt_zero_copy = int(value);
@@ -413,15 +489,28 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     } else if (!std::strcmp(key, "inject_host_fault")) {
         if (value < 0 || value > 1000) return RSMI_ERR_INVALID_ARG;
         c->opt_inject_host_fault.store(int(value));
+    } else if (!std::strcmp(key, "coalesce_lanes")) {
+        if (value < 1 || value > 16) return RSMI_ERR_INVALID_ARG;
+        c->opt_coalesce_lanes = value;
     } else {
         return RSMI_ERR_INVALID_ARG;
     }
     return RSMI_OK;
-} catch (...) {
-    return rsmi::impl::exception_status();
 }
 
-const char* rsmi_last_kernel(const rsmi_ctx* c) { return c ? c->last_kernel.c_str() : ""; }
+}  // namespace impl
+}  // namespace rsmi
+
+extern "C" {
+
+// a copy per calling thread: another thread's call may relabel the context meanwhile
+const char* rsmi_last_kernel(const rsmi_ctx* c) {
+    static thread_local std::string copy;
+    if (!c) return "";
+    std::lock_guard<std::mutex> g(c->lk_mu);
+    copy = c->last_kernel;
+    return copy.c_str();
+}
 
 void* rsmi_host_alloc(size_t bytes) {
     void* p = nullptr;

@@ -149,31 +149,41 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
 // (MT <= 4) and either an aligned layout or S >= 16; returns RSMI_ERR_INVALID_ARG otherwise
 // (callers then run the separate pass).
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st) {
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
+                    const BlockBases* tb) {
     if (plan.tiles.size() != 1 || plan.tiles[0].K > 16) return RSMI_ERR_INVALID_ARG;
+    // tb: a table of block bases (in / out are offsets from each), one launch of at most
+    // kTableBlocks blocks on the matrix-core fold; callers fall back to a launch per block
+    if (tb && (nblocks > size_t(kTableBlocks) || c->opt_fused_fold != 1)) return RSMI_ERR_INVALID_ARG;
     const DevTile& tile = plan.tiles[0];
     const size_t nsh = size_t(tile.K + tile.MT);
     const size_t cpb = (S + 15) / 16, tpb = (cpb + kWave - 1) / kWave;
     int rc;
     if ((rc = ensure_crc_tables(c))) return rc;
-    const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
-                         in_rs % 16 == 0 && in_bs % 16 == 0 && out_rs % 16 == 0 && out_bs % 16 == 0 &&
-                         in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) && S < (size_t(1) << 31);
+    const uintptr_t tba = table_alignment(tb, nblocks);
+    const bool aligned = (reinterpret_cast<uintptr_t>(in) | tba) % 16 == 0 &&
+                         (reinterpret_cast<uintptr_t>(out) | tba) % 16 == 0 && in_rs % 16 == 0 && in_bs % 16 == 0 &&
+                         out_rs % 16 == 0 && out_bs % 16 == 0 && in_rs >= round_up(S, 16) && out_rs >= round_up(S, 16) &&
+                         S < (size_t(1) << 31);
     // unaligned-window layouts (the Split layout, page-locked host rows at pitch S): S >= 16
     const bool ua = !aligned && S >= 16 && S < (size_t(1) << 31) && in_rs >= S && out_rs >= S;
-    void* mfma_fn = aligned ? fast_kernels().fused[tile.K][tile.MT] : ua ? fast_kernels().fused_ua[tile.K][tile.MT] : nullptr;
+    const FastKernelTable& kt = fast_kernels();
+    void* mfma_fn = aligned ? (tb ? kt.fused_tb : kt.fused)[tile.K][tile.MT]
+                            : ua ? (tb ? kt.fused_ua_tb : kt.fused_ua)[tile.K][tile.MT] : nullptr;
+    if (tb && !mfma_fn) return RSMI_ERR_INVALID_ARG;
     if (mfma_fn && c->opt_fused_fold == 1) {
         // the fold on the matrix cores (rs_fused_mfma_kernel): a unit of 4 tiles per workgroup,
         // then the records' combine
         const size_t upb = (tpb + kFusedUnitTiles - 1) / kFusedUnitTiles;
         const size_t nacc = (nsh + 1) / 2;  // two-shard accumulators: a record byte per lane each
         const size_t rec_per_block = upb * nacc * kWave;
-        if ((rc = reserve(c->d_chunks, c->chunks_cap, nblocks * rec_per_block))) return rc;
-        uint8_t* rec = c->d_chunks;
+        CrcScratch& sc = crc_scratch(c, st);
+        if ((rc = reserve_on(sc.d_chunks, sc.chunks_cap, nblocks * rec_per_block, st))) return rc;
+        uint8_t* rec = sc.d_chunks;
         void* fn = mfma_fn;
         const RsPlanDev* pd = tile.dev;
         uint32_t S32 = uint32_t(S), cpb32 = uint32_t(cpb), tpb32 = uint32_t(tpb), upb32 = uint32_t(upb);
-        const uint32_t* tb = c->d_crc_tbl;
+        const uint32_t* ctb = c->d_crc_tbl;
         uint64_t ibs = in_bs, irs = in_rs, obs = out_bs, ors = out_rs;
         // A^e moves a row's value from the end of its last unit to the row's end
         const int64_t unit_bytes = int64_t(kFusedUnitTiles) * kWave * 16;
@@ -182,18 +192,22 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
         for (int b = 0; b < 16; b++) sh.col[b] = crc16_tables().shift(uint16_t(1u << b), e);
         // a launch of a few units (the per-block calls of DagNode.Put) combines in the kernel: one
         // launch instead of two; big ones keep the separate combine (rs_fused_mfma_kernel INL)
-        void* inl_fn = aligned ? fast_kernels().fused_inl[tile.K][tile.MT] : fast_kernels().fused_ua_inl[tile.K][tile.MT];
+        void* inl_fn = aligned ? (tb ? kt.fused_inl_tb : kt.fused_inl)[tile.K][tile.MT]
+                               : (tb ? kt.fused_ua_inl_tb : kt.fused_ua_inl)[tile.K][tile.MT];
         const bool inline_combine = RSMI_FUSED_COOP && inl_fn && nblocks * upb <= kFusedInlineUnits;
         if (inline_combine) fn = inl_fn;
         // per-block unit counters of the inline combine: zeroed once when allocated, and every
         // launch leaves them at zero again (atomicInc wraps at the block's last unit)
-        if (inline_combine && c->fctr_cap < nblocks) {
-            if (c->d_fctr) HIP_TRY(hipFree(c->d_fctr));
-            c->d_fctr = nullptr;
-            c->fctr_cap = 0;
-            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_fctr), nblocks * 4));
-            HIP_TRY(hipMemsetAsync(c->d_fctr, 0, nblocks * 4, st));
-            c->fctr_cap = nblocks;
+        if (inline_combine && sc.fctr_cap < nblocks) {
+            if (sc.d_fctr) {
+                HIP_TRY(hipStreamSynchronize(st));  // the last launch on this stream may still count
+                HIP_TRY(hipFree(sc.d_fctr));
+            }
+            sc.d_fctr = nullptr;
+            sc.fctr_cap = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sc.d_fctr), nblocks * 4));
+            HIP_TRY(hipMemsetAsync(sc.d_fctr, 0, nblocks * 4, st));
+            sc.fctr_cap = nblocks;
         }
         // launches of at most 2^31 units (32-bit unit index)
         const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(1) << 31) / upb);
@@ -203,10 +217,12 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             const uint8_t* inb = in + b0 * in_bs;
             uint8_t* outb = out + b0 * out_bs;
             uint8_t* rb = rec + b0 * rec_per_block;
-            uint32_t* cb = inline_combine ? c->d_fctr + b0 : nullptr;
+            uint32_t* cb = inline_combine ? sc.d_fctr + b0 : nullptr;
             uint32_t* rw = raw + b0 * nsh;
-            void* args[] = {&pd,  &inb,   &outb,   &ibs, &irs, &obs, &ors, &S32, &cpb32,
-                            &tpb32, &upb32, &nunits, &tb,  &rb,  &cb,  &rw,  &sh};
+            NoBases nob;
+            void* bases = tb ? const_cast<BlockBases*>(tb) : static_cast<void*>(&nob);
+            void* args[] = {&pd,    &inb,   &outb,   &ibs, &irs, &obs, &ors, &S32, &cpb32,
+                            &tpb32, &upb32, &nunits, &ctb, &rb,  &cb,  &rw,  &sh,  bases};
             const uint32_t wgs = RSMI_FUSED_COOP ? nunits : (nunits + kWG / kWave - 1) / (kWG / kWave);
             HIP_TRY(hipLaunchKernel(fn, dim3(wgs), dim3(kWG), args, 0, st));
         }
@@ -214,7 +230,7 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             uint32_t nacc32 = uint32_t(nacc), nsh32 = uint32_t(nsh);
             uint64_t nb64 = nblocks;
             const uint8_t* crec = rec;
-            void* cargs[] = {&tb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
+            void* cargs[] = {&ctb, &crec, &upb32, &nacc32, &nsh32, &sh, &nb64, &raw};
             // a persistent grid of up to 8 workgroups per CU, 4 waves each, over (block, 4-row group) items
             const uint64_t items = nblocks * ((nsh + 3) / 4);
 #ifndef RSMI_COMBINE_WGS_PER_CU
@@ -225,26 +241,28 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             HIP_TRY(hipLaunchKernel(crc16_combine_mfma_kernel(), dim3(grid), dim3(kWG), cargs, 0, st));
         }
         char buf[96];
-        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s%s", tile.K, tile.MT,
-                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA", inline_combine ? ",INL" : "");
-        c->last_kernel = buf;
+        std::snprintf(buf, sizeof buf, "rs_fused_mfma_kernel<K=%d,MT=%d,NT=%d>%s%s%s", tile.K, tile.MT,
+                      auto_cache_policy(tile.K, tile.MT), aligned ? "" : ",UA", inline_combine ? ",INL" : "",
+                      tb ? ",TB" : "");
+        set_last_kernel(c, buf);
         return hip_status(hipGetLastError());
     }
     const size_t ns2 = ((nsh + 3) / 4 + 1) / 2;
     const size_t rec_bytes = nblocks * tpb * ns2 * kWave * 4, tail_bytes = nblocks * nsh * 4;
-    if ((rc = reserve(c->d_chunks, c->chunks_cap, rec_bytes + tail_bytes))) return rc;
+    CrcScratch& sc = crc_scratch(c, st);
+    if ((rc = reserve_on(sc.d_chunks, sc.chunks_cap, rec_bytes + tail_bytes, st))) return rc;
     if (!aligned && S < 16) return RSMI_ERR_INVALID_ARG;
     CrcFuse fz;
     fz.tbl = c->d_crc_tbl;
-    fz.rec = reinterpret_cast<uint32_t*>(c->d_chunks);
-    fz.tail = aligned ? nullptr : reinterpret_cast<uint32_t*>(c->d_chunks + rec_bytes);
+    fz.rec = reinterpret_cast<uint32_t*>(sc.d_chunks);
+    fz.tail = aligned ? nullptr : reinterpret_cast<uint32_t*>(sc.d_chunks + rec_bytes);
     if ((rc = launch_plan(c, plan, in, in_rs, in_bs, out, out_rs, out_bs, S, nblocks, st, &fz))) return rc;
-    const uint32_t* tb = c->d_crc_tbl;
+    const uint32_t* ctb = c->d_crc_tbl;
     const uint32_t* rec = fz.rec;
     const uint32_t* tail = fz.tail;
     uint32_t tpb32 = uint32_t(tpb), nsh32 = uint32_t(nsh);
     uint64_t S64 = S, nb64 = nblocks;
-    void* args[] = {&tb, &rec, &tail, &tpb32, &nsh32, &S64, &nb64, &raw};
+    void* args[] = {&ctb, &rec, &tail, &tpb32, &nsh32, &S64, &nb64, &raw};
     // one wave per block, a persistent grid of up to 8 workgroups per CU (the nibble-sliced
     // power tables take 1.9 KiB of LDS per workgroup)
     const uint32_t grid = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((nblocks + 3) / 4, uint64_t(c->num_cu) * 8)));
@@ -310,8 +328,8 @@ int rsmi_crc16_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
                     static_cast<hipStream_t>(stream));
     if (rc) return rc;
     const bool aligned = reinterpret_cast<uintptr_t>(d_rows) % 16 == 0 && shard_stride % 16 == 0 && block_stride % 16 == 0;
-    c->last_kernel = c->opt_crc16_fold == 1 ? (aligned ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel,MFMA,UA")
-                                            : "rs_crc16_rows_kernel";
+    set_last_kernel(c, c->opt_crc16_fold == 1 ? (aligned ? "rs_crc16_rows_kernel,MFMA" : "rs_crc16_rows_kernel,MFMA,UA")
+                                              : "rs_crc16_rows_kernel");
     return hip_status(hipGetLastError());
 } catch (...) {
     return rsmi::impl::exception_status();
@@ -331,7 +349,7 @@ int rsmi_crc32_rows_dev(rsmi_ctx* c, const uint8_t* d_rows, size_t shard_stride,
     rc = launch_crc32(c, d_rows, shard_stride, block_stride, uint32_t(nrows), S, nblocks, d_raw_out, out_block_stride,
                       st);
     if (rc) return rc;
-    c->last_kernel = c->opt_crc32_fold == 1 ? "rs_crc32_rows_kernel,MFMA" : "rs_crc32_rows_kernel";
+    set_last_kernel(c, c->opt_crc32_fold == 1 ? "rs_crc32_rows_kernel,MFMA" : "rs_crc32_rows_kernel");
     return hip_status(hipGetLastError());
 } catch (...) {
     return rsmi::impl::exception_status();

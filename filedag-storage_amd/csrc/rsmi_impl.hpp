@@ -75,10 +75,23 @@ struct CrcFuse {
 }  // namespace impl
 }  // namespace rsmi
 
+// Device scratch of the fused encode + CRC-16 (records of the tiles or units, and the inline
+// combine's per-block unit counters), one per stream its launches go to: the context's own
+// streams share one (host calls hold the context lock through their synchronisation), and every
+// caller stream of the device-resident calls gets its own, so concurrent calls on different
+// streams never share records or counters.
+struct CrcScratch {
+    uint8_t* d_chunks = nullptr;  // tile records and tails (CrcFuse) or unit records
+    size_t chunks_cap = 0;
+    uint32_t* d_fctr = nullptr;  // per-block unit counters of the inline combine
+    size_t fctr_cap = 0;
+};
+
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0, device = 0;
     rsmi::Matrix M;  // n x k
     std::mutex mu;
+    std::atomic<bool> dev_ready_flag{false};  // dev_ready, readable without mu (coalesce)
     bool dev_ready = false;
     int dev_status = RSMI_OK;
     int num_cu = 256;
@@ -94,10 +107,8 @@ struct rsmi_ctx {
     size_t crc32_cap = 0;
     rsmi::Crc32Shift crc32_shift{};  // launch_crc32's per-S shift matrix, for crc32_shift_S
     uint64_t crc32_shift_S = ~uint64_t(0);
-    uint8_t* d_chunks = nullptr;    // fused encode + CRC-16: tile records and tails (CrcFuse)
-    size_t chunks_cap = 0;
-    uint32_t* d_fctr = nullptr;     // fused encode + CRC-16 on the matrix cores: per-block unit counters
-    size_t fctr_cap = 0;
+    CrcScratch own_scratch;  // the fused encode + CRC-16's scratch on the context's own streams
+    std::map<hipStream_t, CrcScratch> stream_scratch;  // ... and on each caller stream (device-resident calls)
     // options
     int opt_crc16_fold = 1;     // aligned CRC-16 rows pass: 0 = nibble tables, 1 = matrix cores (fp4)
     int opt_crc32_fold = RSMI_CRC32_FOLD_DEFAULT;  // CRC-32 rows pass: 0 = nibble tables, 1 = matrix cores
@@ -111,7 +122,8 @@ struct rsmi_ctx {
     size_t h_raw_cap = 0;
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
-    std::string last_kernel;
+    std::string last_kernel;  // diagnostics (rsmi_last_kernel), under lk_mu
+    mutable std::mutex lk_mu;
     // group commit for rsmi_encode_block_coalesced (see there)
     struct CoalReq {
         // encode: block/B in, out = (k+m)*S shards, raw optional; reconstruct: out = n*S
@@ -131,6 +143,12 @@ struct rsmi_ctx {
     std::atomic<int> opt_inject_host_fault{0};  // test hook: the next coalesced batches throw std::bad_alloc
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;
+    // Coalesced batches run on up to opt_coalesce_lanes lanes at once: lane 0 is this context, lane
+    // i > 0 the child context lanes[i - 1] (same k, m, device and options; opened on first use), so
+    // one batch can be coded while the next is launched and the callers' queue stays one queue
+    long opt_coalesce_lanes = 2;
+    std::vector<rsmi_ctx*> lanes;
+    std::mutex lanes_mu;
 };
 
 namespace rsmi {
@@ -153,9 +171,17 @@ int reconstruct_plan(rsmi_ctx* c, const uint8_t* present, const uint8_t* want, s
 std::vector<uint8_t> want_mask(const rsmi_ctx* c, const uint8_t* present, int data_only);
 const char* kernel_label(int K, int MT, int NT, bool fast);
 int auto_cache_policy(int K, int MT);
+// tb: a table of block bases, in / out then being offsets from each (at most kTableBlocks blocks,
+// the table kernels only: RSMI_ERR_INVALID_ARG when the shape has none, callers then launch per block)
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
-                const CrcFuse* fuse = nullptr);
+                const CrcFuse* fuse = nullptr, const BlockBases* tb = nullptr);
+uintptr_t table_alignment(const BlockBases* tb, uint64_t nblocks);  // OR of the table's first nblocks bases
+void set_last_kernel(rsmi_ctx* c, const std::string& label);
+CrcScratch& crc_scratch(rsmi_ctx* c, hipStream_t st);  // caller holds ctx->mu
+// reserve() for device scratch a stream's kernels may still be reading: that stream is
+// synchronised before the old buffer is freed
+int reserve_on(uint8_t*& p, size_t& cap, size_t need, hipStream_t st);
 int reserve(uint8_t*& p, size_t& cap, size_t need);
 int count_present(const rsmi_ctx* c, const uint8_t* present, int& np, int& dp);
 int reconstruct_precheck(const rsmi_ctx* c, const uint8_t* present, const uint8_t* want);
@@ -193,14 +219,18 @@ int launch_crc(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint64_t bstri
 int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                              size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
-                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
+                    size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
+                    const BlockBases* tb = nullptr);
 int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
                        size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
 int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S);
 void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb);
-void run_coalesced(rsmi_ctx* c, std::vector<rsmi_ctx::CoalReq*>& batch);
+void run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch);
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req);
+int ensure_device_fast(rsmi_ctx* c);
+rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc);  // coalescing lane `lane`'s context (0: c)  // ensure_device without the context lock once the device is bound
+int apply_option(rsmi_ctx* c, const char* key, long value);  // caller holds ctx->mu
 
 }  // namespace impl
 }  // namespace rsmi

@@ -62,6 +62,7 @@ def lib() -> ctypes.CDLL:
     sig = {
         "rsmi_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
         "rsmi_close": (None, [ctypes.c_void_p]),
+        "rsmi_warm": (ctypes.c_int, [ctypes.c_void_p]),
         "rsmi_device_count": (ctypes.c_int, []),
         "rsmi_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "rsmi_abi_version": (ctypes.c_int, []),
@@ -209,6 +210,10 @@ class Codec:
 
     def set_option(self, key: str, value: int) -> None:
         _check(lib().rsmi_set_option(self._h, key.encode(), int(value)))
+
+    def warm(self) -> None:
+        """rsmi_warm: bind the device and bring up every coalescing lane now."""
+        _check(lib().rsmi_warm(self._h))
 
     def last_kernel(self) -> str:
         return lib().rsmi_last_kernel(self._h).decode()

@@ -30,8 +30,11 @@ extern "C" {
  * return RSMI_ERR_INVALID_ARG); device groups, NUMA placement, the key slot hash and
  * rsmi_reconstruct_batch_host_verify were added; "crc16_fused_fold" is new.
  * 3: no C++ exception crosses the boundary: every status-returning entry point that can allocate
- * on the host returns RSMI_ERR_HOST instead (new status). */
-#define RSMI_ABI_VERSION 3
+ * on the host returns RSMI_ERR_HOST instead (new status).
+ * 4: coalesced calls run on up to "coalesce_lanes" batches at once (new option, default 2);
+ * rsmi_warm is new; the device-resident CRC entry points may run concurrently on different streams
+ * of one context; rsmi_last_kernel returns a per-thread copy. */
+#define RSMI_ABI_VERSION 4
 
 typedef struct rsmi_ctx rsmi_ctx;
 
@@ -59,6 +62,11 @@ enum rsmi_status {
  * so opening a context works (and reports argument errors) on a host without a GPU. */
 int rsmi_open(int k, int m, int device, rsmi_ctx** out);
 void rsmi_close(rsmi_ctx* ctx);
+
+/* Bring up the context's device resources before the first real call (a Dag Node does this when
+ * it starts): streams, the encode plan, the CRC tables and every coalescing lane (one tiny fused
+ * encode + CRC-16 each), so the first concurrent callers do not pay for them. */
+int rsmi_warm(rsmi_ctx* ctx);
 
 int rsmi_device_count(void);
 const char* rsmi_status_string(int status);
@@ -153,10 +161,14 @@ int rsmi_reconstruct_rows_batch_dev(rsmi_ctx* ctx, uint8_t* d_shards, size_t sha
 /* Erasure.EncodeData for one block (same output as rsmi_encode_block, plus R(shard) in
  * raw_out[0..k+m) when raw_out is not NULL), coalesced with concurrent callers on the same
  * context: DagNode.Put runs once per block from many goroutines (node.go:358-408), and
- * group commit turns those calls into GPU batches.  The caller that finds no batch running
- * executes every block queued so far (waiting up to option "coalesce_us" for more, default
- * 0; at most "coalesce_max" blocks, default 256) and wakes the others; blocks arriving
- * meanwhile form the next batch.  A lone caller never waits on anyone.  block may be
+ * group commit turns those calls into GPU batches.  A caller whose block is still queued and
+ * that finds one of the context's "coalesce_lanes" lanes free (default 2) executes every block
+ * queued so far (waiting up to option "coalesce_us" for more, default 0; at most
+ * "coalesce_max" blocks, default 256) and wakes the others; blocks arriving while every lane
+ * codes a batch form the next one.  Lane i > 0 codes on a child context of its own (streams and
+ * scratch), so one batch is launched while the one before it runs.  A batch whose blocks lie in
+ * page-locked memory (rsmi_host_alloc) is coded in place, up to 64 blocks per launch.  A lone
+ * caller never waits on anyone.  block may be
  * shards_out itself: the caller has already copied the block to the start of shards_out
  * (Split's copy, done on the caller's own thread), and the engine zero-pads and encodes it in
  * place; any other overlap of block and shards_out is not allowed. */
@@ -350,11 +362,13 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * nibble-table variants), "crc32_fold" (the mutcask CRC-32 rows pass: 1 = the fold on the
  * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
  * next N coalesced batches throw std::bad_alloc in the executor, so their requests return
- * RSMI_ERR_HOST; default 0).  Kernel variants measured slower than the defaults are not
+ * RSMI_ERR_HOST; default 0), "coalesce_lanes" (coalesced batches coded at once, 1-16, default
+ * 2; every option but the test hook also applies to the lanes' child contexts).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
-/* Name of the kernel the last device launch on this context used ("" if none). */
+/* Name of the kernel the last device launch on this context used ("" if none); a copy owned by
+ * the calling thread, valid until its next rsmi_last_kernel call. */
 const char* rsmi_last_kernel(const rsmi_ctx* ctx);
 
 #ifdef __cplusplus

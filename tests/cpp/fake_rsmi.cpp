@@ -98,6 +98,18 @@ struct rsmi_ctx {
 };
 
 namespace {
+// batches coded at once: the CPU codec runs concurrent callers side by side on every core (the
+// fair comparison for tools/bench_dagnode_cpu); the sanitizer builds use 4 lanes
+int coal_lanes() {
+#ifdef FAKE_RSMI_FAST
+    return std::min(cpu_threads(), rsmi::GroupCommit<Req>::kMaxLanes);
+#else
+    return 4;
+#endif
+}
+}  // namespace
+
+namespace {
 
 int encode_one(rsmi_ctx* c, const uint8_t* data, uint8_t* parity, size_t S) {
 #ifdef FAKE_RSMI_FAST
@@ -170,6 +182,7 @@ int rsmi_open(int k, int m, int device, rsmi_ctx** out) {
 }
 
 void rsmi_close(rsmi_ctx* c) { delete c; }
+int rsmi_warm(rsmi_ctx* c) { return c ? RSMI_OK : RSMI_ERR_INVALID_ARG; }
 
 void* rsmi_host_alloc(size_t bytes) { return std::malloc(bytes ? bytes : 1); }
 void rsmi_host_free(void* p) { std::free(p); }
@@ -261,7 +274,7 @@ int rsmi_encode_block_coalesced_crcs(rsmi_ctx* c, const uint8_t* block, size_t B
     if (B == 0) return RSMI_ERR_SHORT_DATA;
     if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
     Req req{true, block, B, shards_out, rsmi_shard_size(B, c->k), nullptr, 0, raw16, raw32, RSMI_OK, false};
-    c->coal.submit(req, 256, 0, [c](std::vector<Req*>& batch) { run_batch(c, batch); });
+    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); });
     return req.rc;
 }
 
@@ -281,7 +294,7 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     if (!any) return RSMI_OK;
     if (np < c->k) return RSMI_ERR_TOO_FEW_SHARDS;
     Req req{false, nullptr, 0, shards, S, present, data_only, nullptr, nullptr, RSMI_OK, false};
-    c->coal.submit(req, 256, 0, [c](std::vector<Req*>& batch) { run_batch(c, batch); });
+    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); });
     return req.rc;
 }
 

@@ -733,6 +733,9 @@ static void test_concurrent_puts() {
     int rc;
     rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
     CHECK(ctx != nullptr);
+    // every Put and degraded Get through the group commit (no lone-caller path), so the counters
+    // are exact
+    c.node->SetLoneCallerPaths(false);
     const long calls0 = lane_stat(k, m, 0, "coalesced_calls"), batches0 = lane_stat(k, m, 0, "coalesced_batches");
     std::vector<std::thread> th;
     std::vector<Status> st(size_t(T * per));
@@ -743,9 +746,7 @@ static void test_concurrent_puts() {
     for (auto& x : th) x.join();
     const long calls = lane_stat(k, m, 0, "coalesced_calls") - calls0;
     const long batches = lane_stat(k, m, 0, "coalesced_batches") - batches0;
-    // a Put that finds no other caller in flight takes the lone path (no group commit), so
-    // every Put is either coalesced or lone, and the concurrent ones coalesce
-    CHECK(calls >= 1 && calls <= T * per);
+    CHECK(calls == T * per);
     CHECK(batches >= 1 && batches <= calls);
     std::printf("concurrent puts: %ld encodes in %ld GPU batches\n", calls, batches);
     // degraded Gets from the same threads with data shard 2's node down: one erasure
@@ -762,7 +763,8 @@ static void test_concurrent_puts() {
     for (auto& x : th) x.join();
     c.dn[2]->SetOffline(false);
     const long rcalls = lane_stat(k, m, 0, "coalesced_calls") - rc0, rbatches = lane_stat(k, m, 0, "coalesced_batches") - rb0;
-    CHECK(rcalls >= 1 && rcalls <= T * per);
+    CHECK(rcalls == T * per);  // every Get misses data shard 2: one reconstruct each
+    c.node->SetLoneCallerPaths(true);
     std::printf("concurrent degraded gets: %ld reconstructs in %ld GPU batches\n", rcalls, rbatches);
     for (int i = 0; i < T * per; i++) {
         CHECK_OK(gst[i]);
@@ -793,7 +795,7 @@ static void test_group_commit_exec_throws() {
     };
     rsmi::GroupCommit<Req> gc(-7);
     std::atomic<int> throws{0};
-    auto exec = [&](std::vector<Req*>& batch) {
+    auto exec = [&](std::vector<Req*>& batch, int) {
         for (Req* r : batch)
             if (r->id % 3 == 0) {  // a batch holding any multiple of 3 fails as a whole
                 throws++;
@@ -807,7 +809,7 @@ static void test_group_commit_exec_throws() {
         th.emplace_back([&, t] {
             for (int i = t; i < 48; i += 8) {
                 reqs[size_t(i)].id = i;
-                gc.submit(reqs[size_t(i)], 4, 50, exec);
+                gc.submit(reqs[size_t(i)], 4, 50, 1, exec);
             }
         });
     for (auto& x : th) x.join();
@@ -821,8 +823,56 @@ static void test_group_commit_exec_throws() {
     CHECK(throws.load() >= 1 && failed >= 16 && gc.calls() == 48);
     Req last;
     last.id = 100;
-    gc.submit(last, 4, 0, exec);  // the queue still works after the failures
+    gc.submit(last, 4, 0, 1, exec);  // the queue still works after the failures
     CHECK(last.done && last.rc == 100);
+}
+
+// group_commit.hpp with several lanes: at most `lanes` batches execute at once, the batches
+// executing at once hold distinct lane ids, every request completes exactly once with its own
+// result, and the calls group (fewer batches than calls when callers pile up behind busy lanes).
+static void test_group_commit_lanes() {
+    struct Req {
+        int id = 0, rc = -1;
+        bool done = false;
+    };
+    for (int lanes : {1, 2, 3}) {
+        rsmi::GroupCommit<Req> gc(-7);
+        std::atomic<int> running{0}, peak{0}, overlap{0};
+        std::atomic<uint32_t> busy{0};
+        std::atomic<int> executed{0};
+        auto exec = [&](std::vector<Req*>& batch, int lane) {
+            const uint32_t bit = 1u << lane;
+            if (lane < 0 || lane >= lanes || (busy.fetch_or(bit) & bit)) overlap++;  // lane id in use twice
+            const int now = ++running;
+            for (int p = peak.load(); now > p && !peak.compare_exchange_weak(p, now);) {
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+            for (Req* r : batch) {
+                r->rc = r->id;
+                executed++;
+            }
+            running--;
+            busy.fetch_and(~bit);
+        };
+        const int T = 12, per = 20;
+        std::vector<Req> reqs(size_t(T * per));
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                for (int i = t; i < T * per; i += T) {
+                    reqs[size_t(i)].id = i;
+                    gc.submit(reqs[size_t(i)], 256, 0, lanes, exec);
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int i = 0; i < T * per; i++) CHECK(reqs[size_t(i)].done && reqs[size_t(i)].rc == i);
+        CHECK(overlap.load() == 0);
+        CHECK(peak.load() >= 1 && peak.load() <= lanes);
+        CHECK(executed.load() == T * per && gc.calls() == uint64_t(T * per));
+        CHECK(gc.batches() < gc.calls());
+        std::printf("group commit, %d lane(s): %llu calls in %llu batches, at most %d at once\n", lanes,
+                    (unsigned long long)gc.calls(), (unsigned long long)gc.batches(), peak.load());
+    }
 }
 
 int main(int argc, char** argv) {
@@ -840,6 +890,7 @@ int main(int argc, char** argv) {
                              // double lock on the queue's mutex once a throw has crossed a frame)
     test_group_commit_exec_throws();
 #endif
+    test_group_commit_lanes();
     if (mode == "sanitize") {  // the Dag Node suite at 1/32 scale on the fake device layer
         g_big /= 32;
         g_leaf = g_leaf / 32 + 14;

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version_and_status_strings():
-    assert rsmi.lib().rsmi_abi_version() == 3
+    assert rsmi.lib().rsmi_abi_version() == 4
     for code in (0, 1, 2, 3, 4, 5, 6, 7, 8, 100, 101, 102):
         assert rsmi.status_string(code) not in ("", "unknown status")
 

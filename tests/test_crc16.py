@@ -485,6 +485,163 @@ def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B, split_by_calle
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,m,B,T,crc", [
+    (10, 4, 262144, 12, True),      # unaligned windows (S = 26215), the fused kernel + its combine launch
+    (10, 4, 262144, 4, True),       # 28 units: the fused kernel with the combine inside
+    (10, 4, 262144, 12, False),     # the plain encode over the table
+    (2, 1, 262144, 6, True),        # aligned rows (S = 131072)
+    (4, 2, 4099, 80, True),         # more blocks than one table holds: two table launches
+    (16, 4, 1048576 + 14, 5, True),
+    (2, 1, 6, 8, True),             # S = 3: no table kernel (rows under 16 bytes), a launch per block
+    (5, 3, 70000, 7, True),         # a shape without table kernels: a launch per block
+])
+def test_coalesced_table_launch(k, m, B, T, crc):
+    """A coalesced group of T requests whose shard buffers are each page-locked (DagNode.Put and
+    degraded Gets from many goroutines, node.go:358-408 / :220-326) is coded by one launch over a
+    table of the blocks' bases (rs_fast_kernel / rs_fused_mfma_kernel TB, up to 64 blocks per
+    launch): one lane and coalesce_us make the T calls one deterministic batch.  Every shard, raw
+    CRC-16 and rebuilt row equals the oracle's, rows not asked for stay untouched, and the
+    BASELINE shapes' batches ran the table kernels."""
+    import ctypes
+    import threading
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    rng = np.random.default_rng(B + T)
+    blocks = [bytes(rng.integers(0, 256, size=B, dtype=np.uint8)) for _ in range(T)]
+    want = []
+    for b in blocks:
+        w = orc.split(k, m, b)
+        w[k:] = orc.encode(k, m, w[:k])
+        want.append(w)
+    ptrs = [L.rsmi_host_alloc(n * S) for _ in range(T)]
+    assert all(ptrs)
+    table = S >= 16 and (k, m) in ((2, 1), (4, 2), (10, 4), (16, 4))
+    try:
+        views = [np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S) for p in ptrs]
+        raws = [(ctypes.c_uint32 * n)() for _ in range(T)]
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_lanes", 1)
+            c.set_option("coalesce_us", 100000)
+            c.set_option("coalesce_max", T)
+            c.warm()
+            b0 = c.stat("coalesced_batches")
+            rcs = [None] * T
+            for t in range(T):
+                flat = views[t].reshape(-1)
+                flat[:] = 0xA5  # stale bytes: padding and parity must be written
+                flat[:B] = np.frombuffer(blocks[t], dtype=np.uint8)
+
+            def enc(t):
+                rcs[t] = L.rsmi_encode_block_coalesced(c._h, ptrs[t], B, ptrs[t], raws[t] if crc else None)
+
+            th = [threading.Thread(target=enc, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert rcs == [0] * T
+            assert c.stat("coalesced_batches") - b0 == 1
+            assert (",TB" in c.last_kernel()) == table, c.last_kernel()
+            for t in range(T):
+                assert np.array_equal(views[t], want[t]), t
+                for r in range(n if crc else 0):
+                    assert rsmi.crc16_entry(b"", raws[t][r], S) == orc.crc16_ibm(want[t][r].tobytes()), (t, r)
+            for lost, data_only in (([0], True), ([1, n - 1] if m >= 2 else [n - 1], False)):
+                present = (ctypes.c_uint8 * n)(*[0 if r in lost else 1 for r in range(n)])
+                for t in range(T):
+                    views[t][:] = want[t]
+                    views[t][lost] = 0xEE
+
+                def rec(t):
+                    rcs[t] = L.rsmi_reconstruct_coalesced(c._h, ptrs[t], S, present, 1 if data_only else 0)
+
+                b0 = c.stat("coalesced_batches")
+                th = [threading.Thread(target=rec, args=(t,)) for t in range(T)]
+                for x in th:
+                    x.start()
+                for x in th:
+                    x.join()
+                assert rcs == [0] * T
+                assert c.stat("coalesced_batches") - b0 == 1
+                if any(r < k or not data_only for r in lost):
+                    assert (",TB" in c.last_kernel()) == table, c.last_kernel()
+                for t in range(T):
+                    for r in range(n):
+                        if r in lost and (r < k or not data_only):
+                            assert np.array_equal(views[t][r], want[t][r]), (t, lost, r)
+                        elif r in lost:
+                            assert (views[t][r] == 0xEE).all(), (t, r)
+                        else:
+                            assert np.array_equal(views[t][r], want[t][r]), (t, r)
+    finally:
+        for p in ptrs:
+            L.rsmi_host_free(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_coalesced_lanes_concurrent_callers(lanes):
+    """Concurrent coalesced encodes with CRC-16s and degraded reconstructs from 24 threads over 1,
+    2 or 4 coalescing lanes (each lane i > 0 a child context with its own stream and scratch):
+    batches on different lanes run at once, and every result equals the oracle's."""
+    import ctypes
+    import threading
+
+    k, m, B = 10, 4, 65536 + 7
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    T, per = 24, 6
+    rng = np.random.default_rng(lanes)
+    blocks = [bytes(rng.integers(0, 256, size=B, dtype=np.uint8)) for _ in range(T * per)]
+    ptrs = [L.rsmi_host_alloc(n * S) for _ in range(T)]
+    assert all(ptrs)
+    errors = []
+    try:
+        views = [np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S) for p in ptrs]
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_lanes", lanes)
+            c.warm()
+            present = (ctypes.c_uint8 * n)(*[0 if r == 3 else 1 for r in range(n)])
+
+            def work(t):
+                raw = (ctypes.c_uint32 * n)()
+                for j in range(per):
+                    i = t * per + j
+                    w = orc.split(k, m, blocks[i])
+                    w[k:] = orc.encode(k, m, w[:k])
+                    flat = views[t].reshape(-1)
+                    flat[:B] = np.frombuffer(blocks[i], dtype=np.uint8)
+                    if L.rsmi_encode_block_coalesced(c._h, ptrs[t], B, ptrs[t], raw):
+                        errors.append(("enc", i))
+                        return
+                    if not np.array_equal(views[t], w):
+                        errors.append(("shards", i))
+                    for r in range(n):
+                        if rsmi.crc16_entry(b"", raw[r], S) != orc.crc16_ibm(w[r].tobytes()):
+                            errors.append(("crc", i, r))
+                    views[t][3] = 0
+                    if L.rsmi_reconstruct_coalesced(c._h, ptrs[t], S, present, 1):
+                        errors.append(("rec", i))
+                        return
+                    if not np.array_equal(views[t], w):
+                        errors.append(("rebuilt", i))
+
+            th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert c.stat("coalesced_calls") == 2 * T * per  # rsmi_warm codes outside the queue
+    finally:
+        for p in ptrs:
+            L.rsmi_host_free(p)
+    assert errors == []
+
+
+@pytest.mark.gpu
 def test_coalesced_host_fault_reports_err_host():
     """A coalesced batch whose executor throws std::bad_alloc (option "inject_host_fault") fails
     its requests with RSMI_ERR_HOST, the status the boundary gives host-resource exceptions

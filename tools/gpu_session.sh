@@ -1,43 +1,90 @@
 #!/bin/bash
-# One GPU session: the GPU test suite, smoke, the headline bench, the side lines (Split
-# layout, fused CRC-16, two ranks without a launcher), a rocprofv3 kernel trace of the
-# headline bench and the FETCH_SIZE / WRITE_SIZE PMC passes.  Each step has its own time
-# limit; the chain stops at the first failure.  Usage: gpu_session.sh [tests|bench|side|prof|all]...
+# One GPU session as a list of legs, run in order; each leg has its own time limit and the chain
+# stops at the first failure (a GPU step that faults, aborts or times out ends the session).
+#
+#   tools/gpu_session.sh OUT leg [leg ...]      results under gpurun_out/OUT/
+#
+# Legs:
+#   tests            the whole GPU suite (pytest -m gpu)
+#   pytest:EXPR      the GPU tests matching -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            the headline bench line (bench.py, defaults)
+#   side             side lines: Split layout, fused CRC-16, configs[4] device group, two ranks
+#   configs          every BASELINE config as a bench line (tools/bench_all_configs.sh)
+#   crcbench         the CRC passes and the fused encode + CRC-16 against the encode
+#   fused_ab         the fused encode + CRC-16, product library against every tools/build/v_* variant
+#   prof             rocprofv3 kernel trace of the headline bench (+ the trace-window cross-check)
+#                    and the FETCH_SIZE / WRITE_SIZE passes (PMC traffic per kernel)
+#   dagnode_suite    the C++ Dag Node suite on the GPU
+#   dagnode_cmp      the Dag Node bench, GPU codec beside the CPU codec (tools/dagnode_cpu_vs_gpu.sh)
+#   latency          per-block call latencies (tools/latency)
+#   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
+#   threads_traced   the same under rocprofv3 --kernel-trace (crash report: tools/latency.cpp)
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$(pwd)
-mkdir -p gpurun_out
+O=gpurun_out/${1:?usage: gpu_session.sh OUT leg...}
+shift
+mkdir -p "$O"
 export TMPDIR=/tmp
-for STEP in "${@:-all}"; do
-if [[ $STEP == all || $STEP == tests ]]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-  tail -3 gpurun_out/pytest_gpu.log
-fi
-if [[ $STEP == all || $STEP == bench ]]; then
-  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
-  timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
-  cat gpurun_out/bench.json
-fi
-if [[ $STEP == all || $STEP == side ]]; then
-  for args in "--layout split" "--fused-crc" "--fused-crc --layout split" "--config rs10_4_1m --layout split" "--config rs16_4_4m --layout split"; do
-    f=gpurun_out/side_$(echo $args | tr -d ' -').json
-    timeout -k 10 300 python bench.py $args --cpu-seconds 0 > $f 2> $f.err || { echo "bench $args failed"; tail -30 $f.err; exit 1; }
+fail() { echo "$1 failed"; tail -40 "$2"; exit 1; }
+for LEG in "$@"; do
+case $LEG in
+tests)
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || fail pytest $O/pytest_gpu.log
+  tail -3 $O/pytest_gpu.log | tee $O/pytest_gpu_tail.txt ;;
+pytest:*)
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${LEG#pytest:}" > $O/pytest_k.log 2>&1 || fail pytest $O/pytest_k.log
+  tail -3 $O/pytest_k.log ;;
+smoke)
+  timeout -k 10 300 python __graft_entry__.py smoke > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+  tail -1 $O/smoke.log ;;
+bench)
+  timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+  cat $O/bench.json ;;
+side)
+  for args in "--layout split" "--fused-crc" "--fused-crc --layout split"; do
+    f=$O/side_$(echo $args | tr -d ' -').json
+    timeout -k 10 300 python bench.py $args --cpu-seconds 0 > $f 2> $f.err || fail "bench $args" $f.err
     cat $f
   done
-  timeout -k 10 300 python bench.py --config rs16_4_4m --copy-inclusive --group 0,0 --cpu-seconds 0 > gpurun_out/side_group.json 2> gpurun_out/side_group.err || { echo "bench --group failed"; tail -30 gpurun_out/side_group.err; exit 1; }
-  cat gpurun_out/side_group.json
-  timeout -k 10 300 python tools/crcbench.py > gpurun_out/crcbench.txt 2>&1 || { echo "crcbench failed"; tail -30 gpurun_out/crcbench.txt; exit 1; }
-  cat gpurun_out/crcbench.txt
-  timeout -k 10 300 python bench.py --gpus 2 --share-device --cpu-seconds 0 > gpurun_out/side_gpus2.json 2> gpurun_out/side_gpus2.err || { echo "bench --gpus 2 failed"; tail -30 gpurun_out/side_gpus2.err; exit 1; }
-  cat gpurun_out/side_gpus2.json
-fi
-if [[ $STEP == all || $STEP == prof ]]; then
-  rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --cpu-seconds 0 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err") || { echo "rocprof failed"; tail -20 gpurun_out/prof.err; exit 1; }
-  python tools/trace_window.py gpurun_out/prof/bench_kernel_trace.csv gpurun_out/prof_bench.json | tee gpurun_out/prof_window.txt
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_fetch.log" 2>&1) || { echo "pmc fetch failed"; tail -20 gpurun_out/pmc_fetch.log; exit 1; }
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/gpurun_out/pmc_write.log" 2>&1) || { echo "pmc write failed"; tail -20 gpurun_out/pmc_write.log; exit 1; }
-  python tools/pmc_summary.py gpurun_out/pmc_fetch/pmc_counter_collection.csv gpurun_out/pmc_write/pmc_counter_collection.csv gpurun_out/pmc_traffic.json
-  bash tools/pmc_layouts.sh || { echo "pmc layouts failed"; exit 1; }
-fi
+  timeout -k 10 300 python bench.py --config rs16_4_4m --copy-inclusive --group 0,0 --cpu-seconds 0 > $O/side_group.json 2> $O/side_group.err || fail "bench --group" $O/side_group.err
+  cat $O/side_group.json
+  timeout -k 10 300 python bench.py --gpus 2 --share-device --cpu-seconds 0 > $O/side_gpus2.json 2> $O/side_gpus2.err || fail "bench --gpus 2" $O/side_gpus2.err
+  cat $O/side_gpus2.json ;;
+configs)
+  timeout -k 10 900 bash tools/bench_all_configs.sh > $O/configs.txt 2>&1 || fail configs $O/configs.txt
+  cp gpurun_out/cfg_*.json $O/ 2>/dev/null; cat $O/configs.txt ;;
+crcbench)
+  timeout -k 10 300 python tools/crcbench.py > $O/crcbench.txt 2>&1 || fail crcbench $O/crcbench.txt
+  cat $O/crcbench.txt ;;
+fused_ab)
+  FUSED_ROUNDS=${FUSED_ROUNDS:-2} timeout -k 10 600 bash tools/fused_ab.sh > $O/fused_ab.txt 2>&1 || fail fused_ab $O/fused_ab.txt
+  cat $O/fused_ab.txt ;;
+prof)
+  rm -rf $O/prof $O/pmc_fetch $O/pmc_write
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o bench -- python3 "$R/bench.py" --cpu-seconds 0 > "$R/$O/prof_bench.json" 2> "$R/$O/prof.err") || fail rocprof $O/prof.err
+  python tools/trace_window.py $O/prof/bench_kernel_trace.csv $O/prof_bench.json | tee $O/prof_window.txt
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/$O/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/$O/pmc_fetch.log" 2>&1) || fail "pmc fetch" $O/pmc_fetch.log
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/$O/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/$O/pmc_write.log" 2>&1) || fail "pmc write" $O/pmc_write.log
+  python tools/pmc_summary.py $O/pmc_fetch/pmc_counter_collection.csv $O/pmc_write/pmc_counter_collection.csv $O/pmc_traffic.json ;;
+dagnode_suite)
+  timeout -k 10 600 ./tests/cpp/build/test_dagnode gpu > $O/test_dagnode_gpu.log 2>&1 || fail test_dagnode $O/test_dagnode_gpu.log
+  grep -E "concurrent|group commit" $O/test_dagnode_gpu.log; tail -1 $O/test_dagnode_gpu.log | tee $O/test_dagnode_gpu_tail.txt ;;
+dagnode_cmp)
+  timeout -k 10 900 bash tools/dagnode_cpu_vs_gpu.sh > $O/dagnode_cpu_vs_gpu.txt 2>&1 || fail "dagnode cmp" $O/dagnode_cpu_vs_gpu.txt
+  cp gpurun_out/dagnode_cmp.jsonl gpurun_out/dn_phases.jsonl $O/
+  grep -v " done$" $O/dagnode_cpu_vs_gpu.txt | head -60 ;;
+latency)
+  timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
+  cat $O/latency.txt ;;
+threads)
+  timeout -k 10 300 ./tools/build/latency --threads > $O/threads.txt 2>&1 || fail threads $O/threads.txt
+  cat $O/threads.txt ;;
+threads_traced)
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/trace" -o t -- "$R/tools/build/latency" --threads > "$R/$O/threads_traced.txt" 2>&1) || fail "traced threads" $O/threads_traced.txt
+  tail -5 $O/threads_traced.txt ;;
+*)
+  echo "unknown leg $LEG"; exit 2 ;;
+esac
 done

@@ -17,6 +17,11 @@
 #include <vector>
 
 #include <emmintrin.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <ucontext.h>
+#include <unistd.h>
 #include <hip/hip_runtime_api.h>
 
 #include "../include/rsmi.h"
@@ -56,14 +61,101 @@ static void copy_nt(uint8_t* dst, const uint8_t* src, size_t n) {
     _mm_sfence();
 }
 
+// ---- crash report: on SIGSEGV/SIGBUS write the faulting address, the PC and
+// every stack frame with the /proc/self/maps line that owns it (library + offset), plus the
+// mappings that end at or begin at the faulting address, then chain to the previous handler
+// (rocprofv3's own stack printer).  Only read(2)/write(2)-level calls on static buffers, apart
+// from backtrace(), which is preloaded at install time.
+static char g_maps[1 << 20];
+static struct sigaction g_prev_segv, g_prev_bus;
+
+static void put_str(const char* s) { (void)!write(2, s, std::strlen(s)); }
+static void put_hex(uintptr_t v) {
+    char b[19] = "0x";
+    for (int i = 0; i < 16; i++) b[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15];
+    b[18] = 0;
+    put_str(b);
+}
+static uintptr_t parse_hex(const char*& p) {
+    uintptr_t v = 0;
+    for (;; p++) {
+        const char ch = *p;
+        if (ch >= '0' && ch <= '9') v = v * 16 + uintptr_t(ch - '0');
+        else if (ch >= 'a' && ch <= 'f') v = v * 16 + uintptr_t(ch - 'a' + 10);
+        else break;
+    }
+    return v;
+}
+// the maps line containing a (or, with edge, the lines ending or starting exactly at a)
+static void describe(const char* what, uintptr_t a, bool edge) {
+    put_str(what);
+    put_hex(a);
+    bool found = false;
+    for (const char* line = g_maps; *line;) {
+        const char* eol = line;
+        while (*eol && *eol != '\n') eol++;
+        const char* p = line;
+        const uintptr_t lo = parse_hex(p);
+        p++;
+        const uintptr_t hi = parse_hex(p);
+        const bool in = a >= lo && a < hi, at_edge = edge && (hi == a || lo == a);
+        if (in || at_edge) {
+            put_str(in ? "  in  [+" : (hi == a ? "  ends at it: [" : "  starts at it: ["));
+            put_hex(in ? a - lo : 0);
+            put_str("] ");
+            (void)!write(2, line, size_t(eol - line));
+            found = true;
+        }
+        line = *eol ? eol + 1 : eol;
+    }
+    if (!found) put_str("  (no mapping)");
+    put_str("\n");
+}
+static void crash_handler(int sig, siginfo_t* si, void* uc) {
+    size_t len = 0;
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        for (ssize_t r; len + 1 < sizeof g_maps && (r = read(fd, g_maps + len, sizeof g_maps - 1 - len)) > 0;)
+            len += size_t(r);
+        close(fd);
+    }
+    g_maps[len] = 0;
+    put_str(sig == SIGSEGV ? "\n=== latency: SIGSEGV ===\n" : "\n=== latency: SIGBUS ===\n");
+    describe("fault address ", reinterpret_cast<uintptr_t>(si->si_addr), true);
+    const auto* ctx = static_cast<const ucontext_t*>(uc);
+    describe("pc            ", uintptr_t(ctx->uc_mcontext.gregs[REG_RIP]), false);
+    void* frames[64];
+    const int nf = backtrace(frames, 64);
+    for (int i = 0; i < nf; i++) describe("frame         ", reinterpret_cast<uintptr_t>(frames[i]), false);
+    put_str("=== /proc/self/maps ===\n");
+    (void)!write(2, g_maps, len);
+    put_str("=== end ===\n");
+    const struct sigaction& prev = sig == SIGSEGV ? g_prev_segv : g_prev_bus;
+    sigaction(sig, &prev, nullptr);  // chain: the previous handler, or the default action
+    raise(sig);
+}
+static void install_crash_handler() {
+    void* warm[1];
+    (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
+    struct sigaction sa {};
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+}
+
 // T threads, each coding `calls` blocks of B bytes through rsmi_encode_block_coalesced_crcs, in
 // place in its own page-locked buffer (block == shards_out, Split by the thread): the coalesced
 // groups' throughput, GiB/s of block payload, and how many groups they formed
-static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1) {
-    // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes)
+static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2) {
+    // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes);
+    // clanes: each context's coalescing lanes (option "coalesce_lanes")
     std::vector<rsmi_ctx*> cs(static_cast<size_t>(lanes));
-    for (auto& x : cs)
+    for (auto& x : cs) {
         if (rsmi_open(k, m, 0, &x) != RSMI_OK) std::exit(2);
+        if (rsmi_set_option(x, "coalesce_lanes", clanes) != RSMI_OK || rsmi_warm(x) != RSMI_OK) std::exit(2);
+    }
     rsmi_ctx* c = cs[0];
     const size_t n = size_t(k + m), S = rsmi_shard_size(B, k);
     std::vector<uint8_t*> bufs(static_cast<size_t>(T));
@@ -97,21 +189,25 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
     run();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     const long calls_n = stat("coalesced_calls") - c0, batches = stat("coalesced_batches") - b0;
-    std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s): %7.2f GiB/s, "
-                "%ld calls in %ld groups (last kernel %s)\n", k, m, B, T, calls, lanes,
-                double(T) * calls * B / sec / 1073741824.0, calls_n, batches, rsmi_last_kernel(c));
+    std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s) x %d lane(s): "
+                "%7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls, lanes, clanes,
+                double(T) * calls * B / sec / 1073741824.0, calls_n, batches, double(batches) / double(calls_n),
+                rsmi_last_kernel(c));
     for (auto* p : bufs) rsmi_host_free(p);
     for (auto* x : cs) rsmi_close(x);
 }
 
 int main(int argc, char** argv) {
+    install_crash_handler();
     if (argc > 1 && !std::strcmp(argv[1], "--threads")) {
-        for (int lanes : {1, 4, 8, 16})
+        // one context with 1, 2 or 4 coalescing lanes (one queue), and round 4's spread over 4
+        // contexts of one lane each
+        for (auto cfg : {std::make_pair(1, 1), std::make_pair(1, 2), std::make_pair(1, 4), std::make_pair(4, 1)})
             for (int T : {4, 16})
                 for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
                                    std::make_tuple(16, 4, size_t(4194304))})
                     coalesced_threads(std::get<0>(shape), std::get<1>(shape), std::get<2>(shape), T,
-                                      std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, lanes);
+                                      std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, cfg.first, cfg.second);
         return 0;
     }
     const int k = 10, m = 4, n = k + m;
