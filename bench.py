@@ -376,6 +376,16 @@ def load_traffic(label):
         return None
 
 
+def load_trace_window(label):
+    """The kernel's average duration (ms) over the timed window of the committed rocprofv3 kernel
+    trace of this same command (tools/trace_window.py -> profiles/trace_window.json)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "trace_window.json")) as f:
+            return json.load(f).get(label)
+    except Exception:
+        return None
+
+
 def copy_inclusive(codec, k, m, S, nb, lost, data_only, world, group=None):
     """Host-resident encode(+reconstruct) through page-locked buffers (the zero-copy direct
     path).  Every rank runs each leg at the same time, so the aggregate shows
@@ -705,6 +715,12 @@ def main():
             "avg_launch_ms": round(enc_ms, 4),
             "median_launch_ms": round(enc_t[len(enc_t) // 2], 4),
             "launches_timed": len(enc_t),
+            "timing": ("avg_launch_ms / achieved: HIP events on the kernels' stream around each kernel of every "
+                       f"{a.event_every}th step, event-inflated (~3 %: the encode and reconstruct averages sum to more "
+                       "than ms_per_step, which is timed without events); trace_window_avg_ms: the same kernel's "
+                       "average over the timed window of the committed rocprofv3 kernel trace of this command "
+                       "(profiles/trace_window.json, tools/gpu_session.sh prof), not measured in this run"),
+            "trace_window_avg_ms": load_trace_window(enc_kernel) if headline else None,
             "per_rank_frac": {"min": round(min(fr), 4), "max": round(max(fr), 4),
                               "mean": round(sum(fr) / len(fr), 4)},
         },
@@ -720,6 +736,7 @@ def main():
             "frac": round(rec_gbs / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_launch": rec_bytes,
             "avg_launch_ms": round(rec_ms, 4),
+            "trace_window_avg_ms": load_trace_window(rec_kernel) if headline else None,
         }
     if a.copy_inclusive:
         group = None

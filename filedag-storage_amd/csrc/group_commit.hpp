@@ -9,7 +9,9 @@
 // (0 .. lanes-1, distinct among the batches executing), so one batch can be launched while the
 // one before it is still coded; requests that arrive while every lane is busy form the next
 // batch.  A lone caller never waits: its batch is itself.  Req needs a `bool done` member, false
-// on submission, and an `int rc`.  If exec throws (std::bad_alloc from its own vectors), every
+// on submission, and an `int rc`.  An executor may go on to up to `carry` further batches queued
+// by the time its own completes (its caller returns that much later; no thread hand-off per
+// batch).  If exec throws (std::bad_alloc from its own vectors), every
 // request of the batch completes with rc = the fail code given at construction and the lane is
 // released, so no current or later caller waits forever; the exception does not cross the C-ABI.
 #pragma once
@@ -28,8 +30,9 @@ class GroupCommit {
 public:
     static constexpr int kMaxLanes = 32;
     explicit GroupCommit(int fail_rc) : fail_rc_(fail_rc) {}
+    // carry: batches a lane runs after its own before it hands over (0: hand over at once)
     template <class Exec>
-    void submit(Req& req, size_t cap, long wait_us, int lanes, Exec&& exec) {
+    void submit(Req& req, size_t cap, long wait_us, int lanes, Exec&& exec, int carry = 0) {
         calls_++;
         lanes = std::min(std::max(lanes, 1), kMaxLanes);
         cap = std::max<size_t>(cap, 1);
@@ -50,29 +53,35 @@ public:
             executing_++;
             if (wait_us > 0 && pending_.size() < cap)
                 cv_.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return pending_.size() >= cap; });
-            const size_t take = std::min(cap, pending_.size());
-            std::vector<Req*> batch;
-            try {
-                batch.assign(pending_.begin(), pending_.begin() + take);
-            } catch (...) {  // no memory for the batch list: fail these requests in place
-                for (size_t i = 0; i < take; i++) {
-                    pending_[i]->rc = fail_rc_;
-                    pending_[i]->done = true;
+            // the batch that holds this caller's request, then up to `carry` more on the same lane
+            // when requests are queued by then: the lane goes straight on to them instead of
+            // waking a waiting caller to take them (a thread hand-off per batch)
+            for (int round = 0; round <= carry && !pending_.empty(); round++) {
+                const size_t take = std::min(cap, pending_.size());
+                std::vector<Req*> batch;
+                try {
+                    batch.assign(pending_.begin(), pending_.begin() + take);
+                } catch (...) {  // no memory for the batch list: fail these requests in place
+                    for (size_t i = 0; i < take; i++) {
+                        pending_[i]->rc = fail_rc_;
+                        pending_[i]->done = true;
+                    }
+                    pending_.erase(pending_.begin(), pending_.begin() + take);
+                    cv_.notify_all();
+                    break;
                 }
                 pending_.erase(pending_.begin(), pending_.begin() + take);
-                release(lane);
-                continue;
+                lk.unlock();
+                try {
+                    exec(batch, lane);
+                } catch (...) {
+                    for (Req* r : batch) r->rc = fail_rc_;
+                }
+                batches_++;
+                lk.lock();
+                for (Req* r : batch) r->done = true;
+                cv_.notify_all();  // this batch's callers return now, whatever the lane does next
             }
-            pending_.erase(pending_.begin(), pending_.begin() + take);
-            lk.unlock();
-            try {
-                exec(batch, lane);
-            } catch (...) {
-                for (Req* r : batch) r->rc = fail_rc_;
-            }
-            batches_++;
-            lk.lock();
-            for (Req* r : batch) r->done = true;
             release(lane);
         }
     }

@@ -76,15 +76,26 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         uint32_t* d16 = want16 ? reinterpret_cast<uint32_t*>(c->d_crc) : nullptr;
         uint32_t* d32 = want32 ? reinterpret_cast<uint32_t*>(c->d_crc32) : nullptr;
         // the table form: in / out are offsets from each block's base ([k data | m parity] at
-        // pitch S for encode, n rows in place for reconstruct); the CRC-32 keeps a launch per block
+        // pitch S for encode, n rows in place for reconstruct); the CRC-32 keeps a launch per block.
+        // The fused kernel's combine writes each R(shard) once, so the table launches store them
+        // straight into the page-locked read-back area (no read-back kernel after them)
         bool table = nb > 1 && !want32;
+        uint32_t* h16 = nullptr;  // the table launches' R(shard): host view, and its device alias
+        uint32_t* h16_dev = nullptr;
+        if (table && want16) {
+            uint8_t* h = raw_area(c, nb * n * 4);
+            if (!h) return RSMI_ERR_DEVICE;
+            h16 = reinterpret_cast<uint32_t*>(h);
+            h16_dev = reinterpret_cast<uint32_t*>(host_alias(h, nb * n * 4));
+            if (!h16_dev) return RSMI_ERR_DEVICE;
+        }
         for (size_t j0 = 0; j0 < nb && table; j0 += size_t(kTableBlocks)) {
             const size_t cnt = std::min(size_t(kTableBlocks), nb - j0);
             BlockBases tb;
             for (size_t i = 0; i < cnt; i++) tb.b[i] = uint64_t(reinterpret_cast<uintptr_t>(dev[j0 + i]));
             uint8_t* const par = reinterpret_cast<uint8_t*>(uintptr_t(k * S));  // offset of the parity rows
             if (enc && want16)
-                rc = launch_plan_crc(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, d16 + j0 * n, st, &tb);
+                rc = launch_plan_crc(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, h16_dev + j0 * n, st, &tb);
             else if (enc)
                 rc = launch_plan(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, st, nullptr, &tb);
             else
@@ -96,6 +107,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             if (rc) return fail(rc);
             launched = true;
         }
+        if (!table) h16 = nullptr;  // a launch per request: its R(shard) come back by read-back
         for (size_t j = 0; j < nb && !table; j++) {
             if (enc)
                 rc = launch_encode_rows(c, *plan, dev[j], n * S, dev[j] + k * S, n * S, S, 1, d16 ? d16 + j * n : nullptr,
@@ -105,11 +117,11 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             if (rc) return fail(rc);
             launched = true;
         }
-        const uint32_t *h16, *h32;
-        if ((rc = readback(c, d16, d32, nb * n * 4, st, h16, h32))) return fail(rc);
+        const uint32_t *g16 = h16, *g32 = nullptr;
+        if (!h16 && (rc = readback(c, d16, d32, nb * n * 4, st, g16, g32))) return fail(rc);
         HIP_TRY(hipStreamSynchronize(st));
-        if (want16) std::memcpy(r16.data(), h16, nb * n * 4);
-        if (want32) std::memcpy(r32.data(), h32, nb * n * 4);
+        if (want16) std::memcpy(r16.data(), g16, nb * n * 4);
+        if (want32) std::memcpy(r32.data(), g32, nb * n * 4);
     }
     for (size_t j = 0; j < nb; j++) {
         if (rq[j]->raw) std::memcpy(rq[j]->raw, r16.data() + j * n, n * 4);
@@ -238,7 +250,8 @@ int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
     int rc = ensure_device_fast(c);
     if (rc) return rc;
     c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us, int(c->opt_coalesce_lanes),
-                   [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { run_coalesced(c, lane, batch); });
+                   [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { run_coalesced(c, lane, batch); },
+                   int(c->opt_coalesce_carry));
     return req.rc;
 }
 

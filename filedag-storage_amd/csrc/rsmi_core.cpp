@@ -492,6 +492,9 @@ int apply_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "coalesce_lanes")) {
         if (value < 1 || value > 16) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_lanes = value;
+    } else if (!std::strcmp(key, "coalesce_carry")) {
+        if (value < 0 || value > 16) return RSMI_ERR_INVALID_ARG;
+        c->opt_coalesce_carry = value;
     } else {
         return RSMI_ERR_INVALID_ARG;
     }

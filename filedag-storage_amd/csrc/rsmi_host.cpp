@@ -79,18 +79,28 @@ uint8_t* small_stage(rsmi_ctx* c, size_t need) {
 // kernel per buffer into the context's page-locked read-back area, in stream order, so they
 // arrive with the call's own stream synchronisation instead of a blocking hipMemcpy after it (a second
 // round trip).  h16 / h32 are where they land; read them after that synchronisation.
+// The context's page-locked read-back area, at least `bytes` long (caller holds ctx->mu, and no
+// kernel of an earlier call still writes it: every call synchronises before it returns).
+uint8_t* raw_area(rsmi_ctx* c, size_t bytes) {
+    if (c->h_raw_cap < bytes) {
+        if (c->h_raw) (void)hipHostFree(c->h_raw);
+        c->h_raw = nullptr;
+        c->h_raw_cap = 0;
+        const size_t cap = std::max<size_t>(bytes, 64 << 10);
+        if (pinned_alloc(reinterpret_cast<void**>(&c->h_raw), cap) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        c->h_raw_cap = cap;
+    }
+    return c->h_raw;
+}
+
 int readback(rsmi_ctx* c, const uint32_t* d16, const uint32_t* d32, size_t sz, hipStream_t st, const uint32_t*& h16,
              const uint32_t*& h32) {
     h16 = h32 = nullptr;
     if (!sz || (!d16 && !d32)) return RSMI_OK;
-    if (c->h_raw_cap < 2 * sz) {
-        if (c->h_raw) (void)hipHostFree(c->h_raw);
-        c->h_raw = nullptr;
-        c->h_raw_cap = 0;
-        const size_t cap = std::max<size_t>(2 * sz, 64 << 10);
-        HIP_TRY(pinned_alloc(reinterpret_cast<void**>(&c->h_raw), cap));
-        c->h_raw_cap = cap;
-    }
+    if (!raw_area(c, 2 * sz)) return RSMI_ERR_DEVICE;
     uint8_t* dev = host_alias(c->h_raw, 2 * sz);
     if (!dev) return RSMI_ERR_DEVICE;
     int rc;

@@ -147,6 +147,7 @@ struct rsmi_ctx {
     // i > 0 the child context lanes[i - 1] (same k, m, device and options; opened on first use), so
     // one batch can be coded while the next is launched and the callers' queue stays one queue
     long opt_coalesce_lanes = 2;
+    long opt_coalesce_carry = 1;  // batches a lane runs after its own before handing over (group_commit.hpp)
     std::vector<rsmi_ctx*> lanes;
     std::mutex lanes_mu;
 };
@@ -192,6 +193,7 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
             hipStream_t stream);
 uint8_t* host_alias(void* p, size_t len);
 uint8_t* small_stage(rsmi_ctx* c, size_t need);
+uint8_t* raw_area(rsmi_ctx* c, size_t bytes);
 int readback(rsmi_ctx* c, const uint32_t* d16, const uint32_t* d32, size_t sz, hipStream_t st, const uint32_t*& h16,
              const uint32_t*& h32);
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,

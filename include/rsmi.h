@@ -363,7 +363,9 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
  * next N coalesced batches throw std::bad_alloc in the executor, so their requests return
  * RSMI_ERR_HOST; default 0), "coalesce_lanes" (coalesced batches coded at once, 1-16, default
- * 2; every option but the test hook also applies to the lanes' child contexts).  Kernel variants measured slower than the defaults are not
+ * 2; every option but the test hook also applies to the lanes' child contexts), "coalesce_carry"
+ * (batches a lane's executor goes on to when they are queued by the time its own completes,
+ * before it hands the lane to a waiting caller, 0-16, default 1).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);

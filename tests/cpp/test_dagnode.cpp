@@ -827,7 +827,8 @@ static void test_group_commit_exec_throws() {
     CHECK(last.done && last.rc == 100);
 }
 
-// group_commit.hpp with several lanes: at most `lanes` batches execute at once, the batches
+// group_commit.hpp with several lanes (and lanes that carry on to queued batches): at most
+// `lanes` batches execute at once, the batches
 // executing at once hold distinct lane ids, every request completes exactly once with its own
 // result, and the calls group (fewer batches than calls when callers pile up behind busy lanes).
 static void test_group_commit_lanes() {
@@ -835,7 +836,8 @@ static void test_group_commit_lanes() {
         int id = 0, rc = -1;
         bool done = false;
     };
-    for (int lanes : {1, 2, 3}) {
+    for (int lanes : {1, 2, 3})
+    for (int carry : {0, 2}) {
         rsmi::GroupCommit<Req> gc(-7);
         std::atomic<int> running{0}, peak{0}, overlap{0};
         std::atomic<uint32_t> busy{0};
@@ -861,7 +863,7 @@ static void test_group_commit_lanes() {
             th.emplace_back([&, t] {
                 for (int i = t; i < T * per; i += T) {
                     reqs[size_t(i)].id = i;
-                    gc.submit(reqs[size_t(i)], 256, 0, lanes, exec);
+                    gc.submit(reqs[size_t(i)], 256, 0, lanes, exec, carry);
                 }
             });
         for (auto& x : th) x.join();
@@ -870,8 +872,8 @@ static void test_group_commit_lanes() {
         CHECK(peak.load() >= 1 && peak.load() <= lanes);
         CHECK(executed.load() == T * per && gc.calls() == uint64_t(T * per));
         CHECK(gc.batches() < gc.calls());
-        std::printf("group commit, %d lane(s): %llu calls in %llu batches, at most %d at once\n", lanes,
-                    (unsigned long long)gc.calls(), (unsigned long long)gc.batches(), peak.load());
+        std::printf("group commit, %d lane(s), carry %d: %llu calls in %llu batches, at most %d at once\n", lanes,
+                    carry, (unsigned long long)gc.calls(), (unsigned long long)gc.batches(), peak.load());
     }
 }
 

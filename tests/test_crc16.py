@@ -966,6 +966,57 @@ def test_fused_mfma_counts_exact(k, m, fill):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nb", [2, 64])
+def test_encode_batch_dev_crc_concurrent_streams(nb):
+    """Two threads call rsmi_encode_batch_dev_crc on one context, each on its own stream, over and
+    over (the fused kernel's unit records and the inline combine's counters used to be
+    one per context, so kernels of the two streams could share them).  Each stream now has its
+    own scratch; every parity row and R(shard) equals the oracle's.  nb = 2: small launches, the
+    combine inside the kernel (its counters); nb = 64: the separate combine."""
+    import threading
+
+    import torch
+
+    k, m, S = 10, 4, 26215
+    n = k + m
+    rs = rsmi.recommended_pitch(S)
+    errors = []
+    with rsmi.Codec(k, m) as c:
+        def work(seed):
+            st = torch.cuda.Stream()
+            data = np.random.default_rng(seed).integers(0, 256, size=(nb, k, S), dtype=np.uint8)
+            host = np.zeros((nb, n, rs), dtype=np.uint8)
+            host[:, :k, :S] = data
+            want = orc.encode_fast(k, m, data)
+            with torch.cuda.stream(st):
+                d = torch.from_numpy(host.reshape(-1).copy()).cuda()
+                raw = torch.zeros((nb, n), dtype=torch.int32, device="cuda")
+                for _ in range(20):
+                    raw.zero_()
+                    d.view(nb, n, rs)[:, k:, :] = 0
+                    c.encode_batch_dev_crc(d.data_ptr(), rs, n * rs, d.data_ptr() + k * rs, rs, n * rs, S, nb,
+                                           raw.data_ptr(), st.cuda_stream)
+                    got = d.view(nb, n, rs)[:, k:, :S].cpu().numpy()
+                    r = raw.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+                    if not np.array_equal(got, want):
+                        errors.append(("parity", seed))
+                        return
+                    for b in (0, nb - 1):
+                        rows = list(data[b]) + list(want[b])
+                        for i in range(n):
+                            if rsmi.crc16_entry(b"", int(r[b, i]), S) != orc.crc16_ibm(rows[i].tobytes()):
+                                errors.append(("crc", seed, b, i))
+                                return
+
+        th = [threading.Thread(target=work, args=(s,)) for s in (1, 2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert errors == []
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m", [(10, 4), (16, 4), (2, 1), (5, 3)])
 @pytest.mark.parametrize("mis", [0, 1, 3])
 def test_fused_mfma_split_every_tail(k, m, mis):

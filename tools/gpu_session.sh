@@ -64,7 +64,7 @@ fused_ab)
 prof)
   rm -rf $O/prof $O/pmc_fetch $O/pmc_write
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o bench -- python3 "$R/bench.py" --cpu-seconds 0 > "$R/$O/prof_bench.json" 2> "$R/$O/prof.err") || fail rocprof $O/prof.err
-  python tools/trace_window.py $O/prof/bench_kernel_trace.csv $O/prof_bench.json | tee $O/prof_window.txt
+  python tools/trace_window.py $O/prof/bench_kernel_trace.csv $O/prof_bench.json $O/trace_window.json | tee $O/prof_window.txt
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/$O/pmc_fetch" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/$O/pmc_fetch.log" 2>&1) || fail "pmc fetch" $O/pmc_fetch.log
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/$O/pmc_write" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 > "$R/$O/pmc_write.log" 2>&1) || fail "pmc write" $O/pmc_write.log
   python tools/pmc_summary.py $O/pmc_fetch/pmc_counter_collection.csv $O/pmc_write/pmc_counter_collection.csv $O/pmc_traffic.json ;;

@@ -148,13 +148,15 @@ static void install_crash_handler() {
 // T threads, each coding `calls` blocks of B bytes through rsmi_encode_block_coalesced_crcs, in
 // place in its own page-locked buffer (block == shards_out, Split by the thread): the coalesced
 // groups' throughput, GiB/s of block payload, and how many groups they formed
-static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2) {
+static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2, int carry = 1) {
     // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes);
     // clanes: each context's coalescing lanes (option "coalesce_lanes")
     std::vector<rsmi_ctx*> cs(static_cast<size_t>(lanes));
     for (auto& x : cs) {
         if (rsmi_open(k, m, 0, &x) != RSMI_OK) std::exit(2);
-        if (rsmi_set_option(x, "coalesce_lanes", clanes) != RSMI_OK || rsmi_warm(x) != RSMI_OK) std::exit(2);
+        if (rsmi_set_option(x, "coalesce_lanes", clanes) != RSMI_OK || rsmi_set_option(x, "coalesce_carry", carry) != RSMI_OK ||
+            rsmi_warm(x) != RSMI_OK)
+            std::exit(2);
     }
     rsmi_ctx* c = cs[0];
     const size_t n = size_t(k + m), S = rsmi_shard_size(B, k);
@@ -189,8 +191,8 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
     run();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     const long calls_n = stat("coalesced_calls") - c0, batches = stat("coalesced_batches") - b0;
-    std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s) x %d lane(s): "
-                "%7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls, lanes, clanes,
+    std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s) x %d lane(s), "
+                "carry %d: %7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls, lanes, clanes, carry,
                 double(T) * calls * B / sec / 1073741824.0, calls_n, batches, double(batches) / double(calls_n),
                 rsmi_last_kernel(c));
     for (auto* p : bufs) rsmi_host_free(p);
@@ -202,12 +204,15 @@ int main(int argc, char** argv) {
     if (argc > 1 && !std::strcmp(argv[1], "--threads")) {
         // one context with 1, 2 or 4 coalescing lanes (one queue), and round 4's spread over 4
         // contexts of one lane each
-        for (auto cfg : {std::make_pair(1, 1), std::make_pair(1, 2), std::make_pair(1, 4), std::make_pair(4, 1)})
+        // (contexts, lanes, carry)
+        for (auto cfg : {std::make_tuple(1, 1, 0), std::make_tuple(1, 1, 1), std::make_tuple(1, 2, 0),
+                         std::make_tuple(1, 2, 1), std::make_tuple(1, 4, 1), std::make_tuple(4, 1, 0)})
             for (int T : {4, 16})
                 for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
                                    std::make_tuple(16, 4, size_t(4194304))})
                     coalesced_threads(std::get<0>(shape), std::get<1>(shape), std::get<2>(shape), T,
-                                      std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, cfg.first, cfg.second);
+                                      std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, std::get<0>(cfg),
+                                      std::get<1>(cfg), std::get<2>(cfg));
         return 0;
     }
     const int k = 10, m = 4, n = k + m;

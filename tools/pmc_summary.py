@@ -18,10 +18,11 @@ def label(name):
     UA, CRC> -> rs_fast_kernel<K=..,MT=..,NT=..>[,UA][,CRC]); every other rsmi:: kernel (the fused
     matrix-core encode + CRC-16, the combine kernels, the rows passes, repitch) by its name and
     template arguments; None for kernels outside the library (torch's generators)."""
-    m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", name)
+    m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)(?:, (true|false))?>", name)
     if m:
         return f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (
-            ",UA" if m.group(5) == "true" else "") + (",CRC" if m.group(6) == "true" else "")
+            ",UA" if m.group(5) == "true" else "") + (",CRC" if m.group(6) == "true" else "") + (
+            ",TB" if m.group(7) == "true" else "")
     m = re.search(r"rsmi::(\w+)(<[^>]*>)?", name)
     if not m:
         return None

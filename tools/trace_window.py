@@ -4,8 +4,10 @@
 bench.py launches the encode (and reconstruct) kernel once per step; the timed window is
 the `steps` dispatches of each kernel after the settle steps, the warmup steps and one
 label probe (the sustained run and the self check come after it).
-Usage: trace_window.py <kernel_trace.csv> <bench.json>
-Prints, per kernel, the window average next to bench.py's own HIP-event average.
+Usage: trace_window.py <kernel_trace.csv> <bench.json> [out.json]
+Prints, per kernel, the window average next to bench.py's own HIP-event average; out.json gets
+{kernel label: window average in ms} (profiles/trace_window.json, which bench.py's roofline
+block carries beside its event-timed figures).
 """
 import csv
 import json
@@ -21,7 +23,7 @@ def main():
     first = bench["config"]["settle"]["steps"] + bench["warmup"] + 1
     per = {}
     for r in rows:
-        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", r["Kernel_Name"])
+        m = re.search(r"rs_fast_kernel<(\d+), (\d+), (\d+), (\d+), (true|false), (true|false)(?:, (true|false))?>", r["Kernel_Name"])
         if not m:
             continue
         key = f"rs_fast_kernel<K={m.group(1)},MT={m.group(2)},NT={m.group(3)}>" + (",UA" if m.group(5) == "true" else "") + (
@@ -34,6 +36,7 @@ def main():
     # bench.py times every `every`-th step with HIP events (round 3; every step before)
     timed = bench["roofline"].get("launches_timed", steps)
     every = -(-steps // timed)
+    summary = {}
     for k, d in per.items():
         w = d[first:first + steps]
         avg = sum(w) / len(w)
@@ -44,6 +47,10 @@ def main():
                  f"({(e / avs - 1) * 100:+.1f} %)") if e else ""
         print(f"{k}: {len(d)} dispatches, timed window ({len(w)} steps) avg {avg:.1f} us, "
               f"min {min(w):.1f}, max {max(w):.1f}{extra}")
+        summary[k] = round(avg / 1e3, 4)
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as f:
+            json.dump(summary, f, indent=1)
 
 
 if __name__ == "__main__":
