@@ -87,6 +87,14 @@ struct CrcScratch {
     size_t fctr_cap = 0;
 };
 
+// defaults of options "coalesce_lanes" / "coalesce_carry" (build macros for A/B library variants)
+#ifndef RSMI_COALESCE_LANES
+#define RSMI_COALESCE_LANES 2
+#endif
+#ifndef RSMI_COALESCE_CARRY
+#define RSMI_COALESCE_CARRY 1
+#endif
+
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0, device = 0;
     rsmi::Matrix M;  // n x k
@@ -146,8 +154,8 @@ struct rsmi_ctx {
     // Coalesced batches run on up to opt_coalesce_lanes lanes at once: lane 0 is this context, lane
     // i > 0 the child context lanes[i - 1] (same k, m, device and options; opened on first use), so
     // one batch can be coded while the next is launched and the callers' queue stays one queue
-    long opt_coalesce_lanes = 2;
-    long opt_coalesce_carry = 1;  // batches a lane runs after its own before handing over (group_commit.hpp)
+    long opt_coalesce_lanes = RSMI_COALESCE_LANES;
+    long opt_coalesce_carry = RSMI_COALESCE_CARRY;  // batches a lane runs after its own before handing over (group_commit.hpp)
     std::vector<rsmi_ctx*> lanes;
     std::mutex lanes_mu;
 };

@@ -299,9 +299,10 @@ int main(int argc, char** argv) {
 #endif
     std::printf("\"k\": %d, \"m\": %d, \"B\": %zu, \"N\": %d, \"put\": %.3f, \"putmany\": %.3f, \"put_threads\": %.3f, "
                 "\"get\": %.3f, \"getmany\": %.3f, \"get_threads\": %.3f, \"repair\": %.3f, \"repair_batched\": %.3f, "
-                "\"put_nolone\": %.3f, \"get_nolone\": %.3f, \"repair_nolone\": %.3f}\n",
+                "\"put_nolone\": %.3f, \"get_nolone\": %.3f, \"repair_nolone\": %.3f, \"put_threads_calls\": %ld, "
+                "\"put_threads_batches\": %ld, \"get_threads_calls\": %ld, \"get_threads_batches\": %ld}\n",
                 k, m, B, N, gib / put1, gib / putb, gib / putT, gib / get1, gib / getb, gib / getT, gib / rep1, gib / repb,
-                gib / put1n, gib / get1n, gib / rep1n);
+                gib / put1n, gib / get1n, gib / rep1n, calls, batches, gcalls, gbatches);
 #ifdef FAKE_RSMI_FAST
     std::printf("PHASES {\"codec\": \"cpu\", \"k\": %d, \"m\": %d, \"B\": %zu, %s}\n", k, m, B, phases.c_str());
 #else

@@ -17,8 +17,10 @@
 #                    and the FETCH_SIZE / WRITE_SIZE passes (PMC traffic per kernel)
 #   dagnode_suite    the C++ Dag Node suite on the GPU
 #   dagnode_cmp      the Dag Node bench, GPU codec beside the CPU codec (tools/dagnode_cpu_vs_gpu.sh)
+#   dagnode_ab       the Dag Node bench (GPU codec) on the product library and every tools/build/v_* variant
 #   latency          per-block call latencies (tools/latency)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
+#   group_sweep      one thread, in-place host calls of 1..256 blocks back to back (tools/latency --group-sweep)
 #   threads_traced   the same under rocprofv3 --kernel-trace (crash report: tools/latency.cpp)
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -75,12 +77,18 @@ dagnode_cmp)
   timeout -k 10 900 bash tools/dagnode_cpu_vs_gpu.sh > $O/dagnode_cpu_vs_gpu.txt 2>&1 || fail "dagnode cmp" $O/dagnode_cpu_vs_gpu.txt
   cp gpurun_out/dagnode_cmp.jsonl gpurun_out/dn_phases.jsonl $O/
   grep -v " done$" $O/dagnode_cpu_vs_gpu.txt | head -60 ;;
+dagnode_ab)
+  DN_OUT=$O/dagnode_ab.jsonl timeout -k 10 1000 bash tools/dagnode_ab.sh > $O/dagnode_ab.txt 2>&1 || fail "dagnode ab" $O/dagnode_ab.txt
+  grep -v " done$" $O/dagnode_ab.txt ;;
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
 threads)
   timeout -k 10 300 ./tools/build/latency --threads > $O/threads.txt 2>&1 || fail threads $O/threads.txt
   cat $O/threads.txt ;;
+group_sweep)
+  timeout -k 10 300 ./tools/build/latency --group-sweep > $O/group_sweep.txt 2>&1 || fail group_sweep $O/group_sweep.txt
+  cat $O/group_sweep.txt ;;
 threads_traced)
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/trace" -o t -- "$R/tools/build/latency" --threads > "$R/$O/threads_traced.txt" 2>&1) || fail "traced threads" $O/threads_traced.txt
   tail -5 $O/threads_traced.txt ;;

@@ -148,14 +148,15 @@ static void install_crash_handler() {
 // T threads, each coding `calls` blocks of B bytes through rsmi_encode_block_coalesced_crcs, in
 // place in its own page-locked buffer (block == shards_out, Split by the thread): the coalesced
 // groups' throughput, GiB/s of block payload, and how many groups they formed
-static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2, int carry = 1) {
+static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2, int carry = 1,
+                              int wait_us = 0, bool nt = false) {
     // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes);
     // clanes: each context's coalescing lanes (option "coalesce_lanes")
     std::vector<rsmi_ctx*> cs(static_cast<size_t>(lanes));
     for (auto& x : cs) {
         if (rsmi_open(k, m, 0, &x) != RSMI_OK) std::exit(2);
         if (rsmi_set_option(x, "coalesce_lanes", clanes) != RSMI_OK || rsmi_set_option(x, "coalesce_carry", carry) != RSMI_OK ||
-            rsmi_warm(x) != RSMI_OK)
+            rsmi_set_option(x, "coalesce_us", wait_us) != RSMI_OK || rsmi_warm(x) != RSMI_OK)
             std::exit(2);
     }
     rsmi_ctx* c = cs[0];
@@ -172,7 +173,8 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
             th.emplace_back([&, t] {
                 std::vector<uint32_t> raw(n);
                 for (int i = 0; i < calls; i++) {
-                    std::memcpy(bufs[size_t(t)], blocks[size_t(t)].data(), B);
+                    if (nt) copy_nt(bufs[size_t(t)], blocks[size_t(t)].data(), B);
+                    else std::memcpy(bufs[size_t(t)], blocks[size_t(t)].data(), B);
                     if (rsmi_encode_block_coalesced_crcs(cs[size_t(t % lanes)], bufs[size_t(t)], B, bufs[size_t(t)],
                                                          raw.data(), nullptr))
                         std::exit(3);
@@ -192,27 +194,72 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     const long calls_n = stat("coalesced_calls") - c0, batches = stat("coalesced_batches") - b0;
     std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s) x %d lane(s), "
-                "carry %d: %7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls, lanes, clanes, carry,
+                "carry %d, wait %d us%s: %7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls, lanes, clanes,
+                carry, wait_us, nt ? ", streaming copies" : "",
                 double(T) * calls * B / sec / 1073741824.0, calls_n, batches, double(batches) / double(calls_n),
                 rsmi_last_kernel(c));
     for (auto* p : bufs) rsmi_host_free(p);
     for (auto* x : cs) rsmi_close(x);
 }
 
+// One thread, back-to-back in-place host calls of N blocks each (a coalesced group's shape without
+// the queue): the rate of the zero-copy kernel + launch + synchronisation against group size.
+static void group_sweep() {
+    for (auto shape : {std::make_tuple(10, 4, size_t(262144)), std::make_tuple(2, 1, size_t(262144))}) {
+        const int k = std::get<0>(shape), m = std::get<1>(shape);
+        const size_t B = std::get<2>(shape), n = size_t(k + m), S = rsmi_shard_size(B, k);
+        rsmi_ctx* c = nullptr;
+        if (rsmi_open(k, m, 0, &c) != RSMI_OK || rsmi_warm(c) != RSMI_OK) std::exit(2);
+        for (size_t N : {1, 2, 4, 8, 16, 32, 64, 256}) {
+            uint8_t* buf = static_cast<uint8_t*>(rsmi_host_alloc(N * n * S));
+            for (size_t i = 0; i < N * n * S; i++) buf[i] = uint8_t(i * 7);
+            std::vector<uint32_t> raw(N * n);
+            for (int crc = 0; crc < 2; crc++) {
+                auto call = [&] {
+                    return crc ? rsmi_encode_batch_host_crcs(c, buf, n * S, buf + k * S, n * S, S, N, raw.data(), nullptr)
+                               : rsmi_encode_batch_host(c, buf, n * S, buf + k * S, n * S, S, N);
+                };
+                const int it = int(std::max<size_t>(20, 2048 / N));
+                for (int i = 0; i < 5; i++) call();
+                const auto a = clk::now();
+                for (int i = 0; i < it; i++)
+                    if (call() != RSMI_OK) std::exit(3);
+                const double us = std::chrono::duration<double, std::micro>(clk::now() - a).count() / it;
+                std::printf("RS(%d,%d) B=%zu  %3zu blocks per in-place call%s: %8.1f us per call, %6.2f GiB/s, "
+                            "%5.1f GB/s host->device (%s)\n", k, m, B, N, crc ? " + CRC-16" : "          ", us,
+                            double(N * B) / us / 1073.741824, double(N * k * S) / us / 1e3, rsmi_last_kernel(c));
+            }
+            rsmi_host_free(buf);
+        }
+        rsmi_close(c);
+    }
+}
+
 int main(int argc, char** argv) {
     install_crash_handler();
+    if (argc > 1 && !std::strcmp(argv[1], "--group-sweep")) {
+        group_sweep();
+        return 0;
+    }
     if (argc > 1 && !std::strcmp(argv[1], "--threads")) {
         // one context with 1, 2 or 4 coalescing lanes (one queue), and round 4's spread over 4
         // contexts of one lane each
-        // (contexts, lanes, carry)
-        for (auto cfg : {std::make_tuple(1, 1, 0), std::make_tuple(1, 1, 1), std::make_tuple(1, 2, 0),
-                         std::make_tuple(1, 2, 1), std::make_tuple(1, 4, 1), std::make_tuple(4, 1, 0)})
-            for (int T : {4, 16})
+        // (contexts, lanes, carry, coalesce_us, streaming copies); THREADS_CFG=quick: the first
+        // (default) configuration and its variants at 16 threads only
+        const bool quick = std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "quick");
+        for (auto cfg : {std::make_tuple(1, 2, 1, 0, false), std::make_tuple(1, 2, 1, 0, true),
+                         std::make_tuple(1, 1, 1, 30, false), std::make_tuple(1, 2, 1, 30, false),
+                         std::make_tuple(1, 1, 0, 0, false), std::make_tuple(1, 1, 1, 0, false),
+                         std::make_tuple(1, 2, 0, 0, false), std::make_tuple(1, 4, 1, 0, false),
+                         std::make_tuple(4, 1, 0, 0, false)})
+            for (int T : {4, 16}) {
+                if (quick && T != 16) continue;
                 for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
                                    std::make_tuple(16, 4, size_t(4194304))})
                     coalesced_threads(std::get<0>(shape), std::get<1>(shape), std::get<2>(shape), T,
                                       std::get<2>(shape) > (size_t(1) << 20) ? 16 : 128, std::get<0>(cfg),
-                                      std::get<1>(cfg), std::get<2>(cfg));
+                                      std::get<1>(cfg), std::get<2>(cfg), std::get<3>(cfg), std::get<4>(cfg));
+            }
         return 0;
     }
     const int k = 10, m = 4, n = k + m;
