@@ -71,6 +71,19 @@ void set_last_kernel(rsmi_ctx* c, const std::string& label) {
 CrcScratch& crc_scratch(rsmi_ctx* c, hipStream_t st) {
     for (const Staging& s : c->staging)
         if (s.stream == st) return c->own_scratch;
+    auto it = c->stream_scratch.find(st);
+    if (it != c->stream_scratch.end()) return it->second;
+    // a caller that cycles through many streams: past 32 of them the device is drained once and
+    // every caller stream's scratch freed (a stream the caller has destroyed cannot be
+    // synchronised by itself, the device can)
+    if (c->stream_scratch.size() >= 32) {
+        (void)hipDeviceSynchronize();
+        for (auto& e : c->stream_scratch) {
+            if (e.second.d_chunks) (void)hipFree(e.second.d_chunks);
+            if (e.second.d_fctr) (void)hipFree(e.second.d_fctr);
+        }
+        c->stream_scratch.clear();
+    }
     return c->stream_scratch[st];
 }
 
@@ -402,10 +415,8 @@ void rsmi_close(rsmi_ctx* c) {
                 if (x.d_fctr) (void)hipFree(x.d_fctr);
             };
             free_scratch(c->own_scratch);
-            for (auto& e : c->stream_scratch) {
-                (void)hipStreamSynchronize(e.first);
-                free_scratch(e.second);
-            }
+            if (!c->stream_scratch.empty()) (void)hipDeviceSynchronize();  // caller streams may be gone
+            for (auto& e : c->stream_scratch) free_scratch(e.second);
             if (c->d_crc32_tbl) (void)hipFree(c->d_crc32_tbl);
             if (c->d_crc32) (void)hipFree(c->d_crc32);
         }

@@ -162,11 +162,27 @@ def test_new_options_and_stats_validate():
     L = rsmi.lib()
     with rsmi.Codec(10, 4) as c:
         for key, good, bad in [(b"waves_per_cu", 8, -1), (b"coalesce_us", 50, -1), (b"coalesce_max", 16, 0),
-                               (b"crc16_fold", 0, 2), (b"crc16_fused_fold", 0, 2)]:
+                               (b"crc16_fold", 0, 2), (b"crc16_fused_fold", 0, 2), (b"coalesce_lanes", 4, 0),
+                               (b"coalesce_lanes", 16, 17), (b"coalesce_carry", 0, -1), (b"coalesce_carry", 16, 17)]:
             assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
             assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key
         assert c.stat("coalesced_calls") == 0 and c.stat("coalesced_batches") == 0
         assert c.stat("no_such_counter") == -1
+
+
+def test_warm_fails_loudly_without_gpu():
+    """rsmi_warm binds the device and opens the coalescing lanes: on a host without a GPU it
+    reports RSMI_ERR_NO_DEVICE (no CPU fallback), and a NULL context is an argument error."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = rsmi.lib()
+    assert L.rsmi_warm(None) == rsmi.ErrInvalidArg
+    with rsmi.Codec(10, 4) as c:
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.warm()
+        assert e.value.code == rsmi.ErrNoDevice
 
 
 def test_coalesced_calls_fail_loudly_without_gpu():
