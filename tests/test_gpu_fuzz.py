@@ -72,3 +72,94 @@ def test_random_shape_encode_reconstruct(seed):
                 assert np.array_equal(row, full[b, i]), (k, m, S, layout, lost, data_only, b, i)
             else:
                 assert not row.any()
+
+
+GROUP_CASES = 16
+
+
+def _group_case(seed):
+    r = np.random.default_rng(5000 + seed)
+    k, m = [(2, 1), (4, 2), (10, 4), (16, 4), (3, 2), (10, 4)][int(r.integers(0, 6))]
+    B = int(r.choice([int(r.integers(1, 64)), int(r.integers(64, 5000)), int(r.integers(5000, 300000)),
+                      262144, 1048576 + 14]))
+    T = int(r.choice([2, 3, int(r.integers(4, 20)), int(r.integers(60, 70))]))
+    crc = bool(r.integers(0, 2))
+    nlost = int(r.integers(1, m + 1))
+    lost = sorted(int(x) for x in r.choice(k + m, size=nlost, replace=False))
+    data_only = bool(r.integers(0, 2))
+    return k, m, B, T, crc, lost, data_only, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(GROUP_CASES))
+def test_random_coalesced_groups(seed):
+    """Seeded random coalesced groups (DagNode.Put / degraded Get from T goroutines at once,
+    node.go:358-408 / :220-326) over page-locked buffers: random (k, m) among the table shapes and
+    one without, block sizes from 1 byte to 1 MiB + 14 (rows under 16 bytes, aligned and odd
+    shard sizes), 2..69 requests in one deterministic batch (one lane, coalesce_us; more than 64
+    take two table launches), with and without CRC-16, then a random loss pattern rebuilt the same
+    way.  Every shard, R(shard) and rebuilt row equals the oracle's; rows not asked for stay
+    untouched."""
+    import ctypes
+    import threading
+
+    k, m, B, T, crc, lost, data_only, r = _group_case(seed)
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    blocks = [bytes(r.integers(0, 256, size=B, dtype=np.uint8)) for _ in range(T)]
+    want = []
+    for b in blocks:
+        w = orc.split(k, m, b)
+        w[k:] = orc.encode(k, m, w[:k])
+        want.append(w)
+    ptrs = [L.rsmi_host_alloc(n * S) for _ in range(T)]
+    assert all(ptrs)
+    try:
+        views = [np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S) for p in ptrs]
+        raws = [(ctypes.c_uint32 * n)() for _ in range(T)]
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_lanes", 1)
+            c.set_option("coalesce_us", 100000)
+            c.set_option("coalesce_max", T)
+            for t in range(T):
+                flat = views[t].reshape(-1)
+                flat[:] = 0x5A
+                flat[:B] = np.frombuffer(blocks[t], dtype=np.uint8)
+            rcs = [None] * T
+
+            def enc(t):
+                rcs[t] = L.rsmi_encode_block_coalesced(c._h, ptrs[t], B, ptrs[t], raws[t] if crc else None)
+
+            th = [threading.Thread(target=enc, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert rcs == [0] * T, c.last_kernel()
+            for t in range(T):
+                assert np.array_equal(views[t], want[t]), (t, c.last_kernel())
+                for i in range(n if crc else 0):
+                    assert rsmi.crc16_entry(b"", raws[t][i], S) == orc.crc16_ibm(want[t][i].tobytes()), (t, i)
+            present = (ctypes.c_uint8 * n)(*[0 if i in lost else 1 for i in range(n)])
+            for t in range(T):
+                views[t][lost] = 0xEE
+
+            def rec(t):
+                rcs[t] = L.rsmi_reconstruct_coalesced(c._h, ptrs[t], S, present, 1 if data_only else 0)
+
+            th = [threading.Thread(target=rec, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert rcs == [0] * T
+            for t in range(T):
+                for i in range(n):
+                    if i in lost and data_only and i >= k:
+                        assert (views[t][i] == 0xEE).all(), (t, i)
+                    else:
+                        assert np.array_equal(views[t][i], want[t][i]), (t, i, c.last_kernel())
+    finally:
+        for p in ptrs:
+            L.rsmi_host_free(p)
