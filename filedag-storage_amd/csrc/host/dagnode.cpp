@@ -8,6 +8,12 @@
 #include <map>
 #include <stdexcept>
 
+// 1: PutMany and GetMany without their overlap (one chunk at a time: writes joined at once, no
+// fetch ahead) -- round 4's loops, for same-box A/B library builds (tools/dagnode_ab.sh)
+#ifndef RSMI_BATCH_SERIAL
+#define RSMI_BATCH_SERIAL 0
+#endif
+
 namespace rsmi {
 namespace host {
 
@@ -346,24 +352,35 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             continue;
         }
         const size_t S = rsmi_shard_size(B, k);
-        const size_t chunk = staging_blocks(size_t(n) * S);
+        // Two halves of the thread's staging: a chunk's datanode writes run on a helper thread
+        // while the next chunk is staged and coded into the other half (the GPU call leaves the
+        // cores free for the writes), as RepairDataNodeBatched does.  A chunk joins the previous
+        // chunk's writes before it hands over its own, and the group joins the last before the
+        // next group (or the return), so every block's outcome is the sequential loop's.
+        const size_t chunk = std::max<size_t>(1, staging_blocks(size_t(n) * S) / (RSMI_BATCH_SERIAL ? 1 : 2));
+        const size_t half = std::min(chunk, g.second.size()) * size_t(n) * S;
         const Bytes meta = encode_meta(int32_t(B));
         const int wq = EntryQuorum().second;
         // datanodes over mutcask keep a CRC-32 of every value: the GPU pass supplies it too when
         // asked (SetGpuValueChecksums), else each datanode folds its own
         bool want32 = false;
         for (auto& sn : nodes_) want32 |= gpu_value_checksums_ && sn.client->WantsValueChecksum();
-        std::vector<uint32_t> raw, raw32;
+        uint8_t* base = thread_staging().reserve(2 * half);
+        if (!base) {
+            for (size_t i : g.second) results[i] = Status::Error("out of host memory");
+            continue;
+        }
+        std::future<void> writing;
+        auto join_writes = [&] {
+            if (writing.valid()) writing.get();
+        };
+        int cur = 0;
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
             const size_t* idx = g.second.data() + c0;
             // per block: k data rows (Split, zero-padded) + m parity rows
             const auto t0 = PhaseClock::now();
-            uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);
-            if (!flat) {
-                for (size_t j = 0; j < nb; j++) results[idx[j]] = Status::Error("out of host memory");
-                continue;
-            }
+            uint8_t* flat = base + (cur ? half : 0);
             fan_keys(int(std::min<size_t>(nb, 16)), [&](int t) {
                 for (size_t j = size_t(t); j < nb; j += std::min<size_t>(nb, 16)) {
                     std::memcpy(flat + j * n * S, blocks[idx[j]].data(), B);
@@ -372,6 +389,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             });
             phase_add(Phase::Stage, t0);
             const auto t1 = PhaseClock::now();
+            std::vector<uint32_t> raw, raw32;
             if (gpu_checksums_) {
                 raw.resize(nb * size_t(n));
                 raw32.resize(want32 ? nb * size_t(n) : 0);
@@ -381,35 +399,42 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
             }
             phase_add(Phase::Codec, t1);
+            join_writes();  // the other half is free again
             if (rc) {
                 for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
                 continue;
             }
             // the blocks' datanode writes run concurrently (the reference's concurrent Puts),
-            // each with its own node fan-out
-            const auto t2 = PhaseClock::now();
-            fan_keys(int(nb), [&](int j) {
-                const uint8_t* base = flat + size_t(j) * n * S;
-                std::vector<Status> res(static_cast<size_t>(n));
-                fan(n, [&](int i) {
-                    const ByteView shard(base + size_t(i) * S, S);
-                    DataNodeClient& cl = *nodes_[i].client;
-                    if (!gpu_checksums_) {
-                        res[i] = cl.Put(keys[idx[j]], meta, shard);
-                        return;
-                    }
-                    const uint16_t c16 = entry_checksum(meta, S, raw[j * n + i]);
-                    res[i] = want32 && cl.WantsValueChecksum()
-                                 ? cl.PutWithChecksums(keys[idx[j]], meta, shard, c16,
-                                                       value_checksum(meta, S, c16, raw32[j * n + i]))
-                                 : cl.PutWithChecksum(keys[idx[j]], meta, shard, c16);
-                }, S);
-                QuorumWait w(wq, n - wq + 1);
-                for (const Status& r : res) w.add(r);
-                results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
+            // each with its own node fan-out, each shard a view of the staging
+            writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, n, wq, want32,
+                                                      raw = std::move(raw), raw32 = std::move(raw32)] {
+                const auto t2 = PhaseClock::now();
+                fan_keys(int(nb), [&](int j) {
+                    const uint8_t* bb = flat + size_t(j) * n * S;
+                    std::vector<Status> res(static_cast<size_t>(n));
+                    fan(n, [&](int i) {
+                        const ByteView shard(bb + size_t(i) * S, S);
+                        DataNodeClient& cl = *nodes_[i].client;
+                        if (!gpu_checksums_) {
+                            res[i] = cl.Put(keys[idx[j]], meta, shard);
+                            return;
+                        }
+                        const uint16_t c16 = entry_checksum(meta, S, raw[j * n + i]);
+                        res[i] = want32 && cl.WantsValueChecksum()
+                                     ? cl.PutWithChecksums(keys[idx[j]], meta, shard, c16,
+                                                           value_checksum(meta, S, c16, raw32[j * n + i]))
+                                     : cl.PutWithChecksum(keys[idx[j]], meta, shard, c16);
+                    }, S);
+                    QuorumWait w(wq, n - wq + 1);
+                    for (const Status& r : res) w.add(r);
+                    results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
+                });
+                phase_add(Phase::Put, t2);
             });
-            phase_add(Phase::Put, t2);
+            cur ^= 1;
+            if (RSMI_BATCH_SERIAL) join_writes();
         }
+        join_writes();
     }
     // node.go:411-416 returns the error of the last Put
     return results.empty() ? Status::Ok() : results.back();
@@ -684,17 +709,36 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
     if (batch == 0) batch = 1;
     blocks->assign(keys.size(), Bytes());
     statuses->assign(keys.size(), Status());
-    // `batch` keys at a time: fetched shards are held only for the current chunk
+    // `batch` keys at a time: fetched shards are held for the current chunk and the next.  The
+    // keys' fetches run concurrently, like the reference's concurrent Gets (one goroutine per dag
+    // pool request), each with its own node fan-out, and the next chunk's fetch runs on a helper
+    // thread while this one is checked, decoded and assembled (the GPU decode leaves the cores to
+    // it); fetches only read, so fetching one chunk ahead changes no key's outcome.
+    // With GPU-verified reads, the first waves of all keys are checked together: one GPU
+    // pass per shard size instead of one per key and wave.  A key with a bad shard runs the
+    // per-key fetch again (checked wave by wave), so quorum, repair list and errors are
+    // exactly Get's; its first attempt only read.
+    struct Chunk {
+        std::vector<Fetched> fs;
+        std::vector<Status> st;
+    };
+    auto fetch_chunk = [this, &keys](size_t c0, size_t cn) {
+        Chunk c;
+        c.fs.resize(cn);
+        c.st.resize(cn);
+        fan_keys(int(cn), [&](int q) { c.st[size_t(q)] = fetch_for_get(keys[c0 + size_t(q)], &c.fs[size_t(q)], true); });
+        return c;
+    };
+    // the first chunk on this thread (a one-key GetMany is Get: no helper thread), later ones
+    // fetched ahead
+    std::future<Chunk> ahead;
     for (size_t k0 = 0; k0 < keys.size(); k0 += batch) {
         const size_t nk = std::min(batch, keys.size() - k0);
-        std::vector<Fetched> fs(nk);
-        // the keys' fetches run concurrently, like the reference's concurrent Gets (one
-        // goroutine per dag pool request), each with its own node fan-out
-        // With GPU-verified reads, the first waves of all keys are checked together: one GPU
-        // pass per shard size instead of one per key and wave.  A key with a bad shard runs the
-        // per-key fetch again (checked wave by wave), so quorum, repair list and errors are
-        // exactly Get's; its first attempt only read.
-        fan_keys(int(nk), [&](int q) { (*statuses)[k0 + q] = fetch_for_get(keys[k0 + q], &fs[q], true); });
+        Chunk cur = k0 == 0 || RSMI_BATCH_SERIAL ? fetch_chunk(k0, nk) : ahead.get();
+        if (k0 + batch < keys.size() && !RSMI_BATCH_SERIAL)
+            ahead = std::async(std::launch::async, fetch_chunk, k0 + batch, std::min(batch, keys.size() - k0 - batch));
+        std::vector<Fetched>& fs = cur.fs;
+        for (size_t q = 0; q < nk; q++) (*statuses)[k0 + q] = std::move(cur.st[q]);
         // does key q's data need the batched decode below (else the per-key path decides)
         auto needs_decode = [&](size_t q) {
             if (!(*statuses)[k0 + q].ok() || fs[q].meta.block_size <= 0) return false;
