@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
 #pragma unroll
             for (int j = 0; j < MT; j++) {
                 const u32x4 o = u32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-                st16u<NT == 1>(ob + out_off[j] + win, o);
+                st16u<NT == 1 && RSMI_UA_NT_STORES>(ob + out_off[j] + win, o);
             }
         } else if (!UA && ch < cpb) {
             const uint32_t boff = ch * 16u;
@@ -1463,6 +1463,7 @@ void* crc16_rows_kernel(bool aligned) {
 // One kernel per (K, MT) and layout, with the cache policy of the shape (auto_cache_policy in
 // rsmi_core.cpp): nontemporal stores unless the tile reads at least 4 rows per row it writes.
 constexpr int auto_nt(int K, int MT) { return K >= 4 * MT ? 2 : 1; }
+constexpr int ua_nt(int K, int MT) { return RSMI_UA_NT ? RSMI_UA_NT : auto_nt(K, MT); }
 
 #ifdef RSMI_TB_UNIT
 // the table-of-bases forms (rs_kernels_tb.hip, its own translation unit so the build compiles it
@@ -1472,7 +1473,7 @@ template <int K, int MT>
 static void fill_tb_km(FastKernelTable& t) {
     constexpr int NT = auto_nt(K, MT);
     t.fn_tb[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, false, true>);
-    t.ua_tb[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, false, true>);
+    t.ua_tb[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, ua_nt(K, MT), kMinWavesPerSimd, true, false, true>);
 }
 template <int K, int MT>
 static void fill_tb_fused(FastKernelTable& t) {
@@ -1505,7 +1506,7 @@ template <int K, int MT>
 static void fill_km(FastKernelTable& t) {
     constexpr int NT = auto_nt(K, MT);
     t.fn[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT>);
-    t.ua[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true>);
+    t.ua[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, ua_nt(K, MT), kMinWavesPerSimd, true>);
     t.crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, false, true>);
     t.ua_crc[K][MT] = reinterpret_cast<void*>(&rs_fast_kernel<K, MT, NT, kMinWavesPerSimd, true, true>);
     t.fused[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd>);

@@ -16,6 +16,15 @@ constexpr int kMinWavesPerSimd = 4;  // caps the fast kernels at 128 VGPRs (16 w
 #ifndef RSMI_UA_DWORD_LOADS
 #define RSMI_UA_DWORD_LOADS 1
 #endif
+// A/B knobs for the unaligned-window coding kernels (tools/ua_ab.sh, Split layout): the cache
+// policy of their instantiations (0: the shape's own, auto_nt; 1 or 2: that one for every UA
+// shape), and whether a write-heavy UA tile's stores are nontemporal (1) or default (0)
+#ifndef RSMI_UA_NT
+#define RSMI_UA_NT 0
+#endif
+#ifndef RSMI_UA_NT_STORES
+#define RSMI_UA_NT_STORES 1
+#endif
 
 // One launch tile: MT (<= 4) output rows computed from K input rows.
 // tbl[c*20 + f*4 + j] = field-f product word for coefficient coef[j][c] (gf256.hpp

@@ -18,6 +18,8 @@
 #   dagnode_suite    the C++ Dag Node suite on the GPU
 #   dagnode_cmp      the Dag Node bench, GPU codec beside the CPU codec (tools/dagnode_cpu_vs_gpu.sh)
 #   dagnode_ab       the Dag Node bench (GPU codec) on the product library and every tools/build/v_* variant
+#   ua_ab            the Split-layout (UA) kernels: product library against every tools/build/v_*
+#                    variant (tools/ua_ab.sh), then each library's FETCH_SIZE / WRITE_SIZE passes
 #   latency          per-block call latencies (tools/latency)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   group_sweep      one thread, in-place host calls of 1..256 blocks back to back (tools/latency --group-sweep)
@@ -80,6 +82,19 @@ dagnode_cmp)
 dagnode_ab)
   DN_OUT=$O/dagnode_ab.jsonl timeout -k 10 1000 bash tools/dagnode_ab.sh > $O/dagnode_ab.txt 2>&1 || fail "dagnode ab" $O/dagnode_ab.txt
   grep -v " done$" $O/dagnode_ab.txt ;;
+ua_ab)
+  timeout -k 10 600 bash tools/ua_ab.sh > $O/ua_ab.txt 2>&1 || fail ua_ab $O/ua_ab.txt
+  cat $O/ua_ab.txt
+  for lib in filedag-storage_amd/lib/librsmi.so tools/build/v_*/lib/librsmi.so; do
+    v=$(basename $(dirname $(dirname $lib))); [ "$v" = filedag-storage_amd ] && v=product
+    export RSMI_LIB=$R/$lib
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$R/$O/pmc_${v}_$ctr" -o pmc -- python3 "$R/tools/prof_kernels.py" 5 split > "$R/$O/pmc_${v}_$ctr.log" 2>&1) || fail "pmc $v $ctr" $O/pmc_${v}_$ctr.log
+    done
+    unset RSMI_LIB
+    python tools/pmc_summary.py $O/pmc_${v}_FETCH_SIZE/pmc_counter_collection.csv $O/pmc_${v}_WRITE_SIZE/pmc_counter_collection.csv $O/pmc_ua_$v.json
+    echo "$v: $(cat $O/pmc_ua_$v.json | tr -d '\n')"
+  done ;;
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
