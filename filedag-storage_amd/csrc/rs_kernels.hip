@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             } else if constexpr (UA) {
                 // nontemporal loads for write-heavy tiles; read-heavy UA tiles keep the lines
                 // they share with their neighbours in the L2
-                return ld16u<NT == 1>(ib + in_off[c] + win);
+                return ld16u<NT == 1 && RSMI_UA_NT_LOADS>(ib + in_off[c] + win);
             } else {
                 return ld16<true>(reinterpret_cast<const u32x4*>(ib + in_off[c]) + chl);
             }

@@ -25,6 +25,10 @@ constexpr int kMinWavesPerSimd = 4;  // caps the fast kernels at 128 VGPRs (16 w
 #ifndef RSMI_UA_NT_STORES
 #define RSMI_UA_NT_STORES 1
 #endif
+// ... and whether its loads are nontemporal (1) or default (0)
+#ifndef RSMI_UA_NT_LOADS
+#define RSMI_UA_NT_LOADS 1
+#endif
 
 // One launch tile: MT (<= 4) output rows computed from K input rows.
 // tbl[c*20 + f*4 + j] = field-f product word for coefficient coef[j][c] (gf256.hpp
