@@ -1452,25 +1452,6 @@ void* crc16_combine_kernel(int ns2) {
 }
 
 // aligned rows: the pipelined pass; any other layout: the plain nibble pass
-// The completion release of a small host call (finish_call, rsmi_core.cpp), queued on its stream
-// behind the call's kernels: every workgroup makes the writes of its XCD visible to the host (the
-// fetch-add at system scope is a release, which writes the XCD's L2 back; the dispatcher deals
-// workgroups round-robin over the 8 XCDs, so kDoneWGs of them reach every L2) and counts itself in
-// the call's counter; the last one resets the counter for the slot's next call and releases the
-// slot's page-locked flag with the call's sequence number.  The host spins on that flag: it sees
-// the release ~4 us before a stream synchronisation returns (tools/doneflag_probe.hip).
-__global__ __launch_bounds__(kWave) void rs_done_kernel(uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag,
-                                                        uint32_t seq) {
-    if (threadIdx.x != 0) return;
-    const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1u == gridDim.x) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-void* done_kernel() { return reinterpret_cast<void*>(&rs_done_kernel); }
-
 void* crc16_rows_kernel(bool aligned) {
     return aligned ? reinterpret_cast<void*>(&rs_crc16_rows_pipe_kernel)
                    : reinterpret_cast<void*>(&rs_crc16_rows_kernel<false>);

@@ -162,9 +162,5 @@ void* crc16_combine_kernel(int ns2);  // ns2 = record dwords per lane (rows / 8,
 void* crc16_combine_mfma_kernel();    // records of rs_fused_mfma_kernel
 void* crc32_rows_kernel(bool aligned);
 void* crc32_rows_mfma_kernel(bool aligned);  // the fold on the matrix cores (512-thread workgroups)
-// the completion release of a small host call (rsmi_core.cpp finish_call): kDoneWGs workgroups,
-// one wave each
-constexpr int kDoneWGs = 64;
-void* done_kernel();
 
 }  // namespace rsmi

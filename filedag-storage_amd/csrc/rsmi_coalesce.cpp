@@ -119,7 +119,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         }
         const uint32_t *g16 = h16, *g32 = nullptr;
         if (!h16 && (rc = readback(c, d16, d32, nb * n * 4, st, g16, g32))) return fail(rc);
-        if ((rc = finish_call(c, st))) return fail(rc);
+        HIP_TRY(hipStreamSynchronize(st));
         if (want16) std::memcpy(r16.data(), g16, nb * n * 4);
         if (want32) std::memcpy(r32.data(), g32, nb * n * 4);
     }
@@ -210,7 +210,6 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
         x->opt_waves_per_cu = c->opt_waves_per_cu;
         x->opt_zero_copy = c->opt_zero_copy;
         x->opt_small_bytes = c->opt_small_bytes;
-        x->opt_spin_wait = c->opt_spin_wait;
         *rc = ensure_device(x);
     }
     if (*rc) {

@@ -2,7 +2,6 @@
 // entry points of include/rsmi.h (see rsmi_impl.hpp for the file map).
 #include "rsmi_impl.hpp"
 
-#include <chrono>
 #include <limits>
 
 using namespace rsmi;
@@ -409,8 +408,6 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->h_coal) (void)hipHostFree(c->h_coal);
             if (c->h_small) (void)hipHostFree(c->h_small);
             if (c->h_raw) (void)hipHostFree(c->h_raw);
-            if (c->h_done) (void)hipHostFree(c->h_done);
-            if (c->d_done_ctr) (void)hipFree(c->d_done_ctr);
             if (c->d_crc_tbl) (void)hipFree(c->d_crc_tbl);
             if (c->d_crc) (void)hipFree(c->d_crc);
             auto free_scratch = [](CrcScratch& x) {
@@ -475,66 +472,6 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
 namespace rsmi {
 namespace impl {
 
-namespace {
-constexpr uint32_t kDoneSlots = 64;          // calls in flight per context (callers hold its lock)
-constexpr uint32_t kDoneStride = 16;         // one 64-byte line per slot
-constexpr long kDoneSpinUs = 200;            // then a blocking synchronisation instead of the spin
-}  // namespace
-
-// Replaces hipStreamSynchronize at the end of a small host call (one block, a coalesced group):
-// rs_done_kernel queued behind the call's kernels releases the slot's page-locked flag with the
-// call's sequence number, and the caller spins on it.  The stream is queried every 128 polls: an
-// error is returned as the synchronisation would return it, a stream that drained without the
-// flag is an error too, and a call still running after kDoneSpinUs blocks in the synchronisation.
-int finish_call(rsmi_ctx* c, hipStream_t st) {
-    if (!c->opt_spin_wait) {
-        HIP_TRY(hipStreamSynchronize(st));
-        return RSMI_OK;
-    }
-    if (!c->h_done) {
-        void* h = nullptr;
-        HIP_TRY(pinned_alloc(&h, kDoneSlots * kDoneStride * 4));
-        std::memset(h, 0, kDoneSlots * kDoneStride * 4);
-        // the counters are zeroed on this stream and the zeros waited for: a plain hipMemset is
-        // not ordered before kernels on a non-blocking stream
-        void* d = nullptr;
-        uint8_t* hd = host_alias(h, kDoneSlots * kDoneStride * 4);
-        hipError_t e = hd ? hipMalloc(&d, kDoneSlots * kDoneStride * 4) : hipErrorInvalidValue;
-        if (e == hipSuccess) e = hipMemsetAsync(d, 0, kDoneSlots * kDoneStride * 4, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            if (d) (void)hipFree(d);
-            (void)hipHostFree(h);
-            return hip_status(e);
-        }
-        c->h_done = static_cast<uint32_t*>(h);
-        c->h_done_dev = reinterpret_cast<uint32_t*>(hd);
-        c->d_done_ctr = static_cast<uint32_t*>(d);
-    }
-    uint32_t seq = c->done_seq.fetch_add(1) + 1;
-    if (seq == 0) seq = c->done_seq.fetch_add(1) + 1;  // 0 is every flag's initial value
-    const uint32_t slot = seq % kDoneSlots;
-    uint32_t* flag = c->h_done + slot * kDoneStride;
-    uint32_t* dflag = c->h_done_dev + slot * kDoneStride;
-    uint32_t* ctr = c->d_done_ctr + slot * kDoneStride;
-    void* args[] = {&ctr, &dflag, &seq};
-    HIP_TRY(hipLaunchKernel(done_kernel(), dim3(kDoneWGs), dim3(kWave), args, 0, st));
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 1;; i++) {
-        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return RSMI_OK;
-        if ((i & 127u) == 0) {
-            const hipError_t q = hipStreamQuery(st);
-            if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? RSMI_OK : RSMI_ERR_DEVICE;
-            if (q != hipErrorNotReady) return hip_status(q);
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kDoneSpinUs)) {
-                HIP_TRY(hipStreamSynchronize(st));
-                return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? RSMI_OK : RSMI_ERR_DEVICE;
-            }
-        }
-        __builtin_ia32_pause();
-    }
-}
-
 int apply_option(rsmi_ctx* c, const char* key, long value) {
     if (!std::strcmp(key, "zero_copy")) {
         if (value < 0 || value > 2) return RSMI_ERR_INVALID_ARG;
@@ -569,9 +506,6 @@ int apply_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "coalesce_carry")) {
         if (value < 0 || value > 16) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_carry = value;
-    } else if (!std::strcmp(key, "spin_wait")) {
-        if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
-        c->opt_spin_wait = int(value);
     } else {
         return RSMI_ERR_INVALID_ARG;
     }

@@ -175,7 +175,7 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
         if (!d32) return RSMI_ERR_DEVICE;
         if ((rc = repitch(d32, raw32_sz, reinterpret_cast<uint8_t*>(cr), raw32_sz, raw32_sz, 1, st))) return rc;
     }
-    if ((rc = finish_call(c, st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
     if (stage_out)
         for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
     if (raw_out) std::memcpy(raw_out, hraw, raw_sz);
@@ -367,7 +367,7 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
         return rc;
     const uint32_t *h16, *h32;
     if ((rc = readback(c, d16, d32, raw_sz, st, h16, h32))) return rc;
-    if ((rc = finish_call(c, st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
     if (raw16) std::memcpy(raw16, h16, raw_sz);
     if (raw32) std::memcpy(raw32, h32, raw_sz);
     if (hs)
@@ -623,7 +623,7 @@ int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t bloc
             const uint32_t *all = nullptr, *unused;
             if (rc == RSMI_OK) rc = readback(c, d, nullptr, nblocks * nsh * 4, st, all, unused);
             if (rc == RSMI_OK) {
-                if ((rc = finish_call(c, st))) return rc;
+                HIP_TRY(hipStreamSynchronize(st));
                 for (size_t b = 0; b < nblocks; b++)
                     std::memcpy(raw16_in + b * k, all + b * nsh, k * 4);
                 return RSMI_OK;

@@ -94,10 +94,6 @@ struct CrcScratch {
 #ifndef RSMI_COALESCE_CARRY
 #define RSMI_COALESCE_CARRY 1
 #endif
-// default of option "spin_wait" (finish_call)
-#ifndef RSMI_SPIN_WAIT
-#define RSMI_SPIN_WAIT 1
-#endif
 
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0, device = 0;
@@ -132,13 +128,6 @@ struct rsmi_ctx {
     size_t h_small_cap = 0;
     uint8_t* h_raw = nullptr;  // page-locked landing area of row CRCs read back by kernel (readback)
     size_t h_raw_cap = 0;
-    // completion of small host calls (finish_call): page-locked flags and device counters, one
-    // slot (64 bytes apart) per call in flight, and the calls' sequence numbers
-    uint32_t* h_done = nullptr;
-    uint32_t* h_done_dev = nullptr;  // its device alias
-    uint32_t* d_done_ctr = nullptr;
-    std::atomic<uint32_t> done_seq{0};
-    int opt_spin_wait = RSMI_SPIN_WAIT;  // 1: small host calls spin on rs_done_kernel's flag; 0: hipStreamSynchronize
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;  // diagnostics (rsmi_last_kernel), under lk_mu
@@ -213,9 +202,6 @@ int repitch(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size
 uint8_t* host_alias(void* p, size_t len);
 uint8_t* small_stage(rsmi_ctx* c, size_t need);
 uint8_t* raw_area(rsmi_ctx* c, size_t bytes);
-// the end of a small host call: its kernels' writes visible to the host and the stream's work
-// done with the caller's buffers (rs_done_kernel's flag, or a stream synchronisation)
-int finish_call(rsmi_ctx* c, hipStream_t st);
 int readback(rsmi_ctx* c, const uint32_t* d16, const uint32_t* d32, size_t sz, hipStream_t st, const uint32_t*& h16,
              const uint32_t*& h32);
 int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs, uint8_t* parity, size_t pbs,

@@ -365,11 +365,7 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * RSMI_ERR_HOST; default 0), "coalesce_lanes" (coalesced batches coded at once, 1-16, default
  * 2; every option but the test hook also applies to the lanes' child contexts), "coalesce_carry"
  * (batches a lane's executor goes on to when they are queued by the time its own completes,
- * before it hands the lane to a waiting caller, 0-16, default 1), "spin_wait" (how a small host
- * call -- one block or a coalesced group, coded in place -- waits for its kernels: 1 = default, a
- * small kernel queued behind them releases a page-locked flag and the caller spins on it, ~4 us
- * sooner than a stream synchronisation returns; after 200 us, or on a stream error, it falls back
- * to the synchronisation; 0 = hipStreamSynchronize).  Kernel variants measured slower than the defaults are not
+ * before it hands the lane to a waiting caller, 0-16, default 1).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);

@@ -1055,48 +1055,3 @@ def test_fused_mfma_split_every_tail(k, m, mis):
                 rows = list(data[b]) + list(want[b])
                 for i in range(n):
                     assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (S, fill, b, i)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 4096), (16, 4, 1 << 20)])
-@pytest.mark.parametrize("spin", [0, 1])
-def test_spin_wait_small_calls(k, m, B, spin):
-    """Option spin_wait (finish_call, rsmi_core.cpp): the small in-place host calls of a lone Put,
-    a degraded Get (with the survivors' R(row)) and a repair wait for their kernels on
-    rs_done_kernel's page-locked flag (1) or a stream synchronisation (0).  150 rounds of each
-    (the flag slots wrap twice) on fresh data, every result against the oracle."""
-    n = k + m
-    S = (B + k - 1) // k
-    L = rsmi.lib()
-    p = L.rsmi_host_alloc(n * S)
-    assert p
-    try:
-        sh = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S)
-        rng = np.random.default_rng(B + spin)
-        lost = [0] if m == 1 else [1, k]
-        present = [i not in lost for i in range(n)]
-        used = [i for i in range(n) if present[i]][:k]
-        with rsmi.Codec(k, m) as c:
-            c.set_option("spin_wait", spin)
-            for it in range(150):
-                block = rng.integers(0, 256, size=B, dtype=np.uint8).tobytes()
-                full = orc.split(k, m, block)
-                full[k:] = orc.encode_fast(k, m, full[None, :k], threads=4)[0]
-                r16 = [orc.crc16_ibm(full[r].tobytes()) for r in range(n)] if it % 50 == 0 else None
-                sh.reshape(-1)[:] = 0x5A
-                sh[:k] = full[:k]
-                raw = np.zeros(n, dtype=np.uint32)
-                c.encode_batch_host_crcs_ptr(p, n * S, p + k * S, n * S, S, 1, raw.ctypes.data, None)
-                assert np.array_equal(sh, full), it
-                sh[lost] = 0
-                v16 = np.zeros(k, dtype=np.uint32)
-                c.reconstruct_batch_host_verify_ptr(p, n * S, S, 1, present, False, v16.ctypes.data)
-                assert np.array_equal(sh, full), it
-                sh[lost] = 0
-                c.reconstruct_rows_batch_host_ptr(p, n * S, S, 1, present, [i in lost for i in range(n)])
-                assert np.array_equal(sh, full), it
-                if r16:
-                    assert [rsmi.crc16_entry(b"", int(x), S) for x in raw] == r16, it
-                    assert [rsmi.crc16_entry(b"", int(v16[j]), S) for j in range(k)] == [r16[r] for r in used], it
-    finally:
-        L.rsmi_host_free(p)

@@ -21,7 +21,6 @@
 #   ua_ab            the Split-layout (UA) kernels: product library against every tools/build/v_*
 #                    variant (tools/ua_ab.sh), then each library's FETCH_SIZE / WRITE_SIZE passes
 #   latency          per-block call latencies (tools/latency)
-#   spin_ab          option spin_wait off / on, alternated, for the small in-place host calls (tools/latency --spin-ab)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   group_sweep      one thread, in-place host calls of 1..256 blocks back to back (tools/latency --group-sweep)
 #   threads_traced   the same under rocprofv3 --kernel-trace (crash report: tools/latency.cpp)
@@ -99,9 +98,6 @@ ua_ab)
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
-spin_ab)
-  timeout -k 10 200 ./tools/build/latency --spin-ab > $O/spin_ab.txt 2>&1 || fail spin_ab $O/spin_ab.txt
-  cat $O/spin_ab.txt ;;
 threads)
   timeout -k 10 300 ./tools/build/latency --threads > $O/threads.txt 2>&1 || fail threads $O/threads.txt
   cat $O/threads.txt ;;

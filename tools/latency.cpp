@@ -235,72 +235,8 @@ static void group_sweep() {
     }
 }
 
-// option spin_wait on and off in one process, alternated twice: the small host calls of the Dag
-// Node's per-block and per-key legs, page-locked buffers coded in place
-static int spin_ab() {
-    const int k = 10, m = 4, n = k + m;
-    rsmi_ctx* c = nullptr;
-    if (rsmi_open(k, m, 0, &c) != RSMI_OK) return 2;
-    for (size_t B : {size_t(4096), size_t(262144), size_t(4194304)}) {
-        const size_t S = rsmi_shard_size(B, k);
-        std::mt19937 r(7);
-        uint8_t* buf = static_cast<uint8_t*>(rsmi_host_alloc(n * S));
-        std::vector<uint8_t> blk(k * S, 0), ref;
-        for (size_t i = 0; i < B; i++) blk[i] = uint8_t(r());
-        std::vector<uint32_t> raw(n), ref_raw;
-        std::vector<uint8_t> present(n, 1), required(n, 0);
-        present[0] = 0;
-        required[0] = 1;
-        std::vector<uint32_t> vraw(k);
-        for (int rep = 0; rep < 2; rep++)
-            for (int spin : {0, 1}) {
-                if (rsmi_set_option(c, "spin_wait", spin) != RSMI_OK) return 3;
-                std::memcpy(buf, blk.data(), k * S);
-                const double enc = median_us([&] {
-                    return rsmi_encode_batch_host_crcs(c, buf, n * S, buf + k * S, n * S, S, 1, raw.data(), nullptr);
-                });
-                std::vector<uint8_t> got(buf, buf + n * S);
-                if (ref.empty()) {
-                    ref = got;
-                    ref_raw = raw;
-                } else if (got != ref || raw != ref_raw) {
-                    std::fprintf(stderr, "spin_wait %d: encode differs\n", spin);
-                    return 4;
-                }
-                const double rec = median_us([&] {
-                    return rsmi_reconstruct_batch_host(c, buf, n * S, S, 1, present.data(), 1);
-                });
-                const double rows = median_us([&] {
-                    return rsmi_reconstruct_rows_batch_host(c, buf, n * S, S, 1, present.data(), required.data());
-                });
-                const double ver = median_us([&] {
-                    return rsmi_reconstruct_batch_host_verify(c, buf, n * S, S, 1, present.data(), 1, vraw.data());
-                });
-                if (!std::equal(buf, buf + n * S, ref.begin())) {
-                    std::fprintf(stderr, "spin_wait %d: reconstruct differs\n", spin);
-                    return 4;
-                }
-                for (int i = 1; i <= k; i++)
-                    if (vraw[size_t(i - 1)] != ref_raw[size_t(i)]) {
-                        std::fprintf(stderr, "spin_wait %d: verify R differs\n", spin);
-                        return 4;
-                    }
-                const double coal = median_us([&] {
-                    return rsmi_encode_block_coalesced_crcs(c, blk.data(), B, buf, raw.data(), nullptr);
-                });
-                std::printf("B=%8zu spin_wait %d: in-place encode + CRC-16 %6.1f us | reconstruct 1 lost %6.1f | "
-                            "rows (repair) %6.1f | reconstruct + verify %6.1f | coalesced encode (lone) %6.1f\n",
-                            B, spin, enc, rec, rows, ver, coal);
-            }
-        rsmi_host_free(buf);
-    }
-    rsmi_close(c);
-    return 0;
-}
-
 int main(int argc, char** argv) {
     install_crash_handler();
-    if (argc > 1 && !std::strcmp(argv[1], "--spin-ab")) return spin_ab();
     if (argc > 1 && !std::strcmp(argv[1], "--group-sweep")) {
         group_sweep();
         return 0;
