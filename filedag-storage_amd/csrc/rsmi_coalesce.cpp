@@ -79,7 +79,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         // pitch S for encode, n rows in place for reconstruct); the CRC-32 keeps a launch per block.
         // The fused kernel's combine writes each R(shard) once, so the table launches store them
         // straight into the page-locked read-back area (no read-back kernel after them)
-        bool table = nb > 1 && !want32;
+        bool table = nb >= size_t(RSMI_TABLE_MIN_BLOCKS) && !want32;
         uint32_t* h16 = nullptr;  // the table launches' R(shard): host view, and its device alias
         uint32_t* h16_dev = nullptr;
         if (table && want16) {

@@ -94,6 +94,12 @@ struct CrcScratch {
 #ifndef RSMI_COALESCE_CARRY
 #define RSMI_COALESCE_CARRY 1
 #endif
+// the fewest blocks a coalesced group codes through the table kernels (R(shard) straight into
+// page-locked memory, no read-back dispatch): 1, a lone caller too (build macro for A/B variants;
+// 2 before profiles/r05/r/)
+#ifndef RSMI_TABLE_MIN_BLOCKS
+#define RSMI_TABLE_MIN_BLOCKS 1
+#endif
 
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0, device = 0;

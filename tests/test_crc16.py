@@ -488,6 +488,9 @@ def test_coalesced_group_in_place_on_page_locked_buffers(k, m, B, split_by_calle
 @pytest.mark.parametrize("k,m,B,T,crc", [
     (10, 4, 262144, 12, True),      # unaligned windows (S = 26215), the fused kernel + its combine launch
     (10, 4, 262144, 4, True),       # 28 units: the fused kernel with the combine inside
+    (10, 4, 262144, 1, True),       # a lone caller: one block through the table kernel too
+    (16, 4, 4194304, 1, True),      # a lone 4 MiB block (the combine launch)
+    (10, 4, 262144, 1, False),
     (10, 4, 262144, 12, False),     # the plain encode over the table
     (2, 1, 262144, 6, True),        # aligned rows (S = 131072)
     (4, 2, 4099, 80, True),         # more blocks than one table holds: two table launches
