@@ -20,13 +20,22 @@
 // execute the next batch.  (One shared condition variable woke every waiting caller at each
 // batch's end, and the woken callers then took the queue's lock one after another before the
 // next executor could: with 16 callers that convoy cost more than a small batch's launch.)
+//
+// Pipelined batches: exec may return a finisher (a callable; empty or exec returning void: the
+// batch ran to completion) instead of waiting for its own work.  The executor then launches the
+// next queued batch (within `carry`) behind it before it calls the finisher, so the device is
+// handed the next batch while the host waits for the current one; a batch's callers return once
+// its finisher has run, and finishers run in launch order.
 #pragma once
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <functional>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 namespace rsmi {
@@ -62,39 +71,64 @@ public:
             if (wait_us > 0 && pending_.size() < cap)
                 fill_cv_.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return pending_.size() >= cap; });
             // the batch that holds this caller's request, then up to `carry` more on the same lane
-            // when requests are queued by then
-            for (int round = 0; round <= carry && !pending_.empty(); round++) {
+            // when requests are queued by then; a batch whose exec left work in flight (a
+            // finisher) has the next one launched behind it before it is finished
+            std::deque<Flight> flights;
+            int started = 0;
+            auto start = [&]() {  // under lk; launches unlocked and returns with lk held
+                if (pending_.empty() || started > carry) return;
+                started++;
                 const size_t take = std::min(cap, pending_.size());
-                std::vector<Waiter*> batch;
-                std::vector<Req*> reqs;
+                Flight f;
                 try {
-                    batch.assign(pending_.begin(), pending_.begin() + take);
-                    reqs.reserve(take);
-                    for (Waiter* w : batch) reqs.push_back(w->req);
+                    f.batch.assign(pending_.begin(), pending_.begin() + take);
+                    f.reqs.reserve(take);
+                    for (Waiter* w : f.batch) f.reqs.push_back(w->req);
                 } catch (...) {  // no memory for the batch list: fail these requests in place
                     for (size_t i = 0; i < take; i++) {
                         pending_[i]->queued = false;
                         pending_[i]->req->rc = fail_rc_;
                         pending_[i]->req->done = true;
-                        wake(*pending_[i]);
+                        if (pending_[i] != &me) wake(*pending_[i]);
                     }
                     pending_.erase(pending_.begin(), pending_.begin() + take);
-                    break;
+                    return;
                 }
-                for (Waiter* w : batch) w->queued = false;
+                for (Waiter* w : f.batch) w->queued = false;
                 pending_.erase(pending_.begin(), pending_.begin() + take);
                 lk.unlock();
                 try {
-                    exec(reqs, lane);
+                    if constexpr (std::is_void_v<std::invoke_result_t<Exec&, std::vector<Req*>&, int>>)
+                        exec(f.reqs, lane);
+                    else
+                        f.fin = exec(f.reqs, lane);
                 } catch (...) {
-                    for (Req* r : reqs) r->rc = fail_rc_;
+                    for (Req* r : f.reqs) r->rc = fail_rc_;
+                    f.fin = nullptr;
                 }
                 batches_++;
                 lk.lock();
-                for (Waiter* w : batch) {  // this batch's callers return now, whatever the lane does next
-                    w->req->done = true;
-                    if (w != &me) wake(*w);
+                try {
+                    flights.push_back(std::move(f));
+                } catch (...) {  // cannot track it: finish it here
+                    lk.unlock();
+                    if (f.fin) finish(f);
+                    lk.lock();
+                    complete(f, me);
                 }
+            };
+            start();
+            while (!flights.empty()) {
+                if (flights.size() == 1 && flights.front().fin) start();  // the next, behind it
+                Flight f = std::move(flights.front());
+                flights.pop_front();
+                if (f.fin) {
+                    lk.unlock();
+                    finish(f);
+                    lk.lock();
+                }
+                complete(f, me);  // this batch's callers return now, whatever the lane does next
+                if (flights.empty()) start();
             }
             busy_ &= ~(uint64_t(1) << lane);
             executing_--;
@@ -105,6 +139,26 @@ public:
     uint64_t batches() const { return batches_.load(); }
 
 private:
+    struct Waiter;
+    struct Flight {
+        std::vector<Waiter*> batch;
+        std::vector<Req*> reqs;
+        std::function<void()> fin;  // the batch's wait, when exec left it in flight
+    };
+    void finish(Flight& f) {
+        try {
+            f.fin();
+        } catch (...) {
+            for (Req* r : f.reqs) r->rc = fail_rc_;
+        }
+    }
+    // caller holds mu_
+    static void complete(Flight& f, Waiter& me) {
+        for (Waiter* w : f.batch) {
+            w->req->done = true;
+            if (w != &me) wake(*w);
+        }
+    }
     struct Waiter {
         Req* req = nullptr;
         bool queued = false;  // in pending_ (under mu_)

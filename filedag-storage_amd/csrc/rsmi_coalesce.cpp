@@ -25,6 +25,23 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
     return c->h_coal;
 }
 
+// Landing area `slot` of the pipelined table launches' R(shard) (caller holds ctx->mu; the slot's
+// previous batch has been finished: a lane has at most two batches in flight, alternating slots)
+static uint8_t* pipe_area(rsmi_ctx* c, int slot, size_t bytes) {
+    if (c->h_pipe_cap[slot] < bytes) {
+        if (c->h_pipe[slot]) (void)hipHostFree(c->h_pipe[slot]);
+        c->h_pipe[slot] = nullptr;
+        c->h_pipe_cap[slot] = 0;
+        const size_t cap = std::max<size_t>(bytes, 64 << 10);
+        if (pinned_alloc(reinterpret_cast<void**>(&c->h_pipe[slot]), cap) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        c->h_pipe_cap[slot] = cap;
+    }
+    return c->h_pipe[slot];
+}
+
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
 // run_coalesced_group): one launch over a table of the blocks' bases for up to kTableBlocks
 // requests (BlockBases, the table kernels of the BASELINE shapes), else one launch per request,
@@ -32,7 +49,12 @@ uint8_t* coal_stage(rsmi_ctx* c, size_t need) {
 // block is pageable), outside the context lock -- unless the caller Split it there itself
 // (block == out), as the host mirror does, so the copies run on the callers' threads in
 // parallel instead of one after another on the executor's.
-int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S) {
+// fin (option coalesce_pipeline): a group coded by table launches is left in flight behind an
+// event, and *fin set to its wait (the R(shard) copies and any error land in the requests then),
+// so the executor can launch the next batch first (group_commit.hpp); other groups wait here and
+// leave *fin empty.
+int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S,
+                           std::function<void()>* fin) {
     const size_t k = size_t(c->k), n = size_t(c->n);
     const std::string& key = rq[0]->key;
     const bool enc = key[0] == 'E';
@@ -80,10 +102,13 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         // The fused kernel's combine writes each R(shard) once, so the table launches store them
         // straight into the page-locked read-back area (no read-back kernel after them)
         bool table = nb >= size_t(RSMI_TABLE_MIN_BLOCKS) && !want32;
+        const bool pipe = fin && table && c->opt_coalesce_pipeline;
+        const int slot = c->pipe_slot;
+        if (pipe && !c->pipe_ev[slot]) HIP_TRY(hipEventCreateWithFlags(&c->pipe_ev[slot], hipEventDisableTiming));
         uint32_t* h16 = nullptr;  // the table launches' R(shard): host view, and its device alias
         uint32_t* h16_dev = nullptr;
         if (table && want16) {
-            uint8_t* h = raw_area(c, nb * n * 4);
+            uint8_t* h = pipe ? pipe_area(c, slot, nb * n * 4) : raw_area(c, nb * n * 4);
             if (!h) return RSMI_ERR_DEVICE;
             h16 = reinterpret_cast<uint32_t*>(h);
             h16_dev = reinterpret_cast<uint32_t*>(host_alias(h, nb * n * 4));
@@ -108,6 +133,21 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             launched = true;
         }
         if (!table) h16 = nullptr;  // a launch per request: its R(shard) come back by read-back
+        if (pipe && table) {
+            hipError_t e = hipEventRecord(c->pipe_ev[slot], st);
+            if (e != hipSuccess) return fail(hip_status(e));
+            c->pipe_slot ^= 1;
+            std::vector<rsmi_ctx::CoalReq*> reqs(rq, rq + nb);
+            hipEvent_t ev = c->pipe_ev[slot];
+            *fin = [reqs = std::move(reqs), ev, h16, n]() {
+                const hipError_t w = hipEventSynchronize(ev);
+                for (size_t j = 0; j < reqs.size(); j++) {
+                    if (w != hipSuccess) reqs[j]->rc = hip_status(w);
+                    else if (reqs[j]->raw && h16) std::memcpy(reqs[j]->raw, h16 + j * n, n * 4);
+                }
+            };
+            return RSMI_OK;
+        }
         for (size_t j = 0; j < nb && !table; j++) {
             if (enc)
                 rc = launch_encode_rows(c, *plan, dev[j], n * S, dev[j] + k * S, n * S, S, 1, d16 ? d16 + j * n : nullptr,
@@ -132,7 +172,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
 
 // One group of a coalesced batch: same request key, i.e. same kind and shard size (and,
 // for reconstruct, the same survivor pattern and requested rows).
-void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
+void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, std::function<void()>* fin) {
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     const std::string& key = rq[0]->key;
     const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
@@ -143,7 +183,7 @@ void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb) {
     bool pinned = true;
     for (size_t j = 0; j < nb && pinned; j++) pinned = host_alias(rq[j]->out, n * S) != nullptr;
     if (pinned) {
-        const int rc = run_coalesced_in_place(c, rq, nb, S);
+        const int rc = run_coalesced_in_place(c, rq, nb, S, fin);
         for (size_t j = 0; j < nb; j++) rq[j]->rc = rc;
         return;
     }
@@ -210,6 +250,7 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
         x->opt_waves_per_cu = c->opt_waves_per_cu;
         x->opt_zero_copy = c->opt_zero_copy;
         x->opt_small_bytes = c->opt_small_bytes;
+        x->opt_coalesce_pipeline = c->opt_coalesce_pipeline;
         *rc = ensure_device(x);
     }
     if (*rc) {
@@ -220,7 +261,7 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
     return l;
 }
 
-void run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch) {
+std::function<void()> run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch) {
     const size_t n = size_t(c->n);
     // test hook (option "inject_host_fault"): this batch fails as a host allocation would
     for (int v = c->opt_inject_host_fault.load(); v > 0;)
@@ -229,18 +270,22 @@ void run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch
     rsmi_ctx* x = lane_context(c, lane, &rc);
     if (!x) {
         for (auto* r : batch) r->rc = rc;
-        return;
+        return nullptr;
     }
     std::map<std::string, std::vector<rsmi_ctx::CoalReq*>> groups;
     for (auto* r : batch) groups[r->key].push_back(r);
+    // a batch of one group that one launch sequence codes may be left in flight (pipelined)
+    std::function<void()> fin;
     for (auto& g : groups) {
         const std::string& key = g.first;
         const size_t S = std::stoull(key.substr(1, key.find(':') - 1));
         const size_t chunk = std::max<size_t>(1, (size_t(64) << 20) / (n * S));
+        const bool one = groups.size() == 1 && g.second.size() <= chunk;
         for (size_t j0 = 0; j0 < g.second.size(); j0 += chunk)
-            run_coalesced_group(x, g.second.data() + j0, std::min(chunk, g.second.size() - j0));
+            run_coalesced_group(x, g.second.data() + j0, std::min(chunk, g.second.size() - j0), one ? &fin : nullptr);
     }
     if (x != c) set_last_kernel(c, rsmi_last_kernel(x));
+    return fin;
 }
 
 // Queue a request and either wait for an executor or become one (group_commit.hpp).  The device
@@ -250,7 +295,7 @@ int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
     int rc = ensure_device_fast(c);
     if (rc) return rc;
     c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us, int(c->opt_coalesce_lanes),
-                   [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { run_coalesced(c, lane, batch); },
+                   [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { return run_coalesced(c, lane, batch); },
                    int(c->opt_coalesce_carry));
     return req.rc;
 }
@@ -314,7 +359,7 @@ int rsmi_warm(rsmi_ctx* c) try {
         if (!x) break;
         rsmi_ctx::CoalReq req{buf, B, buf, raw.data(), nullptr, "E" + std::to_string(S) + ":", RSMI_OK, false};
         rsmi_ctx::CoalReq* r = &req;
-        run_coalesced_group(x, &r, 1);
+        run_coalesced_group(x, &r, 1, nullptr);
         rc = req.rc;
     }
     (void)hipHostFree(buf);

@@ -94,6 +94,10 @@ struct CrcScratch {
 #ifndef RSMI_COALESCE_CARRY
 #define RSMI_COALESCE_CARRY 1
 #endif
+// default of option "coalesce_pipeline" (rsmi_coalesce.cpp)
+#ifndef RSMI_COALESCE_PIPELINE
+#define RSMI_COALESCE_PIPELINE 1
+#endif
 // the fewest blocks a coalesced group codes through the table kernels (R(shard) straight into
 // page-locked memory, no read-back dispatch): 1, a lone caller too (build macro for A/B variants;
 // 2 before profiles/r05/r/)
@@ -134,6 +138,14 @@ struct rsmi_ctx {
     size_t h_small_cap = 0;
     uint8_t* h_raw = nullptr;  // page-locked landing area of row CRCs read back by kernel (readback)
     size_t h_raw_cap = 0;
+    // pipelined coalesced batches (rsmi_coalesce.cpp): two page-locked landing areas of the table
+    // launches' R(shard) and an event per area, so a lane's next batch launches while this one is
+    // still coded
+    uint8_t* h_pipe[2] = {nullptr, nullptr};
+    size_t h_pipe_cap[2] = {0, 0};
+    hipEvent_t pipe_ev[2] = {nullptr, nullptr};
+    int pipe_slot = 0;
+    int opt_coalesce_pipeline = RSMI_COALESCE_PIPELINE;
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;  // diagnostics (rsmi_last_kernel), under lk_mu
@@ -240,9 +252,9 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
 int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
                        size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
-int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S);
-void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb);
-void run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch);
+int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S, std::function<void()>* fin);
+void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, std::function<void()>* fin);
+std::function<void()> run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch);
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req);
 int ensure_device_fast(rsmi_ctx* c);
 rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc);  // coalescing lane `lane`'s context (0: c)  // ensure_device without the context lock once the device is bound

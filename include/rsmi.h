@@ -365,7 +365,10 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * RSMI_ERR_HOST; default 0), "coalesce_lanes" (coalesced batches coded at once, 1-16, default
  * 2; every option but the test hook also applies to the lanes' child contexts), "coalesce_carry"
  * (batches a lane's executor goes on to when they are queued by the time its own completes,
- * before it hands the lane to a waiting caller, 0-16, default 1).  Kernel variants measured slower than the defaults are not
+ * before it hands the lane to a waiting caller, 0-16, default 1), "coalesce_pipeline" (1 =
+ * default: a coalesced batch coded by the table kernels is left in flight behind an event while
+ * the lane's next queued batch is launched behind it, and its callers return when the event
+ * completes; 0 = every batch synchronises before the next is launched).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);

@@ -877,6 +877,70 @@ static void test_group_commit_lanes() {
     }
 }
 
+// group_commit.hpp with pipelined batches: exec launches and returns a finisher, and the executor
+// launches the next queued batch before it finishes the current one.  Per lane, finishers run
+// once each in launch order, at most two batches of a lane are in flight, a request's caller
+// returns only after its batch's finisher ran, and a finisher's error reaches its requests.
+static void test_group_commit_pipelined() {
+    struct Req {
+        int id = 0, rc = -1;
+        bool done = false;
+        std::atomic<int> finished{0};
+    };
+    for (int lanes : {1, 2})
+    for (int carry : {1, 3}) {
+        rsmi::GroupCommit<Req> gc(-7);
+        std::mutex mu;
+        std::vector<std::vector<int>> launched(static_cast<size_t>(lanes)), finished(static_cast<size_t>(lanes));
+        std::atomic<int> seq{0}, bad{0}, deep{0};
+        std::vector<std::atomic<int>> inflight(static_cast<size_t>(lanes));
+        auto exec = [&](std::vector<Req*>& batch, int lane) -> std::function<void()> {
+            const int b = seq++;
+            {
+                std::lock_guard<std::mutex> g(mu);
+                launched[size_t(lane)].push_back(b);
+            }
+            if (++inflight[size_t(lane)] > 2) deep++;
+            for (Req* r : batch) r->rc = r->id;
+            std::vector<Req*> mine = batch;
+            return [&, b, lane, mine]() {
+                std::this_thread::sleep_for(std::chrono::microseconds(150));
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    finished[size_t(lane)].push_back(b);
+                }
+                for (Req* r : mine) {
+                    if (r->done) bad++;  // its caller may not have returned yet
+                    r->finished++;
+                    if (r->id % 37 == 5) r->rc = -3;  // an error found by the wait
+                }
+                inflight[size_t(lane)]--;
+            };
+        };
+        const int T = 12, per = 20;
+        std::vector<Req> reqs(size_t(T * per));
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                for (int i = t; i < T * per; i += T) {
+                    reqs[size_t(i)].id = i;
+                    gc.submit(reqs[size_t(i)], 6, 0, lanes, exec, carry);
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int i = 0; i < T * per; i++) {
+            const Req& r = reqs[size_t(i)];
+            CHECK(r.done && r.finished.load() == 1);
+            CHECK(r.rc == (i % 37 == 5 ? -3 : i));
+        }
+        CHECK(bad.load() == 0 && deep.load() == 0);
+        for (int l = 0; l < lanes; l++) CHECK(launched[size_t(l)] == finished[size_t(l)]);
+        CHECK(gc.calls() == uint64_t(T * per) && gc.batches() < gc.calls());
+        std::printf("group commit pipelined, %d lane(s), carry %d: %llu calls in %llu batches\n", lanes, carry,
+                    (unsigned long long)gc.calls(), (unsigned long long)gc.batches());
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (rs_oracle_selftest() != 0) {
@@ -893,6 +957,7 @@ int main(int argc, char** argv) {
     test_group_commit_exec_throws();
 #endif
     test_group_commit_lanes();
+    test_group_commit_pipelined();
     if (mode == "sanitize") {  // the Dag Node suite at 1/32 scale on the fake device layer
         g_big /= 32;
         g_leaf = g_leaf / 32 + 14;

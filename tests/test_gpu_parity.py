@@ -111,6 +111,37 @@ def test_reconstruct_patterns(k, m, S):
                     assert np.array_equal(got[:k], full[:k])
 
 
+@pytest.mark.parametrize("k,m", [(255, 1), (128, 128), (200, 56), (1, 255), (64, 64)])
+@pytest.mark.parametrize("S", [5, 300])
+def test_max_shard_counts(k, m, S):
+    """k + m at the 256-shard limit (erasure.go:22, klauspost's maximum): the encode of every
+    parity row (K > 16: the byte-granular kernel, outputs in launches of 4) and the rebuild of m
+    lost rows spread over data and parity, the data rows only, and a single lost row, against the
+    oracle."""
+    n = k + m
+    data = _rng_bytes(k * 7 + m + S, k * S).reshape(k, S)
+    full = np.zeros((n, S), dtype=np.uint8)
+    full[:k] = data
+    full[k:] = orc.encode(k, m, data)
+    with rsmi.Codec(k, m) as c:
+        par = bytearray(m * S)
+        c.encode(bytearray(data.tobytes()), par, S)
+        assert np.array_equal(np.frombuffer(bytes(par), dtype=np.uint8).reshape(m, S), full[k:]), (k, m)
+        rng = np.random.default_rng(n + S)
+        for lost in (sorted(rng.choice(n, size=m, replace=False).tolist()), [0], list(range(min(m, k)))):
+            present = [i not in lost for i in range(n)]
+            for data_only in (True, False):
+                buf = full.copy()
+                buf[lost] = 0xA5
+                flat = bytearray(buf.tobytes())
+                c.reconstruct(flat, S, present, data_only)
+                got = np.frombuffer(bytes(flat), dtype=np.uint8).reshape(n, S)
+                rc, want = orc.reconstruct(k, m, buf, present, data_only)
+                assert rc == 0
+                assert np.array_equal(got, want), (k, m, S, lost, data_only)
+                assert np.array_equal(got[:k], full[:k]), (k, m, S, lost)
+
+
 def test_reconstruct_errors():
     with rsmi.Codec(4, 2) as c:
         S = 16
