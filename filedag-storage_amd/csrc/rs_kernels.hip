@@ -74,6 +74,26 @@ __device__ __forceinline__ T* block_rows(const BasesArg<TB>& bases, T* p, uint32
         return p + uint64_t(blk) * bs;
 }
 
+// A table launch's completion release (BlockBases::done_flag; every workgroup calls it once, as
+// its last act, with all its waves): the workgroup's stores are complete once the barrier passes
+// (its workgroup-scope release waits for them), the fetch-add at system scope writes the XCD's L2
+// back before it counts, and the launch's last workgroup resets the counter for the next launch
+// and releases the flag.  A table without a flag (and every table-less instantiation) skips it.
+template <bool TB>
+__device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
+    if constexpr (TB) {
+        if (!bases.done_flag) return;  // kernel argument: uniform over the launch
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t old = __hip_atomic_fetch_add(bases.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (old + 1u == gridDim.x) {
+                __hip_atomic_store(bases.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(bases.done_flag, bases.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
 // K inputs, MT (<= 4) outputs, one 16-byte chunk per lane per row.
 // NT: cache policy, 1 = nontemporal loads and stores (write-heavy tiles), 2 = nontemporal
 // loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.
@@ -528,6 +548,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #endif
     if (u >= nunits) {
         stage();
+        if constexpr (RSMI_FUSED_COOP) launch_done<TB>(bases);
         return;
     }
     const uint32_t blk = u / upb;
@@ -857,6 +878,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             __syncthreads();
             if (!s_last) {
                 if constexpr (kDefer) if (dch != ~0u) store_out(dch, dwin, dacc);
+                launch_done<TB>(bases);
                 return;
             }
             __threadfence();
@@ -864,6 +886,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
 #else
         if (u - blk * upb != upb - 1u) {
             if constexpr (kDefer) if (dch != ~0u) store_out(dch, dwin, dacc);
+            launch_done<TB>(bases);
             return;
         }
 #endif
@@ -874,6 +897,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
             crc16_combine_rows(reinterpret_cast<const uint16_t*>(s_p4), rb, upb, NACC, NSH, sh,
                                raw + uint64_t(blk) * NSH, p, lane);
     }
+    launch_done<TB>(bases);
 #else
 #pragma unroll
     for (int a = 0; a < NACC; a++) record(a, cacc[a]);

@@ -46,9 +46,16 @@ struct RsPlanDev {
 // table travels in the kernel arguments (one scalar load per wave, no copy to the device); a
 // group of more blocks takes several launches.  The kernels' table-less instantiations take
 // NoBases in its place, an unused empty argument that leaves their code unchanged.
+// done_flag (the fused encode + CRC-16 with its combine inside, rs_fused_mfma_kernel TB INL): the
+// launch's workgroups count themselves in done_ctr as they finish, and the last one releases
+// done_seq into the page-locked done_flag, so the caller sees the group's end by polling it
+// instead of synchronising the stream (rsmi_coalesce.cpp)
 constexpr int kTableBlocks = 64;
 struct BlockBases {
     uint64_t b[kTableBlocks];
+    uint32_t* done_ctr = nullptr;
+    uint32_t* done_flag = nullptr;
+    uint32_t done_seq = 0, done_pad = 0;
 };
 struct NoBases {};
 template <bool TB>

@@ -42,6 +42,66 @@ static uint8_t* pipe_area(rsmi_ctx* c, int slot, size_t bytes) {
     return c->h_pipe[slot];
 }
 
+// The context's two completion flags (caller holds ctx->mu): page-locked, 64 bytes apart, with
+// device counters zeroed on `st` before first use
+int done_area(rsmi_ctx* c, hipStream_t st) {
+    if (c->h_done) return RSMI_OK;
+    void* h = nullptr;
+    HIP_TRY(pinned_alloc(&h, 128));
+    std::memset(h, 0, 128);
+    uint8_t* hd = host_alias(h, 128);
+    void* d = nullptr;
+    hipError_t e = hd ? hipMalloc(&d, 128) : hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipMemsetAsync(d, 0, 128, st);  // stream-ordered before the kernels
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        (void)hipHostFree(h);
+        return hip_status(e);
+    }
+    c->h_done = static_cast<uint32_t*>(h);
+    c->h_done_dev = reinterpret_cast<uint32_t*>(hd);
+    c->d_done_ctr = static_cast<uint32_t*>(d);
+    return RSMI_OK;
+}
+
+// Arm a table launch's completion flag (caller holds ctx->mu): the next sequence number, its
+// slot's counter and flag in tb; the host view of the flag is done_flag(c, seq)
+int arm_flag(rsmi_ctx* c, hipStream_t st, BlockBases& tb, uint32_t& seq) {
+    int rc = done_area(c, st);
+    if (rc) return rc;
+    if (++c->done_seq == 0) ++c->done_seq;  // 0 is the flags' first value
+    seq = c->done_seq;
+    tb.done_ctr = c->d_done_ctr + (seq & 1u) * 16u;
+    tb.done_flag = c->h_done_dev + (seq & 1u) * 16u;
+    tb.done_seq = seq;
+    return RSMI_OK;
+}
+const uint32_t* done_flag(const rsmi_ctx* c, uint32_t seq) { return c->h_done + (seq & 1u) * 16u; }
+
+// Poll a table launch's completion flag until it holds seq or a later sequence number: a slot's
+// flag is released by launches on the context's one stream in sequence order, so a later number
+// (a synchronous group of the next batch, queued behind this one) means this launch is done too.
+// The poll touches nothing but the flag (a stream or event query every 20 us measured +2 us on a
+// 256 KiB call and slowed concurrent lanes' launches); after 200 us the wait blocks in the event
+// or stream synchronisation instead, which also reports a failed launch, and a launch that
+// finished without its flag is an error.
+bool flag_reached(const uint32_t* flag, uint32_t seq) {
+    return int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - seq) >= 0;
+}
+int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st, hipEvent_t ev) {
+    using clk = std::chrono::steady_clock;
+    const auto until = clk::now() + std::chrono::microseconds(200);
+    for (uint32_t i = 0;; i++) {
+        if (flag_reached(flag, seq)) return RSMI_OK;
+        if ((i & 63u) == 63u && clk::now() > until) break;
+        __builtin_ia32_pause();
+    }
+    const hipError_t e = ev ? hipEventSynchronize(ev) : hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_status(e);
+    return flag_reached(flag, seq) ? RSMI_OK : RSMI_ERR_DEVICE;
+}
+
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
 // run_coalesced_group): one launch over a table of the blocks' bases for up to kTableBlocks
 // requests (BlockBases, the table kernels of the BASELINE shapes), else one launch per request,
@@ -114,13 +174,20 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             h16_dev = reinterpret_cast<uint32_t*>(host_alias(h, nb * n * 4));
             if (!h16_dev) return RSMI_ERR_DEVICE;
         }
+        // a group of one table launch of the fused encode + CRC-16 signals its end through a
+        // completion flag (BlockBases::done_flag), polled instead of synchronising the stream
+        const uint32_t* flag = nullptr;
+        uint32_t seq = 0;
         for (size_t j0 = 0; j0 < nb && table; j0 += size_t(kTableBlocks)) {
             const size_t cnt = std::min(size_t(kTableBlocks), nb - j0);
             BlockBases tb;
             for (size_t i = 0; i < cnt; i++) tb.b[i] = uint64_t(reinterpret_cast<uintptr_t>(dev[j0 + i]));
             uint8_t* const par = reinterpret_cast<uint8_t*>(uintptr_t(k * S));  // offset of the parity rows
+            const bool arm = enc && want16 && c->opt_coalesce_flag && nb <= size_t(kTableBlocks);
+            if (arm && (rc = arm_flag(c, st, tb, seq))) return fail(rc);
+            bool armed = false;
             if (enc && want16)
-                rc = launch_plan_crc(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, h16_dev + j0 * n, st, &tb);
+                rc = launch_plan_crc(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, h16_dev + j0 * n, st, &tb, &armed);
             else if (enc)
                 rc = launch_plan(c, *plan, nullptr, S, 0, par, S, 0, S, cnt, st, nullptr, &tb);
             else
@@ -131,6 +198,7 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             }
             if (rc) return fail(rc);
             launched = true;
+            if (armed) flag = done_flag(c, seq);
         }
         if (!table) h16 = nullptr;  // a launch per request: its R(shard) come back by read-back
         if (pipe && table) {
@@ -139,10 +207,10 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
             c->pipe_slot ^= 1;
             std::vector<rsmi_ctx::CoalReq*> reqs(rq, rq + nb);
             hipEvent_t ev = c->pipe_ev[slot];
-            *fin = [reqs = std::move(reqs), ev, h16, n]() {
-                const hipError_t w = hipEventSynchronize(ev);
+            *fin = [reqs = std::move(reqs), ev, h16, n, flag, seq, st]() {
+                const int w = flag ? wait_flag(flag, seq, st, ev) : hip_status(hipEventSynchronize(ev));
                 for (size_t j = 0; j < reqs.size(); j++) {
-                    if (w != hipSuccess) reqs[j]->rc = hip_status(w);
+                    if (w != RSMI_OK) reqs[j]->rc = w;
                     else if (reqs[j]->raw && h16) std::memcpy(reqs[j]->raw, h16 + j * n, n * 4);
                 }
             };
@@ -159,7 +227,11 @@ int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb,
         }
         const uint32_t *g16 = h16, *g32 = nullptr;
         if (!h16 && (rc = readback(c, d16, d32, nb * n * 4, st, g16, g32))) return fail(rc);
-        HIP_TRY(hipStreamSynchronize(st));
+        if (flag) {
+            if ((rc = wait_flag(flag, seq, st, nullptr))) return fail(rc);
+        } else {
+            HIP_TRY(hipStreamSynchronize(st));
+        }
         if (want16) std::memcpy(r16.data(), g16, nb * n * 4);
         if (want32) std::memcpy(r32.data(), g32, nb * n * 4);
     }
@@ -251,6 +323,7 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
         x->opt_zero_copy = c->opt_zero_copy;
         x->opt_small_bytes = c->opt_small_bytes;
         x->opt_coalesce_pipeline = c->opt_coalesce_pipeline;
+        x->opt_coalesce_flag = c->opt_coalesce_flag;
         *rc = ensure_device(x);
     }
     if (*rc) {

@@ -408,6 +408,8 @@ void rsmi_close(rsmi_ctx* c) {
             if (c->h_coal) (void)hipHostFree(c->h_coal);
             if (c->h_small) (void)hipHostFree(c->h_small);
             if (c->h_raw) (void)hipHostFree(c->h_raw);
+            if (c->h_done) (void)hipHostFree(c->h_done);
+            if (c->d_done_ctr) (void)hipFree(c->d_done_ctr);
             for (int i = 0; i < 2; i++) {
                 if (c->h_pipe[i]) (void)hipHostFree(c->h_pipe[i]);
                 if (c->pipe_ev[i]) (void)hipEventDestroy(c->pipe_ev[i]);
@@ -513,6 +515,9 @@ int apply_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "coalesce_pipeline")) {
         if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_pipeline = int(value);
+    } else if (!std::strcmp(key, "coalesce_flag")) {
+        if (value < 0 || value > 1) return RSMI_ERR_INVALID_ARG;
+        c->opt_coalesce_flag = int(value);
     } else {
         return RSMI_ERR_INVALID_ARG;
     }

@@ -150,7 +150,8 @@ int launch_rebuilt_crcs(rsmi_ctx* c, const uint8_t* base, uint64_t rpitch, uint6
 // (callers then run the separate pass).
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                     size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
-                    const BlockBases* tb) {
+                    const BlockBases* tb, bool* armed) {
+    if (armed) *armed = false;
     if (plan.tiles.size() != 1 || plan.tiles[0].K > 16) return RSMI_ERR_INVALID_ARG;
     // tb: a table of block bases (in / out are offsets from each), one launch of at most
     // kTableBlocks blocks on the matrix-core fold; callers fall back to a launch per block
@@ -220,7 +221,15 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
             uint32_t* cb = inline_combine ? sc.d_fctr + b0 : nullptr;
             uint32_t* rw = raw + b0 * nsh;
             NoBases nob;
-            void* bases = tb ? const_cast<BlockBases*>(tb) : static_cast<void*>(&nob);
+            // a table's completion flag is armed only when this one launch is the whole job (the
+            // combine inside): a separate combine launch would still be writing R after it
+            BlockBases tbl_args;
+            if (tb) {
+                tbl_args = *tb;
+                if (!inline_combine || nblocks > max_blocks) tbl_args.done_flag = nullptr;
+                if (armed) *armed = tbl_args.done_flag != nullptr;
+            }
+            void* bases = tb ? static_cast<void*>(&tbl_args) : static_cast<void*>(&nob);
             void* args[] = {&pd,    &inb,   &outb,   &ibs, &irs, &obs, &ors, &S32, &cpb32,
                             &tpb32, &upb32, &nunits, &ctb, &rb,  &cb,  &rw,  &sh,  bases};
             const uint32_t wgs = RSMI_FUSED_COOP ? nunits : (nunits + kWG / kWave - 1) / (kWG / kWave);

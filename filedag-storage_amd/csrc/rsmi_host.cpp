@@ -145,13 +145,26 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
     uint32_t* hraw32 = raw32_out ? reinterpret_cast<uint32_t*>(hs + in_sz + out_sz + raw_sz) : nullptr;
     if (!in || !out) return RSMI_ERR_DEVICE;
     int rc;
+    uint32_t seq = 0;
+    bool armed = false;
     if (raw_out && S >= 16 && k <= 16 && m <= 4) {
         // fused: the encode folds every row it reads and writes into per-tile CRC records (the
         // shard bytes cross PCIe once), then one wave per block combines them into R(row) and
         // stores it straight into the page-locked staging
         uint32_t* draw = reinterpret_cast<uint32_t*>(host_alias(hraw, raw_sz));
         if (!draw) return RSMI_ERR_DEVICE;
-        if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, draw, st))) return rc;
+        // one block (a lone DagNode.Put): the table form with a single zero base (in / out stay
+        // absolute) and its completion flag, polled below instead of synchronising the stream
+        if (nblocks == 1 && !raw32_out && c->opt_coalesce_flag) {
+            BlockBases tb;
+            tb.b[0] = 0;
+            if ((rc = arm_flag(c, st, tb, seq))) return rc;
+            rc = launch_plan_crc(c, plan, in, S, in_bs, out, S, out_bs, S, 1, draw, st, &tb, &armed);
+            if (rc == RSMI_ERR_INVALID_ARG) rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, 1, draw, st);
+            if (rc) return rc;
+        } else if ((rc = launch_encode_crc(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, draw, st))) {
+            return rc;
+        }
     } else {
         if ((rc = launch_plan(c, plan, in, S, in_bs, out, S, out_bs, S, nblocks, st))) return rc;
         if (raw_out) {  // S < 16, k > 16 or m > 4: a separate CRC pass over the rows where they lie
@@ -175,7 +188,14 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
         if (!d32) return RSMI_ERR_DEVICE;
         if ((rc = repitch(d32, raw32_sz, reinterpret_cast<uint8_t*>(cr), raw32_sz, raw32_sz, 1, st))) return rc;
     }
-    HIP_TRY(hipStreamSynchronize(st));
+    if (armed) {
+        if ((rc = wait_flag(done_flag(c, seq), seq, st, nullptr))) {
+            (void)hipStreamSynchronize(st);
+            return rc;
+        }
+    } else {
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     if (stage_out)
         for (size_t b = 0; b < nblocks; b++) std::memcpy(parity + b * pbs, hout + b * m * S, m * S);
     if (raw_out) std::memcpy(raw_out, hraw, raw_sz);

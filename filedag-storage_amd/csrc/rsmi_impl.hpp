@@ -94,6 +94,10 @@ struct CrcScratch {
 #ifndef RSMI_COALESCE_CARRY
 #define RSMI_COALESCE_CARRY 1
 #endif
+// default of option "coalesce_flag" (rsmi_coalesce.cpp)
+#ifndef RSMI_COALESCE_FLAG
+#define RSMI_COALESCE_FLAG 1
+#endif
 // default of option "coalesce_pipeline" (rsmi_coalesce.cpp)
 #ifndef RSMI_COALESCE_PIPELINE
 #define RSMI_COALESCE_PIPELINE 1
@@ -146,6 +150,14 @@ struct rsmi_ctx {
     hipEvent_t pipe_ev[2] = {nullptr, nullptr};
     int pipe_slot = 0;
     int opt_coalesce_pipeline = RSMI_COALESCE_PIPELINE;
+    // completion flags of table launches (BlockBases::done_flag): two page-locked flags (64 bytes
+    // apart; slot = sequence number & 1, at most two launches of a context in flight) and their
+    // device counters
+    uint32_t* h_done = nullptr;
+    uint32_t* h_done_dev = nullptr;
+    uint32_t* d_done_ctr = nullptr;
+    uint32_t done_seq = 0;
+    int opt_coalesce_flag = RSMI_COALESCE_FLAG;
     long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
     long opt_coalesce_max = 256;  // blocks per coalesced batch
     std::string last_kernel;  // diagnostics (rsmi_last_kernel), under lk_mu
@@ -248,10 +260,15 @@ int launch_encode_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t i
                              size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st);
 int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_rs, size_t in_bs, uint8_t* out,
                     size_t out_rs, size_t out_bs, size_t S, size_t nblocks, uint32_t* raw, hipStream_t st,
-                    const BlockBases* tb = nullptr);
+                    const BlockBases* tb = nullptr, bool* armed = nullptr);
 int launch_encode_rows(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_bs, uint8_t* out, size_t out_bs,
                        size_t S, size_t nblocks, uint32_t* d16, uint32_t* d32, hipStream_t st);
 uint8_t* coal_stage(rsmi_ctx* c, size_t need);
+// completion flags of table launches (rsmi_coalesce.cpp): arm one in tb (caller holds ctx->mu),
+// its host view, and the poll that replaces the stream (or event) synchronisation
+int arm_flag(rsmi_ctx* c, hipStream_t st, BlockBases& tb, uint32_t& seq);
+const uint32_t* done_flag(const rsmi_ctx* c, uint32_t seq);
+int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st, hipEvent_t ev);
 int run_coalesced_in_place(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, size_t S, std::function<void()>* fin);
 void run_coalesced_group(rsmi_ctx* c, rsmi_ctx::CoalReq* const* rq, size_t nb, std::function<void()>* fin);
 std::function<void()> run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx::CoalReq*>& batch);

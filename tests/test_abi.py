@@ -164,7 +164,8 @@ def test_new_options_and_stats_validate():
         for key, good, bad in [(b"waves_per_cu", 8, -1), (b"coalesce_us", 50, -1), (b"coalesce_max", 16, 0),
                                (b"crc16_fold", 0, 2), (b"crc16_fused_fold", 0, 2), (b"coalesce_lanes", 4, 0),
                                (b"coalesce_lanes", 16, 17), (b"coalesce_carry", 0, -1), (b"coalesce_carry", 16, 17),
-                               (b"coalesce_pipeline", 0, -1), (b"coalesce_pipeline", 1, 2)]:
+                               (b"coalesce_pipeline", 0, -1), (b"coalesce_pipeline", 1, 2),
+                               (b"coalesce_flag", 0, -1), (b"coalesce_flag", 1, 2)]:
             assert L.rsmi_set_option(c._h, key, good) == rsmi.OK, key
             assert L.rsmi_set_option(c._h, key, bad) == rsmi.ErrInvalidArg, key
         assert c.stat("coalesced_calls") == 0 and c.stat("coalesced_batches") == 0

@@ -1058,3 +1058,45 @@ def test_fused_mfma_split_every_tail(k, m, mis):
                 rows = list(data[b]) + list(want[b])
                 for i in range(n):
                     assert rsmi.crc16_entry(b"", int(r[b, i]), S) == orc.crc16_ibm(rows[i].tobytes()), (S, fill, b, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flag", [1, 0])
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 4096), (16, 4, 1 << 20)])
+def test_coalesced_lone_calls_completion_flag(k, m, B, flag):
+    """A lone caller's coalesced encode + CRC-16, and a one-block in-place host call, is one table
+    launch of the fused kernel whose last workgroup releases the context's completion flag (option
+    coalesce_flag 1, BlockBases::done_flag; 0: the stream synchronisation).  150 calls back to back
+    on fresh data, the two kinds alternating (the two flag slots and their counters reused ~75
+    times each), every shard and R(shard) against the oracle."""
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    p = L.rsmi_host_alloc(n * S)
+    assert p
+    try:
+        sh = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S)
+        rng = np.random.default_rng(B + flag)
+        raw = (ctypes.c_uint32 * n)()
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_flag", flag)
+            c.warm()
+            for it in range(150):
+                block = rng.integers(0, 256, size=B, dtype=np.uint8)
+                full = orc.split(k, m, block.tobytes())
+                full[k:] = orc.encode_fast(k, m, full[None, :k], threads=4)[0]
+                flat = sh.reshape(-1)
+                flat[:] = 0xA5
+                flat[:B] = block
+                if it % 2:  # the lone in-place host call (encode_small) takes the same flagged launch
+                    flat[B:k * S] = 0  # Split's zero padding (the coalesced call writes it itself)
+                    c.encode_batch_host_crcs_ptr(p, n * S, p + k * S, n * S, S, 1, ctypes.addressof(raw), None)
+                else:
+                    assert L.rsmi_encode_block_coalesced(c._h, p, B, p, raw) == 0
+                assert np.array_equal(sh, full), it
+                if it % 30 == 0:
+                    assert ",TB" in c.last_kernel(), c.last_kernel()
+                    for r in range(n):
+                        assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(full[r].tobytes()), (it, r)
+    finally:
+        L.rsmi_host_free(p)

@@ -23,6 +23,7 @@
 #   latency          per-block call latencies (tools/latency)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
+#   threads_flag     1 and 16 threads, option coalesce_flag off / on alternated (THREADS_CFG=flag)
 #   group_sweep      one thread, in-place host calls of 1..256 blocks back to back (tools/latency --group-sweep)
 #   threads_traced   the same under rocprofv3 --kernel-trace (crash report: tools/latency.cpp)
 set -o pipefail
@@ -105,6 +106,9 @@ threads)
 threads_pipe)
   THREADS_CFG=pipe timeout -k 10 400 ./tools/build/latency --threads > $O/threads_pipe.txt 2>&1 || fail threads_pipe $O/threads_pipe.txt
   cat $O/threads_pipe.txt ;;
+threads_flag)
+  THREADS_CFG=flag timeout -k 10 400 ./tools/build/latency --threads > $O/threads_flag.txt 2>&1 || fail threads_flag $O/threads_flag.txt
+  cat $O/threads_flag.txt ;;
 group_sweep)
   timeout -k 10 300 ./tools/build/latency --group-sweep > $O/group_sweep.txt 2>&1 || fail group_sweep $O/group_sweep.txt
   cat $O/group_sweep.txt ;;

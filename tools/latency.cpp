@@ -149,7 +149,7 @@ static void install_crash_handler() {
 // place in its own page-locked buffer (block == shards_out, Split by the thread): the coalesced
 // groups' throughput, GiB/s of block payload, and how many groups they formed
 static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lanes = 1, int clanes = 2, int carry = 1,
-                              int wait_us = 0, bool nt = false, int pipe = 1) {
+                              int wait_us = 0, bool nt = false, int pipe = 1, int flag = 1) {
     // lanes > 1: the threads spread over that many contexts (thread t on context t % lanes);
     // clanes: each context's coalescing lanes (option "coalesce_lanes")
     std::vector<rsmi_ctx*> cs(static_cast<size_t>(lanes));
@@ -157,6 +157,7 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
         if (rsmi_open(k, m, 0, &x) != RSMI_OK) std::exit(2);
         if (rsmi_set_option(x, "coalesce_lanes", clanes) != RSMI_OK || rsmi_set_option(x, "coalesce_carry", carry) != RSMI_OK ||
             rsmi_set_option(x, "coalesce_us", wait_us) != RSMI_OK || rsmi_set_option(x, "coalesce_pipeline", pipe) != RSMI_OK ||
+            rsmi_set_option(x, "coalesce_flag", flag) != RSMI_OK ||
             rsmi_warm(x) != RSMI_OK)
             std::exit(2);
     }
@@ -195,8 +196,8 @@ static void coalesced_threads(int k, int m, size_t B, int T, int calls, int lane
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
     const long calls_n = stat("coalesced_calls") - c0, batches = stat("coalesced_batches") - b0;
     std::printf("RS(%d,%d) B=%8zu  %2d threads x %d coalesced encodes + CRC-16 in place, %d context(s) x %d lane(s), "
-                "carry %d, wait %d us%s, pipeline %d: %7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls,
-                lanes, clanes, carry, wait_us, nt ? ", streaming copies" : "", pipe,
+                "carry %d, wait %d us%s, pipeline %d, flag %d: %7.2f GiB/s, %ld calls in %ld groups (%.2f; last kernel %s)\n", k, m, B, T, calls,
+                lanes, clanes, carry, wait_us, nt ? ", streaming copies" : "", pipe, flag,
                 double(T) * calls * B / sec / 1073741824.0, calls_n, batches, double(batches) / double(calls_n),
                 rsmi_last_kernel(c));
     for (auto* p : bufs) rsmi_host_free(p);
@@ -248,6 +249,19 @@ int main(int argc, char** argv) {
         // (contexts, lanes, carry, coalesce_us, streaming copies); THREADS_CFG=quick: the first
         // (default) configuration and its variants at 16 threads only
         const bool quick = std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "quick");
+        if (std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "flag")) {
+            // option coalesce_flag off / on: 1 thread (a lone caller's in-place call) and 16 threads,
+            // alternated twice
+            for (int rep = 0; rep < 2; rep++)
+                for (int T : {1, 16})
+                    for (int flag : {0, 1})
+                        for (auto shape : {std::make_tuple(2, 1, size_t(262144)), std::make_tuple(10, 4, size_t(262144)),
+                                           std::make_tuple(10, 4, size_t(4096)), std::make_tuple(16, 4, size_t(4194304))})
+                            coalesced_threads(std::get<0>(shape), std::get<1>(shape), std::get<2>(shape), T,
+                                              std::get<2>(shape) > (size_t(1) << 20) ? 16 : (T == 1 ? 400 : 128), 1, 2, 1, 0,
+                                              false, 1, flag);
+            return 0;
+        }
         if (std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "pipe")) {
             // option coalesce_pipeline off / on at 16 threads, (lanes, carry) pairs, alternated twice
             for (int rep = 0; rep < 2; rep++)
