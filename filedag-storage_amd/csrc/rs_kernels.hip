@@ -153,7 +153,16 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     uint32_t wg = blockIdx.x;
     if (UA && (gridDim.x & 7u) == 0u) wg = (wg & 7u) * (gridDim.x >> 3) + (wg >> 3);
     uint32_t t = wg * kWavesPerWG + wid;
-    if (t >= ntiles) return;
+    if constexpr (TB) {
+        // a table launch may release a completion flag (launch_done, as every workgroup's last
+        // act): its workgroups leave together, waves past the last tile skip the tile loop
+        if (wg * kWavesPerWG >= ntiles) {
+            launch_done<TB>(bases);
+            return;
+        }
+    } else {
+        if (t >= ntiles) return;
+    }
 
     constexpr int P = rows_in_flight<K, MT>();
     uint64_t in_off[K], out_off[MT];
@@ -403,6 +412,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             blk++;
         }
     }
+    launch_done<TB>(bases);
 }
 
 typedef int mfma_v8i __attribute__((ext_vector_type(8)));

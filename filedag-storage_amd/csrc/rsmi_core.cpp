@@ -223,7 +223,8 @@ uintptr_t table_alignment(const BlockBases* tb, uint64_t nblocks) {
 
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
-                const CrcFuse* fuse, const BlockBases* tb) {
+                const CrcFuse* fuse, const BlockBases* tb, bool* armed) {
+    if (armed) *armed = false;
     if (nblocks == 0 || S == 0) return RSMI_OK;
     // tb: a table of block bases (in / out are offsets from each), one launch of at most
     // kTableBlocks blocks, table kernels only (callers fall back to a launch per block)
@@ -277,7 +278,14 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
                 uint32_t* crec = fuse ? fuse->rec + b0 * rec_per_block : nullptr;
                 uint32_t* ctail = fuse && fuse->tail ? fuse->tail + b0 * uint64_t(t.K + t.MT) : nullptr;
                 NoBases nob;
-                void* bases = tb ? const_cast<BlockBases*>(tb) : static_cast<void*>(&nob);
+                // a table's completion flag is armed only when this one launch is the whole job
+                BlockBases tbl_args;
+                if (tb) {
+                    tbl_args = *tb;
+                    if (plan.tiles.size() != 1 || nblocks > max_blocks) tbl_args.done_flag = nullptr;
+                    if (armed) *armed = tbl_args.done_flag != nullptr;
+                }
+                void* bases = tb ? static_cast<void*>(&tbl_args) : static_cast<void*>(&nob);
                 void* args[] = {&pd,    &inb,   &outb,   &in_bs, &in_rs, &out_bs, &out_rs, &S32,
                                 &cpb32, &tpb32, &ntiles, &ctbl,  &crec,  &ctail, bases};
                 const uint64_t wgs = std::min<uint64_t>((ntiles + wpg - 1) / wpg, uint64_t(wg_cap));

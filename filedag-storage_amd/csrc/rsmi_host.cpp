@@ -376,7 +376,20 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
         dbs = n * S;
         if (!dev) return RSMI_ERR_DEVICE;
     }
-    int rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
+    int rc;
+    uint32_t seq = 0;
+    bool armed = false;
+    if (nblocks == 1 && !raw16 && !raw32 && c->opt_coalesce_flag) {
+        // one block, no checksums (a lone repair or degraded read): the table form with a single
+        // zero base and its completion flag, polled below instead of synchronising the stream
+        BlockBases tb;
+        tb.b[0] = 0;
+        if ((rc = arm_flag(c, st, tb, seq))) return rc;
+        rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, 1, st, nullptr, &tb, &armed);
+        if (rc == RSMI_ERR_INVALID_ARG) rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
+    } else {
+        rc = launch_plan(c, plan, dev, S, dbs, dev, S, dbs, S, nblocks, st);
+    }
     if (rc) return rc;
     const size_t raw_sz = nblocks * n * 4;
     if (raw16 && (rc = reserve(c->d_crc, c->crc_cap, raw_sz))) return rc;
@@ -387,7 +400,14 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
         return rc;
     const uint32_t *h16, *h32;
     if ((rc = readback(c, d16, d32, raw_sz, st, h16, h32))) return rc;
-    HIP_TRY(hipStreamSynchronize(st));
+    if (armed) {
+        if ((rc = wait_flag(done_flag(c, seq), seq, st, nullptr))) {
+            (void)hipStreamSynchronize(st);
+            return rc;
+        }
+    } else {
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     if (raw16) std::memcpy(raw16, h16, raw_sz);
     if (raw32) std::memcpy(raw32, h32, raw_sz);
     if (hs)

@@ -214,7 +214,7 @@ int auto_cache_policy(int K, int MT);
 // the table kernels only: RSMI_ERR_INVALID_ARG when the shape has none, callers then launch per block)
 int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs, uint64_t in_bs, uint8_t* out,
                 uint64_t out_rs, uint64_t out_bs, uint64_t S, uint64_t nblocks, hipStream_t stream,
-                const CrcFuse* fuse = nullptr, const BlockBases* tb = nullptr);
+                const CrcFuse* fuse = nullptr, const BlockBases* tb = nullptr, bool* armed = nullptr);
 uintptr_t table_alignment(const BlockBases* tb, uint64_t nblocks);  // OR of the table's first nblocks bases
 void set_last_kernel(rsmi_ctx* c, const std::string& label);
 CrcScratch& crc_scratch(rsmi_ctx* c, hipStream_t st);  // caller holds ctx->mu

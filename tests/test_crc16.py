@@ -1068,7 +1068,8 @@ def test_coalesced_lone_calls_completion_flag(k, m, B, flag):
     launch of the fused kernel whose last workgroup releases the context's completion flag (option
     coalesce_flag 1, BlockBases::done_flag; 0: the stream synchronisation).  150 calls back to back
     on fresh data, the two kinds alternating (the two flag slots and their counters reused ~75
-    times each), every shard and R(shard) against the oracle."""
+    times each), every shard and R(shard) against the oracle; after each encode a lone repair and a
+    lone degraded read rebuild lost rows in place through the plain table kernel and its flag."""
     n = k + m
     S = (B + k - 1) // k
     L = rsmi.lib()
@@ -1098,5 +1099,19 @@ def test_coalesced_lone_calls_completion_flag(k, m, B, flag):
                     assert ",TB" in c.last_kernel(), c.last_kernel()
                     for r in range(n):
                         assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(full[r].tobytes()), (it, r)
+                # a lone repair (the rows asked for) and a lone degraded read (the data rows) rebuilt
+                # in place: the plain table kernel with the flag
+                lost = [it % n, (it + 3) % n] if m > 1 else [it % n]
+                present = [i not in lost for i in range(n)]
+                sh[lost] = 0xEE
+                c.reconstruct_rows_batch_host_ptr(p, n * S, S, 1, present, [i in lost for i in range(n)])
+                assert np.array_equal(sh, full), (it, lost)
+                sh[lost] = 0xEE
+                c.reconstruct_batch_host_ptr(p, n * S, S, 1, present, True)
+                for r in range(n):
+                    if r in lost and r >= k:
+                        assert (sh[r] == 0xEE).all(), (it, r)
+                    else:
+                        assert np.array_equal(sh[r], full[r]), (it, r)
     finally:
         L.rsmi_host_free(p)
