@@ -1517,6 +1517,12 @@ static void fill_tb_fused(FastKernelTable& t) {
     t.fused_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, false, true, true>);
     t.fused_ua_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true, true, true>);
 }
+template <int K, int MT>
+static void fill_tb_fused_inl(FastKernelTable& t) {
+    constexpr int NT = auto_nt(K, MT);
+    t.fused_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, false, true, true>);
+    t.fused_ua_inl_tb[K][MT] = reinterpret_cast<void*>(&rs_fused_mfma_kernel<K, MT, NT, kFusedWavesPerSimd, true, true, true>);
+}
 template <int K>
 static void fill_tb_k(FastKernelTable& t) {
     fill_tb_km<K, 1>(t);
@@ -1533,6 +1539,15 @@ void fill_table_kernels(FastKernelTable& t) {
     fill_tb_fused<4, 2>(t);
     fill_tb_fused<10, 4>(t);
     fill_tb_fused<16, 4>(t);
+    // the verified reconstructs of a lone degraded read (the survivors' R(row) with the rebuilt
+    // rows, one block: the in-kernel combine and its completion flag) of fewer rows than m
+    fill_tb_fused_inl<4, 1>(t);
+    fill_tb_fused_inl<10, 1>(t);
+    fill_tb_fused_inl<10, 2>(t);
+    fill_tb_fused_inl<10, 3>(t);
+    fill_tb_fused_inl<16, 1>(t);
+    fill_tb_fused_inl<16, 2>(t);
+    fill_tb_fused_inl<16, 3>(t);
 }
 #else
 

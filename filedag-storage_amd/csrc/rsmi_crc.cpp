@@ -171,8 +171,10 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
     const FastKernelTable& kt = fast_kernels();
     void* mfma_fn = aligned ? (tb ? kt.fused_tb : kt.fused)[tile.K][tile.MT]
                             : ua ? (tb ? kt.fused_ua_tb : kt.fused_ua)[tile.K][tile.MT] : nullptr;
-    if (tb && !mfma_fn) return RSMI_ERR_INVALID_ARG;
-    if (mfma_fn && c->opt_fused_fold == 1) {
+    // some table shapes exist only in the in-kernel-combine form (a lone verified reconstruct)
+    void* tb_inl = !tb ? nullptr : aligned ? kt.fused_inl_tb[tile.K][tile.MT] : ua ? kt.fused_ua_inl_tb[tile.K][tile.MT] : nullptr;
+    if (tb && !mfma_fn && !tb_inl) return RSMI_ERR_INVALID_ARG;
+    if ((mfma_fn || tb_inl) && c->opt_fused_fold == 1) {
         // the fold on the matrix cores (rs_fused_mfma_kernel): a unit of 4 tiles per workgroup,
         // then the records' combine
         const size_t upb = (tpb + kFusedUnitTiles - 1) / kFusedUnitTiles;
@@ -197,6 +199,7 @@ int launch_plan_crc(rsmi_ctx* c, const Plan& plan, const uint8_t* in, size_t in_
                                : (tb ? kt.fused_ua_inl_tb : kt.fused_ua_inl)[tile.K][tile.MT];
         const bool inline_combine = RSMI_FUSED_COOP && inl_fn && nblocks * upb <= kFusedInlineUnits;
         if (inline_combine) fn = inl_fn;
+        if (!fn) return RSMI_ERR_INVALID_ARG;  // a table shape without the two-launch form, too big to combine inside
         // per-block unit counters of the inline combine: zeroed once when allocated, and every
         // launch leaves them at zero again (atomicInc wraps at the block's last unit)
         if (inline_combine && sc.fctr_cap < nblocks) {

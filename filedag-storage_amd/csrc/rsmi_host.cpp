@@ -658,12 +658,39 @@ int rsmi_reconstruct_batch_host_verify(rsmi_ctx* c, uint8_t* shards, size_t bloc
             const size_t nsh = size_t(plan->tiles.empty() ? 0 : plan->tiles[0].K + plan->tiles[0].MT);
             if ((rc = reserve(c->d_crc, c->crc_cap, nblocks * nsh * 4))) return rc;
             hipStream_t st = c->staging[0].stream;
-            uint32_t* d = reinterpret_cast<uint32_t*>(c->d_crc);
-            rc = launch_plan_crc(c, *plan, dev, S, block_stride, dev, S, block_stride, S, nblocks, d, st);
             const uint32_t *all = nullptr, *unused;
-            if (rc == RSMI_OK) rc = readback(c, d, nullptr, nblocks * nsh * 4, st, all, unused);
+            uint32_t seq = 0;
+            bool armed = false;
+            rc = RSMI_ERR_INVALID_ARG;
+            if (nblocks == 1 && c->opt_coalesce_flag) {
+                // one block (a lone degraded read): the table form with a single zero base, R(row)
+                // stored straight into the page-locked area by the in-kernel combine, and the
+                // completion flag polled below instead of a read-back kernel and a synchronisation
+                uint8_t* h = raw_area(c, nsh * 4);
+                uint32_t* hd = h ? reinterpret_cast<uint32_t*>(host_alias(h, nsh * 4)) : nullptr;
+                BlockBases tb;
+                tb.b[0] = 0;
+                if (hd && (rc = arm_flag(c, st, tb, seq)) == RSMI_OK)
+                    rc = launch_plan_crc(c, *plan, dev, S, block_stride, dev, S, block_stride, S, 1, hd, st, &tb, &armed);
+                else if (!hd)
+                    rc = RSMI_ERR_INVALID_ARG;
+                if (rc == RSMI_OK && !armed) rc = hip_status(hipStreamSynchronize(st));  // R landed by a second launch
+                if (rc == RSMI_OK) all = reinterpret_cast<const uint32_t*>(h);
+            }
+            if (rc == RSMI_ERR_INVALID_ARG && !armed) {
+                uint32_t* d = reinterpret_cast<uint32_t*>(c->d_crc);
+                rc = launch_plan_crc(c, *plan, dev, S, block_stride, dev, S, block_stride, S, nblocks, d, st);
+                if (rc == RSMI_OK) rc = readback(c, d, nullptr, nblocks * nsh * 4, st, all, unused);
+            }
             if (rc == RSMI_OK) {
-                HIP_TRY(hipStreamSynchronize(st));
+                if (armed) {
+                    if ((rc = wait_flag(done_flag(c, seq), seq, st, nullptr))) {
+                        (void)hipStreamSynchronize(st);
+                        return rc;
+                    }
+                } else {
+                    HIP_TRY(hipStreamSynchronize(st));
+                }
                 for (size_t b = 0; b < nblocks; b++)
                     std::memcpy(raw16_in + b * k, all + b * nsh, k * 4);
                 return RSMI_OK;

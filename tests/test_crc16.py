@@ -1113,5 +1113,17 @@ def test_coalesced_lone_calls_completion_flag(k, m, B, flag):
                         assert (sh[r] == 0xEE).all(), (it, r)
                     else:
                         assert np.array_equal(sh[r], full[r]), (it, r)
+                # a lone verified degraded read: the fused reconstruct with the survivors' R(row)
+                # (the in-kernel-combine table form, its R stored straight to page-locked memory)
+                if any(r < k for r in lost):
+                    sh[lost] = 0xEE
+                    v16 = np.zeros(k, dtype=np.uint32)
+                    c.reconstruct_batch_host_verify_ptr(p, n * S, S, 1, present, True, v16.ctypes.data)
+                    used = [i for i in range(n) if present[i]][:k]
+                    for r in range(k):
+                        assert np.array_equal(sh[r], full[r]), (it, r)
+                    if it % 10 == 0:
+                        for j, r in enumerate(used):
+                            assert rsmi.crc16_entry(b"", int(v16[j]), S) == orc.crc16_ibm(full[r].tobytes()), (it, r)
     finally:
         L.rsmi_host_free(p)
