@@ -249,6 +249,11 @@ int main(int argc, char** argv) {
         // (contexts, lanes, carry, coalesce_us, streaming copies); THREADS_CFG=quick: the first
         // (default) configuration and its variants at 16 threads only
         const bool quick = std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "quick");
+        if (std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "one")) {
+            // the default configuration at 16 threads, RS(10,4) 256 KiB only (for a kernel trace)
+            coalesced_threads(10, 4, size_t(262144), 16, 128);
+            return 0;
+        }
         if (std::getenv("THREADS_CFG") && !std::strcmp(std::getenv("THREADS_CFG"), "flag")) {
             // option coalesce_flag off / on: 1 thread (a lone caller's in-place call) and 16 threads,
             // alternated twice
