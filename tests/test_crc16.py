@@ -1127,3 +1127,66 @@ def test_coalesced_lone_calls_completion_flag(k, m, B, flag):
                             assert rsmi.crc16_entry(b"", int(v16[j]), S) == orc.crc16_ibm(full[r].tobytes()), (it, r)
     finally:
         L.rsmi_host_free(p)
+
+
+@pytest.mark.gpu
+def test_coalesced_pipelined_host_fault_midrun():
+    """Batches failing in their executor (option "inject_host_fault", set by one caller mid-run)
+    while other batches of the same lanes are in flight (pipelined, with completion flags): the
+    failed batches' callers get RSMI_ERR_HOST, every other call's shards and R(shard) equal the
+    oracle's, no caller hangs, and the queue codes correctly afterwards."""
+    import threading
+
+    k, m, B = 10, 4, 262144
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    T, per = 8, 30
+    rng = np.random.default_rng(77)
+    blocks = [rng.integers(0, 256, size=B, dtype=np.uint8) for _ in range(T)]
+    want = []
+    for b in blocks:
+        w = orc.split(k, m, b.tobytes())
+        w[k:] = orc.encode_fast(k, m, w[None, :k], threads=4)[0]
+        want.append((w, [orc.crc16_ibm(w[r].tobytes()) for r in range(n)]))
+    ptrs = [L.rsmi_host_alloc(n * S) for _ in range(T)]
+    assert all(ptrs)
+    rcs = [[] for _ in range(T)]
+    bad = []
+    try:
+        views = [np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S) for p in ptrs]
+        with rsmi.Codec(k, m) as c:
+            c.warm()
+
+            def run(t):
+                raw = (ctypes.c_uint32 * n)()
+                for i in range(per):
+                    if t == 0 and i == 10:
+                        c.set_option("inject_host_fault", 3)
+                    flat = views[t].reshape(-1)
+                    flat[:] = 0xA5
+                    flat[:B] = blocks[t]
+                    rc = L.rsmi_encode_block_coalesced(c._h, ptrs[t], B, ptrs[t], raw)
+                    rcs[t].append(rc)
+                    if rc == 0 and (not np.array_equal(views[t], want[t][0]) or
+                                    [rsmi.crc16_entry(b"", raw[r], S) for r in range(n)] != want[t][1]):
+                        bad.append((t, i))
+
+            th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join(timeout=60)
+            assert not any(x.is_alive() for x in th)
+            flat = views[0].reshape(-1)
+            flat[:B] = blocks[0]
+            raw = (ctypes.c_uint32 * n)()
+            assert L.rsmi_encode_block_coalesced(c._h, ptrs[0], B, ptrs[0], raw) == 0
+            assert np.array_equal(views[0], want[0][0])
+    finally:
+        for p in ptrs:
+            L.rsmi_host_free(p)
+    codes = [rc for r in rcs for rc in r]
+    assert set(codes) <= {0, rsmi.ErrHost}, set(codes)
+    assert codes.count(rsmi.ErrHost) >= 1
+    assert bad == []
