@@ -105,7 +105,8 @@ int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st, hipEvent_t ev)
 // A group whose requests' shard buffers are page-locked, coded where they lie (see
 // run_coalesced_group): one launch over a table of the blocks' bases for up to kTableBlocks
 // requests (BlockBases, the table kernels of the BASELINE shapes), else one launch per request,
-// and one synchronisation.  Encode: each block is Split into its own buffer first (the caller's
+// and one wait: the completion flag of a one-launch fused encode + CRC-16, else a stream
+// synchronisation.  Encode: each block is Split into its own buffer first (the caller's
 // block is pageable), outside the context lock -- unless the caller Split it there itself
 // (block == out), as the host mirror does, so the copies run on the callers' threads in
 // parallel instead of one after another on the executor's.
