@@ -369,9 +369,10 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * default: a coalesced batch coded by the table kernels is left in flight behind an event while
  * the lane's next queued batch is launched behind it, and its callers return when the event
  * completes; 0 = every batch synchronises before the next is launched), "coalesce_flag" (1 =
- * default: a group coded by one table launch of the encode + CRC-16 signals its end through a
- * page-locked flag its last workgroup releases, which the executor polls instead of synchronising
- * -- falling back to the synchronisation after 200 us or on a stream error; 0 = event / stream
+ * default: a coalesced group coded by one table launch of the encode + CRC-16, and a one-block
+ * in-place host call (encode + CRC-16, reconstruct, verified reconstruct), signal their end through
+ * a page-locked flag the launch's last workgroup releases, which the caller polls instead of
+ * synchronising -- blocking in the synchronisation after 200 us; 0 = event / stream
  * synchronisation).  Kernel variants measured slower than the defaults are not
  * built into the library.  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
