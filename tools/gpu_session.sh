@@ -23,6 +23,7 @@
 #   latency          per-block call latencies (tools/latency)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
+#   threads_ab       THREADS_AB_CFG (default flag) on the product library and each tools/build/v_* variant
 #   threads_flag     1 and 16 threads, option coalesce_flag off / on alternated (THREADS_CFG=flag)
 #   group_sweep      one thread, in-place host calls of 1..256 blocks back to back (tools/latency --group-sweep)
 #   threads_traced   the same under rocprofv3 --kernel-trace (crash report: tools/latency.cpp)
@@ -106,6 +107,18 @@ threads)
 threads_pipe)
   THREADS_CFG=pipe timeout -k 10 400 ./tools/build/latency --threads > $O/threads_pipe.txt 2>&1 || fail threads_pipe $O/threads_pipe.txt
   cat $O/threads_pipe.txt ;;
+threads_ab)
+  # the threads configuration THREADS_AB_CFG (default flag) on the product library and every
+  # tools/build/v_* variant (LD_LIBRARY_PATH), alternated twice
+  : > $O/threads_ab.txt
+  for rep in 1 2; do
+    for lib in filedag-storage_amd/lib tools/build/v_*/lib; do
+      v=$(basename $(dirname $lib)); [ "$lib" = filedag-storage_amd/lib ] && v=product
+      echo "== $v (round $rep)" >> $O/threads_ab.txt
+      LD_LIBRARY_PATH=$R/$lib THREADS_CFG=${THREADS_AB_CFG:-flag} timeout -k 10 300 ./tools/build/latency --threads >> $O/threads_ab.txt 2>&1 || fail "threads_ab $v" $O/threads_ab.txt
+    done
+  done
+  grep -E "^==|threads x" $O/threads_ab.txt | cut -c1-200 ;;
 threads_flag)
   THREADS_CFG=flag timeout -k 10 400 ./tools/build/latency --threads > $O/threads_flag.txt 2>&1 || fail threads_flag $O/threads_flag.txt
   cat $O/threads_flag.txt ;;
