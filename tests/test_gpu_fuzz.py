@@ -163,3 +163,62 @@ def test_random_coalesced_groups(seed):
     finally:
         for p in ptrs:
             L.rsmi_host_free(p)
+
+
+LONE_CASES = 24
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(LONE_CASES))
+def test_random_lone_in_place_calls(seed):
+    """Seeded random one-block in-place host calls on page-locked memory -- a lone DagNode.Put,
+    repair, degraded and verified read (node.go:358-408, :220-326, data_recovery.go:16-112) --
+    which take the one-base table launches with completion flags where the shape has them and
+    the plain launches and stream synchronisation where it does not (rows under 16 bytes, shapes
+    without table kernels, 5+ lost rows): random (k, m), block sizes from 1 byte to 1 MiB + 14,
+    random loss patterns, the option coalesce_flag on and off.  Shards, R(shard), rebuilt rows and
+    the survivors' R(row) against the oracle."""
+    import ctypes
+
+    r = np.random.default_rng(9000 + seed)
+    k, m = [(2, 1), (4, 2), (10, 4), (16, 4), (3, 2), (5, 5), (10, 4)][int(r.integers(0, 7))]
+    B = int(r.choice([int(r.integers(1, 64)), int(r.integers(64, 5000)), int(r.integers(5000, 300000)),
+                      262144, 1048576 + 14]))
+    flag = int(r.integers(0, 2))
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    p = L.rsmi_host_alloc(n * S)
+    assert p
+    try:
+        sh = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p)).reshape(n, S)
+        block = r.integers(0, 256, size=B, dtype=np.uint8)
+        full = orc.split(k, m, block.tobytes())
+        full[k:] = orc.encode(k, m, full[:k])
+        r16 = [orc.crc16_ibm(full[i].tobytes()) for i in range(n)]
+        with rsmi.Codec(k, m) as c:
+            c.set_option("coalesce_flag", flag)
+            for rep in range(3):  # the flag slots reused
+                sh[:] = 0x5A
+                sh[:k] = full[:k]
+                raw = np.zeros(n, dtype=np.uint32)
+                c.encode_batch_host_crcs_ptr(p, n * S, p + k * S, n * S, S, 1, raw.ctypes.data, None)
+                assert np.array_equal(sh, full), (k, m, B, rep)
+                assert [rsmi.crc16_entry(b"", int(x), S) for x in raw] == r16, (k, m, B, rep)
+                nlost = int(r.integers(1, m + 1))
+                lost = sorted(int(x) for x in r.choice(n, size=nlost, replace=False))
+                present = [i not in lost for i in range(n)]
+                sh[lost] = 0xEE
+                c.reconstruct_rows_batch_host_ptr(p, n * S, S, 1, present, [i in lost for i in range(n)])
+                assert np.array_equal(sh, full), (k, m, B, lost)
+                if any(i < k for i in lost):
+                    sh[lost] = 0xEE
+                    v16 = np.zeros(k, dtype=np.uint32)
+                    c.reconstruct_batch_host_verify_ptr(p, n * S, S, 1, present, True, v16.ctypes.data)
+                    for i in range(n):
+                        if i < k or i not in lost:
+                            assert np.array_equal(sh[i], full[i]), (k, m, B, lost, i)
+                    used = [i for i in range(n) if present[i]][:k]
+                    assert [rsmi.crc16_entry(b"", int(v16[j]), S) for j in range(k)] == [r16[i] for i in used]
+    finally:
+        L.rsmi_host_free(p)
