@@ -1190,3 +1190,83 @@ def test_coalesced_pipelined_host_fault_midrun():
     assert set(codes) <= {0, rsmi.ErrHost}, set(codes)
     assert codes.count(rsmi.ErrHost) >= 1
     assert bad == []
+
+
+@pytest.mark.gpu
+def test_mixed_lone_and_coalesced_stress():
+    """24 threads on one context mixing, at random, coalesced encodes + CRC-16 and coalesced
+    degraded reconstructs (the group commit: pipelined table launches, completion flags, two lanes)
+    with direct one-block in-place host calls (encode + CRC-16, repair rows, verified read) that
+    hold the context and share lane 0's stream and flags: three block sizes, every result against
+    the oracle, no caller left waiting."""
+    import threading
+
+    k, m = 10, 4
+    n = k + m
+    L = rsmi.lib()
+    sizes = [4096, 65536 + 7, 262144]
+    ref = {}
+    rng = np.random.default_rng(4242)
+    for B in sizes:
+        S = (B + k - 1) // k
+        block = rng.integers(0, 256, size=B, dtype=np.uint8)
+        full = orc.split(k, m, block.tobytes())
+        full[k:] = orc.encode(k, m, full[:k])
+        ref[B] = (block, full, [orc.crc16_ibm(full[r].tobytes()) for r in range(n)], S)
+    T, per = 24, 40
+    bufs = [L.rsmi_host_alloc(n * ((max(sizes) + k - 1) // k)) for _ in range(T)]
+    assert all(bufs)
+    errors = []
+    try:
+        with rsmi.Codec(k, m) as c:
+            c.warm()
+
+            def run(t):
+                r = np.random.default_rng(t)
+                raw = (ctypes.c_uint32 * n)()
+                for i in range(per):
+                    B = sizes[int(r.integers(0, len(sizes)))]
+                    block, full, r16, S = ref[B]
+                    sh = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(bufs[t])).reshape(n, S)
+                    op = int(r.integers(0, 4))
+                    sh[:] = 0x5A
+                    sh.reshape(-1)[:B] = block
+                    if op == 0:
+                        rc = L.rsmi_encode_block_coalesced(c._h, bufs[t], B, bufs[t], raw)
+                    else:
+                        sh.reshape(-1)[B:k * S] = 0
+                        c.encode_batch_host_crcs_ptr(bufs[t], n * S, bufs[t] + k * S, n * S, S, 1, ctypes.addressof(raw), None)
+                        rc = 0
+                    if rc or not np.array_equal(sh, full) or [rsmi.crc16_entry(b"", raw[x], S) for x in range(n)] != r16:
+                        errors.append((t, i, "encode", op, rc))
+                        continue
+                    lost = sorted(int(x) for x in r.choice(n, size=int(r.integers(1, m + 1)), replace=False))
+                    present = [x not in lost for x in range(n)]
+                    sh[lost] = 0xEE
+                    if op == 1:
+                        c.reconstruct_rows_batch_host_ptr(bufs[t], n * S, S, 1, present, [x in lost for x in range(n)])
+                    elif op == 2 and any(x < k for x in lost):
+                        v16 = np.zeros(k, dtype=np.uint32)
+                        c.reconstruct_batch_host_verify_ptr(bufs[t], n * S, S, 1, present, False, v16.ctypes.data)
+                        used = [x for x in range(n) if present[x]][:k]
+                        if [rsmi.crc16_entry(b"", int(v16[j]), S) for j in range(k)] != [r16[x] for x in used]:
+                            errors.append((t, i, "verify R"))
+                    else:
+                        p = (ctypes.c_uint8 * n)(*[1 if x else 0 for x in present])
+                        rc = L.rsmi_reconstruct_coalesced(c._h, bufs[t], S, p, 0)
+                        if rc:
+                            errors.append((t, i, "reconstruct rc", rc))
+                            continue
+                    if not np.array_equal(sh, full):
+                        errors.append((t, i, "rebuilt", op, lost))
+
+            th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join(timeout=120)
+            assert not any(x.is_alive() for x in th)
+    finally:
+        for p in bufs:
+            L.rsmi_host_free(p)
+    assert errors == []
