@@ -20,6 +20,7 @@
 #   dagnode_ab       the Dag Node bench (GPU codec) on the product library and every tools/build/v_* variant
 #   ua_ab            the Split-layout (UA) kernels: product library against every tools/build/v_*
 #                    variant (tools/ua_ab.sh), then each library's FETCH_SIZE / WRITE_SIZE passes
+#   dagnode_env_ab   the Dag Node bench with ENV_AB=<variable> at ENV_VALUES (default 0 1), alternated
 #   latency          per-block call latencies (tools/latency)
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
@@ -98,6 +99,9 @@ ua_ab)
     python tools/pmc_summary.py $O/pmc_${v}_FETCH_SIZE/pmc_counter_collection.csv $O/pmc_${v}_WRITE_SIZE/pmc_counter_collection.csv $O/pmc_ua_$v.json
     echo "$v: $(cat $O/pmc_ua_$v.json | tr -d '\n')"
   done ;;
+dagnode_env_ab)
+  DN_OUT=$O/dagnode_env_ab.jsonl timeout -k 10 1000 bash tools/dagnode_env_ab.sh > $O/dagnode_env_ab.txt 2>&1 || fail "dagnode env ab" $O/dagnode_env_ab.txt
+  grep -v " done$" $O/dagnode_env_ab.txt ;;
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
