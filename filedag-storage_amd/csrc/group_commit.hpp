@@ -19,7 +19,9 @@
 // batch wakes exactly its own callers, and a released lane wakes the first queued caller to
 // execute the next batch.  (One shared condition variable woke every waiting caller at each
 // batch's end, and the woken callers then took the queue's lock one after another before the
-// next executor could: with 16 callers that convoy cost more than a small batch's launch.)
+// next executor could: with 16 callers that convoy cost more than a small batch's launch.)  An
+// executor that leaves callers queued while a lane is free (a batch capped at `cap`) wakes the
+// first of them too, so two lanes released together cannot leave a free lane idle.
 //
 // Pipelined batches: exec may return a finisher (a callable; empty or exec returning void: the
 // batch ran to completion) instead of waiting for its own work.  The executor then launches the
@@ -96,6 +98,9 @@ public:
                 }
                 for (Waiter* w : f.batch) w->queued = false;
                 pending_.erase(pending_.begin(), pending_.begin() + take);
+                // a batch capped at `cap` leaves callers queued: with a lane free, the first of
+                // them executes the next batch now instead of waiting for this lane
+                if (!pending_.empty() && executing_ < lanes) wake(*pending_.front());
                 lk.unlock();
                 try {
                     if constexpr (std::is_void_v<std::invoke_result_t<Exec&, std::vector<Req*>&, int>>)

@@ -103,18 +103,87 @@ Status find_meta_in_quorum(const std::vector<Meta>& metas, int quorum, Meta* out
 // ------------------------------------------------------------------ construction
 Status DagNode::New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
                     std::unique_ptr<DagNode>* out, int device) {
+    return New(cfg, std::move(clients), out, std::vector<int>{device});
+}
+
+Status DagNode::New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
+                    std::unique_ptr<DagNode>* out, const std::vector<int>& devices) {
     const size_t n = cfg.nodes.size();
     if (n != size_t(cfg.data_blocks + cfg.parity_blocks) || n == 0 || clients.size() != n)
         return Status::Error("dag node config is incorrect");  // node.go:55-57
+    if (devices.empty() || devices.size() > size_t(kClusterSlots)) return Status::Error("dag node device list is empty");
     std::unique_ptr<DagNode> d(new DagNode());
     d->config_ = cfg;
-    d->device_ = device;
+    d->devices_ = devices;
+    d->replicas_.assign(devices.size(), 0);
+    for (size_t i = 0; i < devices.size(); i++)
+        for (size_t j = 0; j < i; j++) d->replicas_[i] += devices[j] == devices[i];
     d->slots_.assign(kClusterSlots / 8, 0);
     for (auto& c : clients) d->nodes_.push_back(StorageNode{c, false});
     d->fan_.reset(new FanOut(int(n) - 1));  // the calling thread runs one share itself
-    warm_contexts(cfg.data_blocks, cfg.parity_blocks, device);  // the codec contexts, before the first call
+    if (devices.size() > 1) d->member_fan_.reset(new FanOut(int(devices.size()) - 1));
+    for (size_t i = 0; i < devices.size(); i++)  // the codec contexts, before the first call
+        warm_contexts(cfg.data_blocks, cfg.parity_blocks, devices[i], d->replicas_[i]);
     *out = std::move(d);
     return Status::Ok();
+}
+
+int DagNode::MemberOfKey(const std::string& key) const {
+    if (devices_.size() <= 1) return 0;
+    const int slot = rsmi_key_slot(reinterpret_cast<const uint8_t*>(key.data()), key.size());
+    if (slot < 0) return 0;
+    return int(size_t(slot) * devices_.size() / size_t(kClusterSlots));  // as rsmi_group_member_of_key
+}
+
+rsmi_ctx* DagNode::member_ctx(int member, int* rc) const {
+    return shared_context(config_.data_blocks, config_.parity_blocks, devices_[size_t(member)], rc,
+                          replicas_[size_t(member)]);
+}
+
+Status DagNode::member_erasure(int member, int64_t block_size, Erasure* out) const {
+    return Erasure::New(config_.data_blocks, config_.parity_blocks, block_size, out, devices_[size_t(member)],
+                        replicas_[size_t(member)]);
+}
+
+DagNode::MemberOrder DagNode::member_order(size_t nb, const std::function<int(size_t)>& member_of_pos) const {
+    MemberOrder o;
+    const size_t M = devices_.size();
+    o.perm.resize(nb);
+    o.ranges.assign(M, {0, 0});
+    if (M == 1) {
+        for (size_t j = 0; j < nb; j++) o.perm[j] = j;
+        o.ranges[0] = {0, nb};
+        return o;
+    }
+    std::vector<int> mem(nb);
+    for (size_t j = 0; j < nb; j++) {
+        mem[j] = member_of_pos(j);
+        o.ranges[size_t(mem[j])].second++;
+    }
+    for (size_t i = 1; i < M; i++) o.ranges[i].first = o.ranges[i - 1].first + o.ranges[i - 1].second;
+    std::vector<size_t> next(M);
+    for (size_t i = 0; i < M; i++) next[i] = o.ranges[i].first;
+    for (size_t j = 0; j < nb; j++) o.perm[next[size_t(mem[j])]++] = j;
+    return o;
+}
+
+int DagNode::code_members(const MemberOrder& order, const std::function<int(rsmi_ctx*, size_t, size_t)>& code) {
+    std::vector<int> live;
+    for (size_t i = 0; i < order.ranges.size(); i++)
+        if (order.ranges[i].second) live.push_back(int(i));
+    std::vector<int> rc(live.size(), RSMI_OK);
+    auto one = [&](int t) {
+        const int i = live[size_t(t)];
+        rsmi_ctx* ctx = member_ctx(i, &rc[size_t(t)]);
+        if (ctx) rc[size_t(t)] = code(ctx, order.ranges[size_t(i)].first, order.ranges[size_t(i)].second);
+    };
+    if (live.size() > 1 && member_fan_)
+        member_fan_->run(int(live.size()), one);  // each member's call on its own thread
+    else
+        for (size_t t = 0; t < live.size(); t++) one(int(t));
+    for (int r : rc)
+        if (r != RSMI_OK) return r;
+    return RSMI_OK;
 }
 
 void DagNode::fan(int count, const std::function<void(int)>& f, size_t shard_bytes) {
@@ -278,8 +347,9 @@ Status DagNode::Has(const std::string& key, bool* has) {
 Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:358-408
     Active act(active_);
     const Bytes meta = encode_meta(int32_t(block.size()));
+    const int member = MemberOfKey(key);
     Erasure enc;
-    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, int64_t(block.size()), &enc, device_);
+    Status s = member_erasure(member, int64_t(block.size()), &enc);
     if (!s.ok()) return s;
     const int n = int(nodes_.size());
     const size_t S = size_t(enc.ShardSize());
@@ -298,7 +368,7 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
         copy_bytes(flat, block.data(), block.size());
         std::memset(flat + block.size(), 0, k * S - block.size());  // Split zero-padding
         int rc;
-        rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+        rsmi_ctx* ctx = member_ctx(member, &rc);
         if (!ctx) return rsmi_status(rc);
         rc = raw.empty() ? rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1)
                          : rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1,
@@ -346,11 +416,6 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             continue;
         }
         int rc;
-        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
-        if (!ctx) {
-            for (size_t i : g.second) results[i] = rsmi_status(rc);
-            continue;
-        }
         const size_t S = rsmi_shard_size(B, k);
         // Two halves of the thread's staging: a chunk's datanode writes run on a helper thread
         // while the next chunk is staged and coded into the other half (the GPU call leaves the
@@ -377,6 +442,13 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         int cur = 0;
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
+            // the chunk's blocks ordered by member (a device list): each member codes one range
+            const MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(keys[g.second[c0 + j]]); });
+            {
+                std::vector<size_t> tmp(nb);
+                for (size_t j = 0; j < nb; j++) tmp[j] = g.second[c0 + ord.perm[j]];
+                std::copy(tmp.begin(), tmp.end(), g.second.begin() + long(c0));
+            }
             const size_t* idx = g.second.data() + c0;
             // per block: k data rows (Split, zero-padded) + m parity rows
             const auto t0 = PhaseClock::now();
@@ -393,11 +465,15 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             if (gpu_checksums_) {
                 raw.resize(nb * size_t(n));
                 raw32.resize(want32 ? nb * size_t(n) : 0);
-                rc = rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb,
-                                                 raw.data(), want32 ? raw32.data() : nullptr);
-            } else {
-                rc = rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, nb);
             }
+            rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                uint8_t* f = flat + j0 * size_t(n) * S;
+                if (!gpu_checksums_)
+                    return rsmi_encode_batch_host(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt);
+                return rsmi_encode_batch_host_crcs(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt,
+                                                   raw.data() + j0 * size_t(n),
+                                                   want32 ? raw32.data() + j0 * size_t(n) : nullptr);
+            });
             phase_add(Phase::Codec, t1);
             join_writes();  // the other half is free again
             if (rc) {
@@ -453,6 +529,7 @@ Status DagNode::DeleteBlock(const std::string& key) {  // node.go:191-208
 // ------------------------------------------------------------------ read path
 Status DagNode::fetch_for_get(const std::string& key, Fetched* f, bool defer_verify) {  // node.go:220-275
     std::vector<StorageNode*> online;
+    f->member = MemberOfKey(key);
     Status s = get_meta_info(key, &f->meta, &online);
     if (!s.ok()) return s;
     const int n = int(nodes_.size()), rq = EntryQuorum().first;
@@ -485,7 +562,7 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f, bool defer_ver
                 got[j] = gpu_verified_reads_ ? online[j]->client->GetForVerify(key, &metas[j], &data[j], &stored[j])
                                              : online[j]->client->Get(key, &metas[j], &data[j]);
             }, size_t(ceil_frac(f->meta.block_size, config_.data_blocks)));
-            if (gpu_verified_reads_ && !defer_verify) verify_wave(wave, metas, data, stored, got);
+            if (gpu_verified_reads_ && !defer_verify) verify_wave(f->member, wave, metas, data, stored, got);
             for (int j : wave) fetched[j] = 1;
         }
         if (!got[i].ok()) {
@@ -507,21 +584,22 @@ Status DagNode::fetch_for_get(const std::string& key, Fetched* f, bool defer_ver
 void DagNode::verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>& st, const std::vector<char>& skip,
                              std::vector<char>* bad) {
     bad->assign(fs.size(), 0);
-    // (key, node) of every accepted shard with a stored checksum to check, by shard size
-    std::map<size_t, std::vector<std::pair<size_t, int>>> by_size;
+    // (key, node) of every accepted shard with a stored checksum to check, by (shard size, the
+    // key's member)
+    std::map<std::pair<size_t, int>, std::vector<std::pair<size_t, int>>> by_size;
     for (size_t q = 0; q < fs.size(); q++) {
         if (!st[q].ok() || fs[q].stored.empty() || skip[q]) continue;
         for (size_t i = 0; i < fs[q].shards.size(); i++)
             if (!fs[q].shards[i].empty() && !fs[q].stored[i].verified)
-                by_size[fs[q].shards[i].size()].push_back({q, int(i)});
+                by_size[{fs[q].shards[i].size(), fs[q].member}].push_back({q, int(i)});
     }
     for (auto& g : by_size) {
-        const size_t S = g.first, w = g.second.size();
+        const size_t S = g.first.first, w = g.second.size();
         bool want32 = false;
         for (auto& e : g.second) want32 |= fs[e.first].stored[size_t(e.second)].has_value_crc;
         std::vector<uint32_t> r16(w, 0), r32(w, 0);
         int rc = RSMI_OK;
-        rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+        rsmi_ctx* ctx = member_ctx(g.first.second, &rc);
         // rows gathered into page-locked staging by the key pool, then read in place by one GPU
         // pass (staging_blocks bounds the buffer; a huge GetMany takes several passes)
         const size_t per = std::max<size_t>(1, kStagingBytes / S);
@@ -553,7 +631,7 @@ void DagNode::verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>
     }
 }
 
-void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas,
+void DagNode::verify_wave(int member, const std::vector<int>& wave, const std::vector<Bytes>& metas,
                           const std::vector<Bytes>& data, const std::vector<DataNodeClient::Stored>& stored,
                           std::vector<Status>& got) {
     // shards to check, grouped by size (one GPU call per size; a block's shards share one)
@@ -567,7 +645,7 @@ void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>
         std::vector<uint32_t> r16(w, 0), r32(w, 0);
         int rc = RSMI_OK;
         if (S > 0) {
-            rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+            rsmi_ctx* ctx = member_ctx(member, &rc);
             uint8_t* flat = ctx ? thread_staging().reserve(w * S) : nullptr;
             if (ctx && !flat) rc = RSMI_ERR_DEVICE;
             if (flat) {
@@ -596,7 +674,7 @@ void DagNode::verify_wave(const std::vector<int>& wave, const std::vector<Bytes>
 // node.go:311-319) taken straight from it.  *done = false leaves the call to the per-shard path:
 // nothing to decode, or shard lengths that are not the block's shard size; every error the
 // per-shard path would return (rsmi_check_shards, the decode) is returned the same way.
-Status DagNode::decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done) {
+Status DagNode::decode_into_block(const std::string& key, Fetched& f, size_t S, Bytes* block, bool* done) {
     *done = false;
     const int k = config_.data_blocks, n = int(f.shards.size());
     if (n != int(nodes_.size())) return Status::Ok();
@@ -620,7 +698,7 @@ Status DagNode::decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done
     int np = 0;
     for (int i = 0; i < n; i++) np += present[i];
     if (np < k) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);
-    rsmi_ctx* ctx = shared_context(config_.data_blocks, config_.parity_blocks, device_, &rc);
+    rsmi_ctx* ctx = member_ctx(MemberOfKey(key), &rc);
     if (!ctx) return rsmi_status(rc);
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
@@ -643,11 +721,11 @@ Status DagNode::decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done
 
 Status DagNode::finish_get(const std::string& key, Fetched& f, Bytes* block) {  // node.go:277-326
     Erasure enc;
-    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, f.meta.block_size, &enc, device_);
+    Status s = member_erasure(MemberOfKey(key), f.meta.block_size, &enc);
     if (!s.ok()) return s;
     const size_t S = size_t(enc.ShardSize());
     bool done = f.assembled;  // GetMany's batch decode already wrote the block
-    if (!done && lone_paths_ && active_.load() <= 1 && (s = decode_into_block(f, S, block, &done), !s.ok()))
+    if (!done && lone_paths_ && active_.load() <= 1 && (s = decode_into_block(key, f, S, block, &done), !s.ok()))
         return s;
     if (!done) {
         s = enc.DecodeDataBlocks(f.shards);
@@ -799,9 +877,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
             bool sizes_ok = true;  // every present shard must have the common size (else per-key errors)
             for (size_t q : g.second)
                 for (int c = 0; c < n; c++) sizes_ok &= !present[c] || fs[q].shards[c].size() == S;
-            int rc;
-            rsmi_ctx* ctx = sizes_ok ? shared_context(k, m, device_, &rc) : nullptr;
-            if (!ctx) {  // finish_get reports the size or device error per key
+            if (!sizes_ok) {  // finish_get reports the size error per key
                 unchecked(g.second, 0, g.second.size());
                 continue;
             }
@@ -814,6 +890,13 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
             std::vector<uint32_t> r16(verify ? chunk * size_t(k) : 0);
             for (size_t b0 = 0; b0 < g.second.size(); b0 += chunk) {
                 const size_t nb = std::min(chunk, g.second.size() - b0);
+                // the chunk's keys ordered by member (a device list): each member decodes one range
+                const MemberOrder ord = member_order(nb, [&](size_t j) { return fs[g.second[b0 + j]].member; });
+                {
+                    std::vector<size_t> tmp(nb);
+                    for (size_t j = 0; j < nb; j++) tmp[j] = g.second[b0 + ord.perm[j]];
+                    std::copy(tmp.begin(), tmp.end(), g.second.begin() + long(b0));
+                }
                 uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
                 if (!flat) {
                     unchecked(g.second, b0, nb);
@@ -824,10 +907,13 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
                 // with verified reads the same kernel returns R of every survivor it read
-                const int drc = verify ? rsmi_reconstruct_batch_host_verify(ctx, flat, size_t(n) * S, S, nb,
-                                                                            present.data(), 1, r16.data())
-                                       : rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(), 1);
-                if (drc != RSMI_OK) {
+                const int drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                    uint8_t* f = flat + j0 * size_t(n) * S;
+                    return verify ? rsmi_reconstruct_batch_host_verify(ctx, f, size_t(n) * S, S, cnt, present.data(), 1,
+                                                                       r16.data() + j0 * size_t(k))
+                                  : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
+                });
+                if (drc != RSMI_OK) {  // finish_get reports a device error per key
                     unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
                 }
@@ -905,7 +991,7 @@ Status DagNode::repair_block(const std::string& key, int32_t block_size, std::ve
     for (auto& sh : shards) available += !sh.empty();
     if (available < EntryQuorum().first) return Status::Error("repair index greater than max index of nodes");
     Erasure enc;
-    Status s = Erasure::New(config_.data_blocks, config_.parity_blocks, block_size, &enc, device_);
+    Status s = member_erasure(MemberOfKey(key), block_size, &enc);
     if (!s.ok()) return s;
     s = enc.DecodeDataAndParityBlocks(shards);
     if (!s.ok()) return s;
@@ -991,7 +1077,14 @@ Status DagNode::fetch_for_repair(const std::string& key, int repair_index, std::
     return w.result(kErrReadQuorum);
 }
 
-Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
+// data_recovery.go:16-112 through the batched form: the same index checks, keys present on the
+// target skipped (:41-43), keys whose size or k-of-n fetch fails skipped (:48-51, :78-81), and a
+// decode or target write error returned (:83-92, :101-106).  Rows of one flush are written
+// concurrently, so when a write fails, later keys of the same flush may have been repaired as
+// well; the error returned is the first in key order.
+Status DagNode::RepairDataNode(int from, int to) { return RepairDataNodeBatched(from, to, kRepairBatch); }
+
+Status DagNode::RepairDataNodePerKey(int from, int to) {  // data_recovery.go:16-112, key by key
     if (from >= int(nodes_.size())) return Status::Error("index greater than max index of nodes");
     if (to >= int(nodes_.size())) return Status::Error("repair index greater than max index of nodes");
     std::vector<std::string> keys;
@@ -1009,7 +1102,7 @@ Status DagNode::RepairDataNode(int from, int to) {  // data_recovery.go:16-112
             return s;
         if (done) continue;
         Erasure enc;
-        s = Erasure::New(config_.data_blocks, config_.parity_blocks, size, &enc, device_);
+        s = member_erasure(MemberOfKey(key), size, &enc);
         if (!s.ok()) return s;
         s = enc.DecodeDataAndParityBlocks(shards);
         if (!s.ok()) return s;
@@ -1045,7 +1138,7 @@ Status DagNode::repair_row_in_place(const std::string& key, int size, const std:
     for (int i = 0; i < n; i++) np += present[i];
     if (np < k) return rsmi_status(RSMI_ERR_TOO_FEW_SHARDS);
     required[to] = 1;
-    rsmi_ctx* ctx = shared_context(k, config_.parity_blocks, device_, &rc);
+    rsmi_ctx* ctx = member_ctx(MemberOfKey(key), &rc);
     if (!ctx) return rsmi_status(rc);
     uint8_t* flat = block_scratch(size_t(n) * S);
     if (!flat) return Status::Error("out of host memory");
@@ -1099,15 +1192,13 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
         int rc;
-        rsmi_ctx* ctx = shared_context(k, m, device_, &rc);
-        if (!ctx) {
-            const Status w = join_writes();
-            return w.ok() ? rsmi_status(rc) : w;
-        }
         const size_t S = rsmi_shard_size(size_t(size), k), nb = pend.size();
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
         required[to] = 1;
+        // the keys ordered by member (a device list): each member rebuilds one range; the
+        // writes' outcomes are taken back in key order
+        const MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(pend[j].key); });
         // the fetch returns exactly the k survivors the plan reads (fetch_for_repair stops at
         // the read quorum k), and only those are staged; the rows being rebuilt are not
         const auto t0 = PhaseClock::now();
@@ -1126,19 +1217,23 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         }
         uint8_t* flat = base + (cur ? st.capacity() / 2 : 0);
         fan_keys(int(nb), [&](int j) {
+            const Pending& p = pend[ord.perm[size_t(j)]];
             for (int i = 0; i < n; i++)
-                if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, pend[j].shards[i].data(), S);
+                if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, p.shards[i].data(), S);
         });
         phase_add(Phase::Stage, t0);
         // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
         const auto t1 = PhaseClock::now();
         const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
         std::vector<uint32_t> r16(gpu_checksums_ ? nb * size_t(n) : 0), r32(want32 ? nb * size_t(n) : 0);
-        rc = gpu_checksums_ ? rsmi_reconstruct_rows_batch_host_crcs(ctx, flat, size_t(n) * S, S, nb, present.data(),
-                                                                    required.data(), r16.data(),
-                                                                    want32 ? r32.data() : nullptr)
-                            : rsmi_reconstruct_rows_batch_host(ctx, flat, size_t(n) * S, S, nb, present.data(),
-                                                               required.data());
+        rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+            uint8_t* f = flat + j0 * size_t(n) * S;
+            if (!gpu_checksums_)
+                return rsmi_reconstruct_rows_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), required.data());
+            return rsmi_reconstruct_rows_batch_host_crcs(ctx, f, size_t(n) * S, S, cnt, present.data(), required.data(),
+                                                         r16.data() + j0 * size_t(n),
+                                                         want32 ? r32.data() + j0 * size_t(n) : nullptr);
+        });
         phase_add(Phase::Codec, t1);
         const Status w = join_writes();
         if (!w.ok()) return w;
@@ -1146,22 +1241,24 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         // the rebuilt rows go to the target concurrently, each as a view of the staging buffer;
         // outcomes are taken in key order by the next join
         std::vector<std::string> wkeys(nb);
-        for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[j].key);
+        for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[ord.perm[j]].key);
         pend.clear();
         writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size),
-                                                  wkeys = std::move(wkeys), r16 = std::move(r16), r32 = std::move(r32)] {
+                                                  perm = ord.perm, wkeys = std::move(wkeys), r16 = std::move(r16),
+                                                  r32 = std::move(r32)] {
             const auto t2 = PhaseClock::now();
-            std::vector<Status> ps(wkeys.size());
+            std::vector<Status> ps(wkeys.size());  // by key order (perm[j]: slot j's key)
             fan_keys(int(wkeys.size()), [&](int j) {
                 const ByteView shard(flat + (size_t(j) * n + size_t(to)) * S, S);
+                Status& out = ps[perm[size_t(j)]];
                 if (!gpu_checksums_) {
-                    ps[j] = target.Put(wkeys[j], meta, shard);
+                    out = target.Put(wkeys[j], meta, shard);
                     return;
                 }
                 const uint16_t c16 = entry_checksum(meta, S, r16[size_t(j) * n + size_t(to)]);
-                ps[j] = want32 ? target.PutWithChecksums(wkeys[j], meta, shard, c16,
-                                                         value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
-                               : target.PutWithChecksum(wkeys[j], meta, shard, c16);
+                out = want32 ? target.PutWithChecksums(wkeys[j], meta, shard, c16,
+                                                       value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
+                             : target.PutWithChecksum(wkeys[j], meta, shard, c16);
             });
             phase_add(Phase::Put, t2);
             return ps;
@@ -1221,7 +1318,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 s = join_writes();
                 if (!s.ok()) return s;
                 Erasure enc;
-                s = Erasure::New(k, m, size, &enc, device_);
+                s = member_erasure(MemberOfKey(key), size, &enc);
                 if (s.ok()) s = enc.DecodeDataAndParityBlocks(shards);
                 if (!s.ok()) return s;  // `ahead` (reads only) is joined by its destructor
                 continue;

@@ -70,6 +70,16 @@ public:
     // node.go:53-73 (clients replace the gRPC dial of datanode.NewClient)
     static Status New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
                       std::unique_ptr<DagNode>* out, int device = 0);
+    // ... coding on a list of GPUs (members; a device may repeat).  Every per-key call (Put, Get,
+    // the read-repair, RepairDataNode's rebuilds) runs on the member that owns the key: the Dag
+    // Pool's hash slot crc16(key) & 0x3FFF (hash_slot.go:20-22) in contiguous ranges of
+    // 16384 / members slots per member, as rsmi_group_member_of_key.  Each member has contexts,
+    // group-commit queue and coalescing lanes of its own, so concurrent callers spread over the
+    // members' PCIe links.  The batch calls (PutMany, GetMany's decode, RepairDataNodeBatched)
+    // order each chunk's blocks by member and code the members' ranges concurrently.  Stored
+    // entries and returned blocks are identical to the one-device node's.
+    static Status New(const DagNodeConfig& cfg, std::vector<std::shared_ptr<DataNodeClient>> clients,
+                      std::unique_ptr<DagNode>* out, const std::vector<int>& devices);
     ~DagNode();
 
     Status Put(const std::string& key, const Bytes& block);
@@ -85,7 +95,11 @@ public:
     void GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* blocks, std::vector<Status>* statuses,
                  size_t batch = 256);
 
+    // RepairDataNode runs the batched form (kRepairBatch keys per flush at most); the per-key
+    // loop of data_recovery.go stays as RepairDataNodePerKey (A/B legs, tools/bench_dagnode)
+    static constexpr size_t kRepairBatch = 256;
     Status RepairDataNode(int from_index, int repair_index);
+    Status RepairDataNodePerKey(int from_index, int repair_index);
     // batched: keys needing repair are grouped by (block size, survivor pattern) and rebuilt
     // `batch` at a time on the GPU
     Status RepairDataNodeBatched(int from_index, int repair_index, size_t batch, size_t* repaired = nullptr);
@@ -102,6 +116,10 @@ public:
     bool GetSlot(uint64_t slot) const;
     int GetNumSlots() const { return num_slots_; }
     const DagNodeConfig& GetConfig() const { return config_; }
+    int Members() const { return int(devices_.size()); }
+    int MemberOfKey(const std::string& key) const;  // the member coding key's per-key calls
+    int MemberDevice(int member) const { return devices_.at(size_t(member)); }
+    int MemberReplica(int member) const { return replicas_.at(size_t(member)); }
     bool GetDataNodeState(int set_index) const;
     void SetDataNodeState(int set_index, bool v) { nodes_.at(set_index).state = v; }
     // Put / PutMany compute each shard's datanode entry checksum on the GPU, from the rows
@@ -159,6 +177,7 @@ private:
         std::vector<Bytes> metas;
         std::vector<DataNodeClient::Stored> stored;
         bool assembled = false;  // GetMany: the block was taken from the batch decode's staging
+        int member = 0;          // the key's member (a device list)
     };
     // defer_verify: with GPU-verified reads on, accept the first wave's shards unchecked and keep
     // their stored checksums in f, for one batched check across many keys (verify_fetched)
@@ -168,7 +187,7 @@ private:
     void verify_fetched(std::vector<Fetched>& fs, const std::vector<Status>& st, const std::vector<char>& skip,
                         std::vector<char>* bad);
     Status finish_get(const std::string& key, Fetched& f, Bytes* block);
-    Status decode_into_block(Fetched& f, size_t S, Bytes* block, bool* done);
+    Status decode_into_block(const std::string& key, Fetched& f, size_t S, Bytes* block, bool* done);
     Status repair_row_in_place(const std::string& key, int size, const std::vector<Bytes>& shards, int to, bool* done);
     Status get_meta_info(const std::string& key, Meta* meta, std::vector<StorageNode*>* online);
     Status repair_block(const std::string& key, int32_t block_size, std::vector<Bytes> shards,
@@ -185,12 +204,27 @@ private:
     std::vector<StorageNode> nodes_;
     std::vector<uint8_t> slots_;
     int num_slots_ = 0;
-    int device_ = 0;
+    // the members' devices and, for a device that repeats, which of its contexts (erasure.hpp)
+    std::vector<int> devices_{0}, replicas_{0};
+    rsmi_ctx* member_ctx(int member, int* rc) const;  // the member's shared context for (k, m)
+    Status member_erasure(int member, int64_t block_size, Erasure* out) const;
+    // A chunk of nb blocks reordered so each member's blocks are contiguous: stable, member
+    // ascending; perm[j] is the chunk position staged at slot j, and ranges[i] = (first slot,
+    // count) of member i.  One member: the identity.
+    struct MemberOrder {
+        std::vector<size_t> perm;
+        std::vector<std::pair<size_t, size_t>> ranges;
+    };
+    MemberOrder member_order(size_t nb, const std::function<int(size_t)>& member_of_pos) const;
+    // code(ctx, first slot, count) for every member range with blocks, concurrently on the
+    // member pool (one member: on this thread); the first nonzero status in member order
+    int code_members(const MemberOrder& order, const std::function<int(rsmi_ctx*, size_t, size_t)>& code);
+    std::unique_ptr<FanOut> member_fan_;
     bool gpu_checksums_ = true;
     bool gpu_value_checksums_ = false;
     bool gpu_verified_reads_ = false;
     // GPU check of the unverified shards of one fetch wave; failures become errors in got[]
-    void verify_wave(const std::vector<int>& wave, const std::vector<Bytes>& metas, const std::vector<Bytes>& data,
+    void verify_wave(int member, const std::vector<int>& wave, const std::vector<Bytes>& metas, const std::vector<Bytes>& data,
                      const std::vector<DataNodeClient::Stored>& stored, std::vector<Status>& got);
     bool parallel_ = true;
     bool lone_paths_ = true;

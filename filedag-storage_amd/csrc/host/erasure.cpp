@@ -143,11 +143,12 @@ uint8_t* block_scratch(size_t bytes) {
 
 namespace {
 std::mutex g_ctx_mu;
-std::map<std::tuple<int, int, int, int>, rsmi_ctx*> g_ctx_cache;  // (k, m, device, lane); lives for the process
+// (k, m, device, replica, lane); lives for the process
+std::map<std::tuple<int, int, int, int, int>, rsmi_ctx*> g_ctx_cache;
 
-rsmi_ctx* lane_context(int k, int m, int device, int lane, int* rc) {
+rsmi_ctx* lane_context(int k, int m, int device, int replica, int lane, int* rc) {
     std::lock_guard<std::mutex> g(g_ctx_mu);
-    auto key = std::make_tuple(k, m, device, lane);
+    auto key = std::make_tuple(k, m, device, replica, lane);
     auto it = g_ctx_cache.find(key);
     if (it != g_ctx_cache.end()) {
         *rc = RSMI_OK;
@@ -166,39 +167,42 @@ void release_shared_contexts() {
     g_ctx_cache.clear();
 }
 
-rsmi_ctx* shared_context(int k, int m, int device, int* rc) { return lane_context(k, m, device, 0, rc); }
-
-rsmi_ctx* call_context(int k, int m, int device, int* rc) {
-    static std::atomic<unsigned> next{0};
-    thread_local const int lane = int(next.fetch_add(1) % unsigned(kCallLanes));
-    return lane_context(k, m, device, lane, rc);
+rsmi_ctx* shared_context(int k, int m, int device, int* rc, int replica) {
+    return lane_context(k, m, device, replica, 0, rc);
 }
 
-void warm_contexts(int k, int m, int device) {
+rsmi_ctx* call_context(int k, int m, int device, int* rc, int replica) {
+    static std::atomic<unsigned> next{0};
+    thread_local const int lane = int(next.fetch_add(1) % unsigned(kCallLanes));
+    return lane_context(k, m, device, replica, lane, rc);
+}
+
+void warm_contexts(int k, int m, int device, int replica) {
     for (int lane = 0; lane < kCallLanes; lane++) {
         int rc;
-        rsmi_ctx* c = lane_context(k, m, device, lane, &rc);
+        rsmi_ctx* c = lane_context(k, m, device, replica, lane, &rc);
         if (c) (void)rsmi_warm(c);  // the context and each of its coalescing lanes
     }
 }
 
-long lane_stat(int k, int m, int device, const char* key) {
+long lane_stat(int k, int m, int device, const char* key, int replica) {
     long v = 0;
     for (int lane = 0; lane < kCallLanes; lane++) {
         int rc;
-        rsmi_ctx* c = lane_context(k, m, device, lane, &rc);
+        rsmi_ctx* c = lane_context(k, m, device, replica, lane, &rc);
         if (c) v += rsmi_get_stat(c, key);
     }
     return v;
 }
 
-Status Erasure::New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device) {
+Status Erasure::New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device, int replica) {
     if (data_blocks <= 0 || parity_blocks <= 0) return rsmi_status(RSMI_ERR_INV_SHARD_NUM);
     if (data_blocks + parity_blocks > 256) return rsmi_status(RSMI_ERR_MAX_SHARD_NUM);
     out->data_blocks_ = data_blocks;
     out->parity_blocks_ = parity_blocks;
     out->block_size_ = block_size;
     out->device_ = device;
+    out->replica_ = replica;
     return Status::Ok();
 }
 
@@ -207,7 +211,7 @@ Status Erasure::EncodeData(const Bytes& data, std::vector<Bytes>* shards) const 
     shards->assign(size_t(n), Bytes());
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc, replica_);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     uint8_t* flat = block_scratch(size_t(n) * S);
@@ -226,7 +230,7 @@ Status Erasure::EncodeDataWithCrc(const Bytes& data, std::vector<Bytes>* shards,
 Status Erasure::EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const {
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc, replica_);
     if (!c) return rsmi_status(rc);
     // Split's copy on this thread (concurrent callers copy in parallel), then coded in place
     copy_to_staging(flat, data.data(), data.size());
@@ -243,7 +247,7 @@ Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards
     if (raw32) raw32->clear();
     if (data.empty()) return Status::Ok();  // erasure.go:52-54
     int rc;
-    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc, replica_);
     if (!c) return rsmi_status(rc);
     const size_t S = rsmi_shard_size(data.size(), data_blocks_);
     uint8_t* flat = block_scratch(size_t(n) * S);
@@ -277,7 +281,7 @@ Status Erasure::reconstruct(std::vector<Bytes>& shards, bool data_only) const {
             if (i < data_blocks_) dp++;
         }
     if (np == n || (data_only && dp == data_blocks_)) return Status::Ok();
-    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc);
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc, replica_);
     if (!c) return rsmi_status(rc);
     // [][]byte -> one contiguous buffer for the C-ABI: the first k present rows, the only ones the
     // decode reads (upstream reconstruct(); missing and later rows: don't-care bytes)

@@ -21,9 +21,11 @@ namespace host {
 Status rsmi_status(int rc);
 int64_t ceil_frac(int64_t numerator, int64_t denominator);  // utils.go:6-21
 
-// Process-wide context per (k, m, device): NewErasure runs per block in the reference
-// (node.go:277,376) but the matrix / device plans are built once.
-rsmi_ctx* shared_context(int k, int m, int device, int* rc);
+// Process-wide context per (k, m, device, replica): NewErasure runs per block in the reference
+// (node.go:277,376) but the matrix / device plans are built once.  `replica` tells apart the
+// members of a Dag Node's device list that name the same device (DagNode::New with a device list:
+// every member has contexts, group-commit queue and coalescing lanes of its own).
+rsmi_ctx* shared_context(int k, int m, int device, int* rc, int replica = 0);
 // Per-block calls from concurrent threads (Erasure's encodes and reconstructs) go to kCallLanes
 // contexts per (k, m, device), one per calling thread in turn; lane 0 is the shared context.  One
 // (the default) keeps every caller in one group-commit queue, whose batches the context codes on
@@ -35,13 +37,13 @@ rsmi_ctx* shared_context(int k, int m, int device, int* rc);
 #define RSMI_HOST_CALL_LANES 1
 #endif
 constexpr int kCallLanes = RSMI_HOST_CALL_LANES;
-rsmi_ctx* call_context(int k, int m, int device, int* rc);
-// rsmi_get_stat summed over the lanes of (k, m, device) (the coalescing counters)
-long lane_stat(int k, int m, int device, const char* key);
+rsmi_ctx* call_context(int k, int m, int device, int* rc, int replica = 0);
+// rsmi_get_stat summed over the lanes of (k, m, device, replica) (the coalescing counters)
+long lane_stat(int k, int m, int device, const char* key, int replica = 0);
 // Bring up every lane's device resources (streams, plans, CRC tables) with one tiny encode each,
 // so the first concurrent calls do not pay for them (a Dag Node does this when it starts);
 // errors are left to the real calls, which fail loudly.
-void warm_contexts(int k, int m, int device);
+void warm_contexts(int k, int m, int device, int replica = 0);
 // Close every shared context (process shutdown, with no call in flight).
 void release_shared_contexts();
 
@@ -89,7 +91,8 @@ inline size_t staging_blocks(size_t block_bytes) {
 
 class Erasure {
 public:
-    static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0);
+    static Status New(int data_blocks, int parity_blocks, int64_t block_size, Erasure* out, int device = 0,
+                      int replica = 0);
     // through rsmi_encode_block_coalesced: concurrent Puts on one process-wide context are
     // batched on the GPU (group commit); a lone caller runs alone, unchanged
     Status EncodeData(const Bytes& data, std::vector<Bytes>* shards) const;
@@ -113,7 +116,7 @@ public:
 
 private:
     Status reconstruct(std::vector<Bytes>& shards, bool data_only) const;
-    int data_blocks_ = 0, parity_blocks_ = 0, device_ = 0;
+    int data_blocks_ = 0, parity_blocks_ = 0, device_ = 0, replica_ = 0;
     int64_t block_size_ = 0;
 };
 

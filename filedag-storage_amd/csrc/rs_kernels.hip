@@ -75,14 +75,19 @@ __device__ __forceinline__ T* block_rows(const BasesArg<TB>& bases, T* p, uint32
 }
 
 // A table launch's completion release (BlockBases::done_flag; every workgroup calls it once, as
-// its last act, with all its waves): the workgroup's stores are complete once the barrier passes
-// (its workgroup-scope release waits for them), the fetch-add at system scope writes the XCD's L2
-// back before it counts, and the launch's last workgroup resets the counter for the next launch
-// and releases the flag.  A table without a flag (and every table-less instantiation) skips it.
+// its last act, with all its waves).  Every thread first releases its own stores at system scope
+// (buffer_wbl2 + s_waitcnt vmcnt(0) in every wave): the barrier alone does not wait for other
+// waves' stores on gfx950 (back-off barrier, and a workgroup-scope release emits no vmcnt wait in
+// non-tgsplit mode), so without the per-wave fence waves 1..3 could still have parity or R(shard)
+// stores in flight to page-locked host memory when wave 0 counts.  After the barrier, one
+// system-scope fetch-add counts the workgroup, and the launch's last workgroup resets the counter
+// for the next launch and releases the flag.  A table without a flag (and every table-less
+// instantiation) skips all of it.  ISA check: DESIGN.md §4 (completion flags).
 template <bool TB>
 __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
     if constexpr (TB) {
         if (!bases.done_flag) return;  // kernel argument: uniform over the launch
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, every thread
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t old = __hip_atomic_fetch_add(bases.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -43,11 +43,16 @@ static uint8_t* pipe_area(rsmi_ctx* c, int slot, size_t bytes) {
 }
 
 // The context's two completion flags (caller holds ctx->mu): page-locked, 64 bytes apart, with
-// device counters zeroed on `st` before first use
+// device counters zeroed on `st` before first use.  The flag page is fine-grained
+// (hipHostMallocCoherent, whatever HIP_HOST_COHERENT says): the host spins on it while the kernel
+// runs, so the kernel's system-scope release store must reach host memory then, not at the end of
+// the kernel.  The R(shard) areas and shard buffers the flag guards may be
+// coarse-grained: the launch_done release (every wave: buffer_wbl2 sc0 sc1 + vmcnt(0), then the
+// counting atomic at system scope) writes their lines back to host memory before the flag moves.
 int done_area(rsmi_ctx* c, hipStream_t st) {
     if (c->h_done) return RSMI_OK;
     void* h = nullptr;
-    HIP_TRY(pinned_alloc(&h, 128));
+    HIP_TRY(hipHostMalloc(&h, 128, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h, 0, 128);
     uint8_t* hd = host_alias(h, 128);
     void* d = nullptr;
@@ -316,6 +321,9 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
     rsmi_ctx* x = nullptr;
     if ((*rc = rsmi_open(c->k, c->m, c->device, &x))) return nullptr;
     {
+        // the parent's coding options, read under its lock (rsmi_set_option writes them there;
+        // lock order c->lanes_mu, then c->mu, then x->mu, as in rsmi_set_option's lane loop)
+        std::lock_guard<std::mutex> gc(c->mu);
         std::lock_guard<std::mutex> gx(x->mu);
         x->opt_crc16_fold = c->opt_crc16_fold;
         x->opt_crc32_fold = c->opt_crc32_fold;
@@ -325,6 +333,9 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
         x->opt_small_bytes = c->opt_small_bytes;
         x->opt_coalesce_pipeline = c->opt_coalesce_pipeline;
         x->opt_coalesce_flag = c->opt_coalesce_flag;
+    }
+    {
+        std::lock_guard<std::mutex> gx(x->mu);
         *rc = ensure_device(x);
     }
     if (*rc) {

@@ -468,10 +468,12 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
         if ((rc = apply_option(c, key, value))) return rc;
     }
     // the coalescer's lane contexts code with the same options (the test hook stays with the
-    // context whose batches it fails)
+    // context whose batches it fails).  A lane whose open failed (or that opened out of order)
+    // leaves a null slot (lane_context): skip it.
     if (std::strcmp(key, "inject_host_fault") != 0) {
         std::lock_guard<std::mutex> g(c->lanes_mu);
         for (rsmi_ctx* l : c->lanes) {
+            if (!l) continue;
             std::lock_guard<std::mutex> gl(l->mu);
             (void)apply_option(l, key, value);
         }

@@ -158,8 +158,9 @@ struct rsmi_ctx {
     uint32_t* d_done_ctr = nullptr;
     uint32_t done_seq = 0;
     int opt_coalesce_flag = RSMI_COALESCE_FLAG;
-    long opt_coalesce_us = 0;     // extra wait for more callers before a coalesced batch runs
-    long opt_coalesce_max = 256;  // blocks per coalesced batch
+    // the coalescer's options are read by callers without ctx->mu (coalesce), so they are atomic
+    std::atomic<long> opt_coalesce_us{0};     // extra wait for more callers before a coalesced batch runs
+    std::atomic<long> opt_coalesce_max{256};  // blocks per coalesced batch
     std::string last_kernel;  // diagnostics (rsmi_last_kernel), under lk_mu
     mutable std::mutex lk_mu;
     // group commit for rsmi_encode_block_coalesced (see there)
@@ -184,8 +185,8 @@ struct rsmi_ctx {
     // Coalesced batches run on up to opt_coalesce_lanes lanes at once: lane 0 is this context, lane
     // i > 0 the child context lanes[i - 1] (same k, m, device and options; opened on first use), so
     // one batch can be coded while the next is launched and the callers' queue stays one queue
-    long opt_coalesce_lanes = RSMI_COALESCE_LANES;
-    long opt_coalesce_carry = RSMI_COALESCE_CARRY;  // batches a lane runs after its own before handing over (group_commit.hpp)
+    std::atomic<long> opt_coalesce_lanes{RSMI_COALESCE_LANES};
+    std::atomic<long> opt_coalesce_carry{RSMI_COALESCE_CARRY};  // batches a lane runs after its own before handing over (group_commit.hpp)
     std::vector<rsmi_ctx*> lanes;
     std::mutex lanes_mu;
 };

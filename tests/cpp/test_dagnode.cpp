@@ -50,6 +50,10 @@ static Bytes str(const char* s) { return Bytes(s, s + std::strlen(s)); }
 static size_t g_big = 262144, g_leaf = 1048590, g_huge = 4194304;
 static size_t g_fanout_min = size_t(128) << 10;  // sanitize: 0, so the fan-out pool runs at the small sizes
 static size_t big(long d = 0) { return size_t(long(g_big) + d); }
+// The Dag Nodes' device list (DagNode::New): {0}, or, for the suite's member pass, two members
+// naming device 0 (the GPU box has one GPU), so every per-key call and batch range is routed by
+// hash slot over two contexts.
+static std::vector<int> g_devices{0};
 
 static Bytes rand_bytes(std::mt19937_64& r, size_t n) {
     Bytes b(n);
@@ -71,7 +75,7 @@ struct Cluster {
             dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back(), engine));
             clients.push_back(dn.back());
         }
-        Status s = DagNode::New(cfg, clients, &node);
+        Status s = DagNode::New(cfg, clients, &node, g_devices);
         if (!s.ok()) {
             std::fprintf(stderr, "NewDagNode: %s\n", s.err.c_str());
             std::exit(2);
@@ -369,12 +373,20 @@ static void test_repair_datanode(bool batched) {
     if (batched)
         CHECK_OK(c.node->RepairDataNodeBatched(0, 6, 16, &repaired));
     else
-        CHECK_OK(c.node->RepairDataNode(0, 6));
+        CHECK_OK(c.node->RepairDataNodePerKey(0, 6));
     if (batched) CHECK(repaired == keys.size());
     c.dn[2]->SetOffline(false);
     for (size_t i = 0; i < keys.size(); i++) {
         auto want = oracle_shards(k, m, blocks[i]);
         CHECK(stored_shard(*c.dn[6], keys[i]) == want[6]);
+    }
+    // RepairDataNode itself (the batched form), onto the node wiped again: the same rows
+    if (!batched) {
+        c.dn[6]->server().Wipe();
+        c.dn[2]->SetOffline(true);
+        CHECK_OK(c.node->RepairDataNode(0, 6));
+        c.dn[2]->SetOffline(false);
+        for (size_t i = 0; i < keys.size(); i++) CHECK(stored_shard(*c.dn[6], keys[i]) == oracle_shards(k, m, blocks[i])[6]);
     }
     // a target that fails its writes: the first failing flush's error comes back (the next
     // window's fetch, running ahead on a helper thread, only read), and nothing counts as repaired
@@ -663,7 +675,7 @@ static void test_gpu_verified_reads() {
             clients.push_back(dn.back());
         }
         std::unique_ptr<DagNode> node;
-        CHECK_OK(DagNode::New(cfg, clients, &node));
+        CHECK_OK(DagNode::New(cfg, clients, &node, g_devices));
         node->HealthCheckAll();
         node->SetGpuVerifiedReads(true);
         std::mt19937_64 r(21);
@@ -733,6 +745,13 @@ static void test_concurrent_puts() {
     int rc;
     rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
     CHECK(ctx != nullptr);
+    // the coalescing counters summed over the node's members
+    auto lane_stat = [&](int kk, int mm, int, const char* key) {
+        long v = 0;
+        for (int i = 0; i < c.node->Members(); i++)
+            v += rsmi::host::lane_stat(kk, mm, c.node->MemberDevice(i), key, c.node->MemberReplica(i));
+        return v;
+    };
     // every Put and degraded Get through the group commit (no lone-caller path), so the counters
     // are exact
     c.node->SetLoneCallerPaths(false);
@@ -783,6 +802,58 @@ static void test_concurrent_puts() {
             CHECK(crc == rs_oracle_datanode_entry_crc(meta.data(), 4, want[s].data(), want[s].size()));
         }
     }
+}
+
+// A Dag Node on a device list (DagNode::New): every per-key call codes on the member that owns the
+// key's hash slot (hash_slot.go:20-22, crc16 IBM of the key & 0x3FFF, in contiguous ranges of
+// 16384 / members slots), and each member's group-commit queue sees exactly its own keys.  The two
+// members name the same device (one GPU per test box; the sanitizer build's fake device layer).
+static void test_member_routing() {
+    const int k = 10, m = 4, n = k + m;
+    const std::vector<int> saved = g_devices;
+    g_devices = {0, 0};
+    Cluster c(k, m);
+    g_devices = saved;
+    CHECK(c.node->Members() == 2);
+    CHECK(c.node->MemberReplica(0) == 0 && c.node->MemberReplica(1) == 1);
+    c.node->SetLoneCallerPaths(false);  // per-block Put through the member's group commit
+    long before[2], expect[2] = {0, 0};
+    for (int r = 0; r < 2; r++) before[r] = lane_stat(k, m, 0, "coalesced_calls", r);
+    std::mt19937_64 rng(31);
+    for (int i = 0; i < 48; i++) {
+        const std::string key = "bafkrei-route-" + std::to_string(i);
+        const int slot = rs_oracle_crc16_ibm(reinterpret_cast<const uint8_t*>(key.data()), key.size()) & 0x3FFF;
+        const int want = slot * 2 / 16384;
+        CHECK(c.node->MemberOfKey(key) == want);
+        expect[want]++;
+        const Bytes b = rand_bytes(rng, size_t(1000 + 97 * i));
+        CHECK_OK(c.node->Put(key, b));
+        const auto sh = oracle_shards(k, m, b);
+        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key) == sh[j]);
+    }
+    for (int r = 0; r < 2; r++) CHECK(lane_stat(k, m, 0, "coalesced_calls", r) - before[r] == expect[r]);
+    CHECK(expect[0] > 0 && expect[1] > 0);
+    c.node->SetLoneCallerPaths(true);
+    // four members: the slot's quarter
+    g_devices = {0, 0, 0, 0};
+    Cluster c4(2, 1);
+    g_devices = saved;
+    for (int i = 0; i < 64; i++) {
+        const std::string key = "QmRoute" + std::to_string(i * 7919);
+        const int slot = rs_oracle_crc16_ibm(reinterpret_cast<const uint8_t*>(key.data()), key.size()) & 0x3FFF;
+        CHECK(c4.node->MemberOfKey(key) == slot * 4 / 16384);
+    }
+    // an empty device list is refused
+    DagNodeConfig cfg;
+    cfg.data_blocks = 2;
+    cfg.parity_blocks = 1;
+    std::vector<std::shared_ptr<DataNodeClient>> cl;
+    for (int i = 0; i < 3; i++) {
+        cfg.nodes.push_back("x" + std::to_string(i));
+        cl.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back()));
+    }
+    std::unique_ptr<DagNode> d;
+    CHECK(!DagNode::New(cfg, cl, &d, std::vector<int>{}).ok());
 }
 
 // group_commit.hpp: an executor whose batch throws completes every request of that batch with
@@ -989,6 +1060,25 @@ int main(int argc, char** argv) {
         test_gpu_value_checksums();
         test_gpu_verified_reads();
         test_concurrent_puts();
+        test_member_routing();
+        // the member pass: the Dag Node tests again on a two-member device list, every shard
+        // and block still the oracle's
+        const int before = g_checks;
+        g_devices = {0, 0};
+        test_dagnode_123456();
+        test_rs10_4_failures();
+        test_read_repair();
+        test_repair_datanode(false);
+        test_repair_datanode(true);
+        test_putmany_batch();
+        test_getmany();
+        test_batches_span_staging_chunks();
+        test_migrate();
+        test_gpu_entry_checksums();
+        test_gpu_verified_reads();
+        test_concurrent_puts();
+        g_devices = {0};
+        std::printf("member pass: %d checks\n", g_checks - before);
     }
     release_shared_contexts();
     std::printf("%s: %d checks, %d failed\n", mode.c_str(), g_checks, g_fail);
