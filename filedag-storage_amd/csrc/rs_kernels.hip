@@ -83,11 +83,14 @@ __device__ __forceinline__ T* block_rows(const BasesArg<TB>& bases, T* p, uint32
 // system-scope fetch-add counts the workgroup, and the launch's last workgroup resets the counter
 // for the next launch and releases the flag.  A table without a flag (and every table-less
 // instantiation) skips all of it.  ISA check: DESIGN.md §4 (completion flags).
+#ifndef RSMI_FLAG_FENCE  // 0: round 5's release (wave 0 only), for the cost A/B (tools/Makefile variant)
+#define RSMI_FLAG_FENCE 1
+#endif
 template <bool TB>
 __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
     if constexpr (TB) {
         if (!bases.done_flag) return;  // kernel argument: uniform over the launch
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, every thread
+        if constexpr (RSMI_FLAG_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, every thread
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t old = __hip_atomic_fetch_add(bases.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -22,6 +22,7 @@
 #                    variant (tools/ua_ab.sh), then each library's FETCH_SIZE / WRITE_SIZE passes
 #   dagnode_env_ab   the Dag Node bench with ENV_AB=<variable> at ENV_VALUES (default 0 1), alternated
 #   latency          per-block call latencies (tools/latency)
+#   latency_ab       lone-call latencies on the product library and every tools/build/v_* variant
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
 #   threads_ab       THREADS_AB_CFG (default flag) on the product library and each tools/build/v_* variant
@@ -105,6 +106,18 @@ dagnode_env_ab)
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
+latency_ab)
+  # lone-call latencies (256 KiB, 4 MiB) on the product library and every tools/build/v_* variant,
+  # alternated three times
+  : > $O/latency_ab.txt
+  for rep in 1 2 3; do
+    for lib in filedag-storage_amd/lib tools/build/v_*/lib; do
+      v=$(basename $(dirname $lib)); [ "$lib" = filedag-storage_amd/lib ] && v=product
+      echo "== $v (round $rep)" >> $O/latency_ab.txt
+      LD_LIBRARY_PATH=$R/$lib timeout -k 10 200 ./tools/build/latency 262144 4194304 >> $O/latency_ab.txt 2>&1 || fail "latency_ab $v" $O/latency_ab.txt
+    done
+  done
+  grep -E "^==|lone Put|Split copy" $O/latency_ab.txt | cut -c1-200 ;;
 threads)
   timeout -k 10 300 ./tools/build/latency --threads > $O/threads.txt 2>&1 || fail threads $O/threads.txt
   cat $O/threads.txt ;;
