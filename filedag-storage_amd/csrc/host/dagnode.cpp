@@ -1180,7 +1180,9 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     std::future<std::vector<Status>> writing;
     auto join_writes = [&]() -> Status {
         if (!writing.valid()) return Status::Ok();
+        const auto tw = PhaseClock::now();
         const std::vector<Status> ps = writing.get();
+        trace_add(kTraceWaitWrites, tw, PhaseClock::now());
         for (const Status& st : ps) {
             if (!st.ok()) return st;
             done++;
@@ -1335,7 +1337,9 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         }
         c0 = c1;
         nk = nk1;
+        const auto tw = PhaseClock::now();
         if (nk1) fr = ahead.get();
+        trace_add(kTraceWaitFetch, tw, PhaseClock::now());
     }
     for (auto& g : groups) {
         s = flush(g.first, g.second);
@@ -1349,7 +1353,21 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
 
 void DagNode::phase_add(Phase p, PhaseClock::time_point t0) {
     if (!phase_on_.load(std::memory_order_relaxed)) return;
-    phase_ns_[int(p)] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t0).count());
+    const auto t1 = PhaseClock::now();
+    phase_ns_[int(p)] += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+    trace_add(int(p), t0, t1);
+}
+
+void DagNode::trace_add(int id, PhaseClock::time_point t0, PhaseClock::time_point t1) {
+    if (!phase_on_.load(std::memory_order_relaxed) || !trace_on_.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> g(trace_mu_);
+    const auto sec = [&](PhaseClock::time_point t) { return std::chrono::duration<double>(t - trace_epoch_).count(); };
+    trace_.push_back(PhaseEvent{id, uint64_t(std::hash<std::thread::id>()(std::this_thread::get_id())), sec(t0), sec(t1)});
+}
+
+std::vector<DagNode::PhaseEvent> DagNode::PhaseEvents() {
+    std::lock_guard<std::mutex> g(trace_mu_);
+    return trace_;
 }
 
 std::array<double, 4> DagNode::PhaseSeconds() const {
@@ -1360,6 +1378,9 @@ std::array<double, 4> DagNode::PhaseSeconds() const {
 
 void DagNode::ResetPhases() {
     for (auto& x : phase_ns_) x = 0;
+    std::lock_guard<std::mutex> g(trace_mu_);
+    trace_.clear();
+    trace_epoch_ = PhaseClock::now();
 }
 
 }  // namespace host

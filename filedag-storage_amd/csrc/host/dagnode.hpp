@@ -163,12 +163,27 @@ public:
     void SetPhaseTiming(bool v) { phase_on_ = v; }
     std::array<double, 4> PhaseSeconds() const;
     void ResetPhases();
+    // With phase timing on, also keep every phase interval (phase, thread, start and end in
+    // seconds since ResetPhases) for a timeline of the overlap (diagnostic, tools/bench_dagnode)
+    struct PhaseEvent {
+        int phase;
+        uint64_t thread;
+        double t0, t1;
+    };
+    void SetPhaseTrace(bool v) { trace_on_ = v; }
+    static constexpr int kTraceWaitFetch = 4, kTraceWaitWrites = 5;  // trace-only ids: waits on helpers
+    std::vector<PhaseEvent> PhaseEvents();
 
 private:
     using PhaseClock = std::chrono::steady_clock;
     void phase_add(Phase p, PhaseClock::time_point t0);
+    void trace_add(int id, PhaseClock::time_point t0, PhaseClock::time_point t1);
     std::atomic<bool> phase_on_{false};
     std::atomic<uint64_t> phase_ns_[4] = {};
+    std::atomic<bool> trace_on_{false};
+    std::mutex trace_mu_;
+    std::vector<PhaseEvent> trace_;
+    PhaseClock::time_point trace_epoch_ = PhaseClock::now();
     struct Fetched {
         Meta meta;
         std::vector<Bytes> shards;

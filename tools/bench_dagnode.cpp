@@ -46,8 +46,17 @@ int main(int argc, char** argv) {
         dn.push_back(std::make_shared<InProcDataNode>(cfg.nodes.back()));
         cl.push_back(dn.back());
     }
+    // BENCH_DAGNODE_DEVICES="0,0": the Dag Node on a device list (member routing, DagNode::New)
+    std::vector<int> devices;
+    if (const char* e = std::getenv("BENCH_DAGNODE_DEVICES"))
+        for (const char* p = e; *p;) {
+            devices.push_back(std::atoi(p));
+            while (*p && *p != ',') p++;
+            if (*p == ',') p++;
+        }
+    if (devices.empty()) devices.push_back(0);
     std::unique_ptr<DagNode> d;
-    if (!DagNode::New(cfg, cl, &d).ok()) return 2;
+    if (!DagNode::New(cfg, cl, &d, devices).ok()) return 2;
     d->HealthCheckAll();
     std::mt19937_64 r(1);
     std::vector<std::string> keys;
@@ -108,7 +117,13 @@ int main(int argc, char** argv) {
     const int T = 16;
     long c0 = 0, b0 = 0;
     int rc;
-    rsmi_ctx* ctx = shared_context(k, m, 0, &rc);
+    rsmi_ctx* ctx = shared_context(k, m, d->MemberDevice(0), &rc, d->MemberReplica(0));
+    // the coalescing counters summed over the node's members
+    auto node_stat = [&](const char* key) {
+        long v = 0;
+        for (int i = 0; i < d->Members(); i++) v += lane_stat(k, m, d->MemberDevice(i), key, d->MemberReplica(i));
+        return v;
+    };
     // an untimed pass first: the threads' page-locked scratch comes from the pool their
     // predecessors leave (erasure.hpp block_scratch), as in a server whose workers come and go
     auto put_threads = [&] {
@@ -121,8 +136,8 @@ int main(int argc, char** argv) {
     };
     if (!std::getenv("BENCH_DAGNODE_NO_WARM")) put_threads();  // diagnostic switch: no untimed pass
     if (ctx) {
-        c0 = lane_stat(k, m, 0, "coalesced_calls");
-        b0 = lane_stat(k, m, 0, "coalesced_batches");
+        c0 = node_stat("coalesced_calls");
+        b0 = node_stat("coalesced_batches");
     }
     d->SetPhaseTiming(true);
     d->ResetPhases();
@@ -131,8 +146,8 @@ int main(int argc, char** argv) {
     const double putT = secs(t0);
     phase_json("put_threads", putT);
     d->SetPhaseTiming(false);
-    const long calls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - c0 : 0;
-    const long batches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - b0 : 0;
+    const long calls = ctx ? node_stat("coalesced_calls") - c0 : 0;
+    const long batches = ctx ? node_stat("coalesced_batches") - b0 : 0;
     // CRC + framing alone (the datanode's byte-serial CPU loop), for context
     t0 = clk::now();
     volatile uint16_t sink = 0;
@@ -170,7 +185,7 @@ int main(int argc, char** argv) {
         }
     }
     // degraded Get from 16 threads: the reconstructs coalesce (one erasure pattern)
-    const long gc0 = ctx ? lane_stat(k, m, 0, "coalesced_calls") : 0, gb0 = ctx ? lane_stat(k, m, 0, "coalesced_batches") : 0;
+    const long gc0 = ctx ? node_stat("coalesced_calls") : 0, gb0 = ctx ? node_stat("coalesced_batches") : 0;
     d->SetPhaseTiming(true);
     d->ResetPhases();
     t0 = clk::now();
@@ -186,8 +201,8 @@ int main(int argc, char** argv) {
     const double getT = secs(t0);
     phase_json("get_threads", getT);
     d->SetPhaseTiming(false);
-    const long gcalls = ctx ? lane_stat(k, m, 0, "coalesced_calls") - gc0 : 0;
-    const long gbatches = ctx ? lane_stat(k, m, 0, "coalesced_batches") - gb0 : 0;
+    const long gcalls = ctx ? node_stat("coalesced_calls") - gc0 : 0;
+    const long gbatches = ctx ? node_stat("coalesced_batches") - gb0 : 0;
     // the same degraded reads with the checksums checked on the GPU instead of by each datanode
     d->SetGpuVerifiedReads(true);
     t0 = clk::now();
@@ -227,10 +242,30 @@ int main(int argc, char** argv) {
     dn[size_t(rj)]->server().Wipe();
     size_t rep = 0;
     d->SetPhaseTiming(true);
+    // BENCH_DAGNODE_TRACE=1: the batched repair's phase intervals as a TRACE line (thread index,
+    // phase id: 0 fetch, 1 stage, 2 codec, 3 put, 4 wait for the fetch ahead, 5 wait for the writes;
+    // start and end in ms)
+    const bool trace = std::getenv("BENCH_DAGNODE_TRACE") != nullptr;
+    d->SetPhaseTrace(trace);
     d->ResetPhases();
     t0 = clk::now();
     d->RepairDataNodeBatched(0, rj, 256, &rep);
     const double repb = secs(t0);
+    if (trace) {
+        const auto ev = d->PhaseEvents();
+        std::vector<uint64_t> tids;
+        std::string out;
+        for (const auto& e : ev) {
+            size_t ti = std::find(tids.begin(), tids.end(), e.thread) - tids.begin();
+            if (ti == tids.size()) tids.push_back(e.thread);
+            char buf[96];
+            std::snprintf(buf, sizeof buf, "%s[%zu,%d,%.3f,%.3f]", out.empty() ? "" : ",", ti, e.phase, e.t0 * 1e3, e.t1 * 1e3);
+            out += buf;
+        }
+        std::printf("TRACE {\"leg\": \"repair_batched\", \"k\": %d, \"m\": %d, \"B\": %zu, \"wall_ms\": %.3f, \"events\": [%s]}\n",
+                    k, m, B, repb * 1e3, out.c_str());
+        d->SetPhaseTrace(false);
+    }
     phase_json("repair_batched", repb);
     d->SetPhaseTiming(false);
     // mutcask-backed datanodes (server.go:207): every value also carries a CRC-32 of the whole
