@@ -415,13 +415,13 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             for (size_t i : g.second) results[i] = Put(keys[i], blocks[i]);
             continue;
         }
-        int rc;
         const size_t S = rsmi_shard_size(B, k);
-        // Two halves of the thread's staging: a chunk's datanode writes run on a helper thread
-        // while the next chunk is staged and coded into the other half (the GPU call leaves the
-        // cores free for the writes), as RepairDataNodeBatched does.  A chunk joins the previous
-        // chunk's writes before it hands over its own, and the group joins the last before the
-        // next group (or the return), so every block's outcome is the sequential loop's.
+        // Two halves of the thread's staging: a chunk is staged into one half, then a helper task
+        // runs its codec call and its datanode writes while the next chunk is staged into the other
+        // half (the codec call overlaps the next staging copy, the writes the next codec call).  A
+        // chunk joins the previous chunk's task before it hands over its own, and the group joins
+        // the last before the next group (or the return), so every block's outcome is the
+        // sequential loop's.
         const size_t chunk = std::max<size_t>(1, staging_blocks(size_t(n) * S) / (RSMI_BATCH_SERIAL ? 1 : 2));
         const size_t half = std::min(chunk, g.second.size()) * size_t(n) * S;
         const Bytes meta = encode_meta(int32_t(B));
@@ -443,7 +443,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
             // the chunk's blocks ordered by member (a device list): each member codes one range
-            const MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(keys[g.second[c0 + j]]); });
+            MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(keys[g.second[c0 + j]]); });
             {
                 std::vector<size_t> tmp(nb);
                 for (size_t j = 0; j < nb; j++) tmp[j] = g.second[c0 + ord.perm[j]];
@@ -460,30 +460,26 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 }
             });
             phase_add(Phase::Stage, t0);
-            const auto t1 = PhaseClock::now();
-            std::vector<uint32_t> raw, raw32;
-            if (gpu_checksums_) {
-                raw.resize(nb * size_t(n));
-                raw32.resize(want32 ? nb * size_t(n) : 0);
-            }
-            rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
-                uint8_t* f = flat + j0 * size_t(n) * S;
-                if (!gpu_checksums_)
-                    return rsmi_encode_batch_host(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt);
-                return rsmi_encode_batch_host_crcs(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt,
-                                                   raw.data() + j0 * size_t(n),
-                                                   want32 ? raw32.data() + j0 * size_t(n) : nullptr);
-            });
-            phase_add(Phase::Codec, t1);
-            join_writes();  // the other half is free again
-            if (rc) {
-                for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
-                continue;
-            }
-            // the blocks' datanode writes run concurrently (the reference's concurrent Puts),
+            join_writes();  // the previous chunk's task ends before this one starts
+            // the codec call, then the blocks' datanode writes (the reference's concurrent Puts),
             // each with its own node fan-out, each shard a view of the staging
-            writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, n, wq, want32,
-                                                      raw = std::move(raw), raw32 = std::move(raw32)] {
+            writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, k, n, wq, want32,
+                                                      ord = std::move(ord)] {
+                const auto t1 = PhaseClock::now();
+                std::vector<uint32_t> raw(gpu_checksums_ ? nb * size_t(n) : 0), raw32(want32 ? nb * size_t(n) : 0);
+                const int rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                    uint8_t* f = flat + j0 * size_t(n) * S;
+                    if (!gpu_checksums_)
+                        return rsmi_encode_batch_host(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt);
+                    return rsmi_encode_batch_host_crcs(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt,
+                                                       raw.data() + j0 * size_t(n),
+                                                       want32 ? raw32.data() + j0 * size_t(n) : nullptr);
+                });
+                phase_add(Phase::Codec, t1);
+                if (rc) {
+                    for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
+                    return;
+                }
                 const auto t2 = PhaseClock::now();
                 fan_keys(int(nb), [&](int j) {
                     const uint8_t* bb = flat + size_t(j) * n * S;
@@ -1172,11 +1168,14 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     // (block size, survivor pattern) -> pending keys
     std::map<std::pair<int, std::string>, std::vector<Pending>> groups;
     DataNodeClient& target = *nodes_[to].client;
-    // The rebuilt rows of one flush go to the target on a helper thread while the next flush
-    // stages and codes into the other of two page-locked buffers (the GPU call leaves the cores
-    // free for the writes). A flush joins the previous flush's writes, in key order, before it
-    // starts its own, and every return joins them first, so the rows written, the count and the
-    // first error returned are those of the sequential loop.
+    // A flush stages its keys' survivors into one of two page-locked buffers (the halves of the
+    // thread's staging), then hands the buffer to a helper task that runs the codec call and writes
+    // the rebuilt rows to the target; the next flush stages into the other half meanwhile, so the
+    // codec call overlaps the next staging copy as well as the next window's fetch.  A flush joins
+    // the previous task before it launches its own (at most one in flight; the staging only grows
+    // after it is joined), and every return joins it first, so the rows written, the count and the
+    // first error returned (in key order; a codec error counts for every key of its flush, none
+    // written) are those of the sequential loop.
     std::future<std::vector<Status>> writing;
     auto join_writes = [&]() -> Status {
         if (!writing.valid()) return Status::Ok();
@@ -1193,22 +1192,19 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
-        int rc;
         const size_t S = rsmi_shard_size(size_t(size), k), nb = pend.size();
         std::vector<uint8_t> present(static_cast<size_t>(n)), required(static_cast<size_t>(n), 0);
         for (int i = 0; i < n; i++) present[i] = uint8_t(gk.second[i] == '1');
         required[to] = 1;
         // the keys ordered by member (a device list): each member rebuilds one range; the
         // writes' outcomes are taken back in key order
-        const MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(pend[j].key); });
+        MemberOrder ord = member_order(nb, [&](size_t j) { return MemberOfKey(pend[j].key); });
         // the fetch returns exactly the k survivors the plan reads (fetch_for_repair stops at
         // the read quorum k), and only those are staged; the rows being rebuilt are not
         const auto t0 = PhaseClock::now();
-        // the two buffers are the halves of the thread's staging (kept warm by the batch calls);
-        // it only grows after the writes reading the other half are joined
         PinnedBuf& st = thread_staging();
         const size_t bytes = nb * size_t(n) * S;
-        if (st.capacity() < 2 * bytes) {
+        if (st.capacity() < 2 * bytes) {  // growing frees the buffer the task may be reading
             const Status w = join_writes();
             if (!w.ok()) return w;
         }
@@ -1224,35 +1220,40 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, p.shards[i].data(), S);
         });
         phase_add(Phase::Stage, t0);
-        // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
-        const auto t1 = PhaseClock::now();
-        const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
-        std::vector<uint32_t> r16(gpu_checksums_ ? nb * size_t(n) : 0), r32(want32 ? nb * size_t(n) : 0);
-        rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
-            uint8_t* f = flat + j0 * size_t(n) * S;
-            if (!gpu_checksums_)
-                return rsmi_reconstruct_rows_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), required.data());
-            return rsmi_reconstruct_rows_batch_host_crcs(ctx, f, size_t(n) * S, S, cnt, present.data(), required.data(),
-                                                         r16.data() + j0 * size_t(n),
-                                                         want32 ? r32.data() + j0 * size_t(n) : nullptr);
-        });
-        phase_add(Phase::Codec, t1);
-        const Status w = join_writes();
-        if (!w.ok()) return w;
-        if (rc) return rsmi_status(rc);
-        // the rebuilt rows go to the target concurrently, each as a view of the staging buffer;
-        // outcomes are taken in key order by the next join
         std::vector<std::string> wkeys(nb);
         for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[ord.perm[j]].key);
         pend.clear();
+        // the previous flush's task (its codec call and writes) ends before this one starts
+        const Status w = join_writes();
+        if (!w.ok()) return w;
+        // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
+        const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
         writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size),
-                                                  perm = ord.perm, wkeys = std::move(wkeys), r16 = std::move(r16),
-                                                  r32 = std::move(r32)] {
+                                                  ord = std::move(ord), present = std::move(present),
+                                                  required = std::move(required), wkeys = std::move(wkeys)] {
+            const size_t nw = wkeys.size();
+            std::vector<uint32_t> r16(gpu_checksums_ ? nw * size_t(n) : 0), r32(want32 ? nw * size_t(n) : 0);
+            const auto t1 = PhaseClock::now();
+            const int rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                uint8_t* f = flat + j0 * size_t(n) * S;
+                if (!gpu_checksums_)
+                    return rsmi_reconstruct_rows_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(),
+                                                            required.data());
+                return rsmi_reconstruct_rows_batch_host_crcs(ctx, f, size_t(n) * S, S, cnt, present.data(),
+                                                             required.data(), r16.data() + j0 * size_t(n),
+                                                             want32 ? r32.data() + j0 * size_t(n) : nullptr);
+            });
+            phase_add(Phase::Codec, t1);
+            std::vector<Status> ps(nw);  // by key order (perm[j]: slot j's key)
+            if (rc) {
+                for (auto& x : ps) x = rsmi_status(rc);
+                return ps;
+            }
+            // the rebuilt rows go to the target concurrently, each as a view of the staging buffer
             const auto t2 = PhaseClock::now();
-            std::vector<Status> ps(wkeys.size());  // by key order (perm[j]: slot j's key)
-            fan_keys(int(wkeys.size()), [&](int j) {
+            fan_keys(int(nw), [&](int j) {
                 const ByteView shard(flat + (size_t(j) * n + size_t(to)) * S, S);
-                Status& out = ps[perm[size_t(j)]];
+                Status& out = ps[ord.perm[size_t(j)]];
                 if (!gpu_checksums_) {
                     out = target.Put(wkeys[j], meta, shard);
                     return;

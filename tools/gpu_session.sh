@@ -22,6 +22,7 @@
 #                    variant (tools/ua_ab.sh), then each library's FETCH_SIZE / WRITE_SIZE passes
 #   dagnode_env_ab   the Dag Node bench with ENV_AB=<variable> at ENV_VALUES (default 0 1), alternated
 #   latency          per-block call latencies (tools/latency)
+#   dagnode_trace    the Dag Node bench with the batched repair's phase timeline (BENCH_DAGNODE_TRACE)
 #   latency_ab       lone-call latencies on the product library and every tools/build/v_* variant
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
@@ -106,6 +107,17 @@ dagnode_env_ab)
 latency)
   timeout -k 10 200 ./tools/build/latency > $O/latency.txt 2>&1 || fail latency $O/latency.txt
   cat $O/latency.txt ;;
+dagnode_trace)
+  # the Dag Node bench (GPU codec) with the batched repair's phase timeline (TRACE lines,
+  # tools/trace_timeline.py), RS(16,4) 4 MiB and RS(10,4) 256 KiB, twice each
+  : > $O/dagnode_trace.txt
+  for rep in 1 2; do
+    for shape in "16 4 4194304 64" "10 4 262144 512"; do
+      BENCH_DAGNODE_TRACE=1 timeout -k 10 300 ./tools/build/bench_dagnode $shape >> $O/dagnode_trace.txt 2>&1 || fail "dagnode_trace $shape" $O/dagnode_trace.txt
+    done
+  done
+  python3 tools/trace_timeline.py $O/dagnode_trace.txt
+  grep -E "^(PutMany|Repair|RepairDataNode)" $O/dagnode_trace.txt ;;
 latency_ab)
   # lone-call latencies (256 KiB, 4 MiB) on the product library and every tools/build/v_* variant,
   # alternated three times
