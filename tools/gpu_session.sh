@@ -23,6 +23,7 @@
 #   dagnode_env_ab   the Dag Node bench with ENV_AB=<variable> at ENV_VALUES (default 0 1), alternated
 #   latency          per-block call latencies (tools/latency)
 #   dagnode_trace    the Dag Node bench with the batched repair's phase timeline (BENCH_DAGNODE_TRACE)
+#   groupcost        a small zero-copy group's fixed cost: launch, dispatch, load round trip, tail
 #   latency_ab       lone-call latencies on the product library and every tools/build/v_* variant
 #   threads          concurrent coalesced encodes, contexts x lanes (tools/latency --threads)
 #   threads_pipe     the same at 16 threads, option coalesce_pipeline off / on alternated (THREADS_CFG=pipe)
@@ -118,6 +119,16 @@ dagnode_trace)
   done
   python3 tools/trace_timeline.py $O/dagnode_trace.txt
   grep -E "^(PutMany|Repair|RepairDataNode)" $O/dagnode_trace.txt ;;
+groupcost)
+  # a small zero-copy group's fixed cost split (tools/groupcost_probe.hip), page-locked host data,
+  # then device data, twice each
+  : > $O/groupcost.txt
+  for rep in 1 2; do
+    for a in "" --device-data; do
+      timeout -k 10 120 ./tools/build/groupcost_probe $a >> $O/groupcost.txt 2>&1 || fail "groupcost $a" $O/groupcost.txt
+    done
+  done
+  cat $O/groupcost.txt ;;
 latency_ab)
   # lone-call latencies (256 KiB, 4 MiB) on the product library and every tools/build/v_* variant,
   # alternated three times
