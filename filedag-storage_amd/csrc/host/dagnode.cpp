@@ -13,6 +13,11 @@
 #ifndef RSMI_BATCH_SERIAL
 #define RSMI_BATCH_SERIAL 0
 #endif
+// 1: PutMany and RepairDataNodeBatched run each chunk's codec call on the calling thread, before
+// the chunk's writes are handed to the helper (round 5's order), for same-box A/B library builds
+#ifndef RSMI_BATCH_CODEC_INLINE
+#define RSMI_BATCH_CODEC_INLINE 0
+#endif
 
 namespace rsmi {
 namespace host {
@@ -460,22 +465,30 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 }
             });
             phase_add(Phase::Stage, t0);
-            join_writes();  // the previous chunk's task ends before this one starts
-            // the codec call, then the blocks' datanode writes (the reference's concurrent Puts),
-            // each with its own node fan-out, each shard a view of the staging
-            writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, k, n, wq, want32,
-                                                      ord = std::move(ord)] {
+            // the chunk's codec call (the task's first step; RSMI_BATCH_CODEC_INLINE: here)
+            auto raw = std::make_shared<std::vector<uint32_t>>(gpu_checksums_ ? nb * size_t(n) : 0);
+            auto raw32 = std::make_shared<std::vector<uint32_t>>(want32 ? nb * size_t(n) : 0);
+            auto code = [this, flat, S, k, n, want32, raw, raw32, ord = std::make_shared<MemberOrder>(std::move(ord))] {
                 const auto t1 = PhaseClock::now();
-                std::vector<uint32_t> raw(gpu_checksums_ ? nb * size_t(n) : 0), raw32(want32 ? nb * size_t(n) : 0);
-                const int rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                const int rc = code_members(*ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
                     uint8_t* f = flat + j0 * size_t(n) * S;
                     if (!gpu_checksums_)
                         return rsmi_encode_batch_host(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt);
                     return rsmi_encode_batch_host_crcs(ctx, f, size_t(n) * S, f + size_t(k) * S, size_t(n) * S, S, cnt,
-                                                       raw.data() + j0 * size_t(n),
-                                                       want32 ? raw32.data() + j0 * size_t(n) : nullptr);
+                                                       raw->data() + j0 * size_t(n),
+                                                       want32 ? raw32->data() + j0 * size_t(n) : nullptr);
                 });
                 phase_add(Phase::Codec, t1);
+                return rc;
+            };
+            const bool inline_codec = RSMI_BATCH_CODEC_INLINE;
+            const int pre = inline_codec ? code() : RSMI_OK;
+            join_writes();  // the previous chunk's task ends before this one starts
+            // the codec call, then the blocks' datanode writes (the reference's concurrent Puts),
+            // each with its own node fan-out, each shard a view of the staging
+            writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, n, wq, want32,
+                                                      code, pre, inline_codec, raw, raw32] {
+                const int rc = inline_codec ? pre : code();
                 if (rc) {
                     for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
                     return;
@@ -491,10 +504,10 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                             res[i] = cl.Put(keys[idx[j]], meta, shard);
                             return;
                         }
-                        const uint16_t c16 = entry_checksum(meta, S, raw[j * n + i]);
+                        const uint16_t c16 = entry_checksum(meta, S, (*raw)[j * n + i]);
                         res[i] = want32 && cl.WantsValueChecksum()
                                      ? cl.PutWithChecksums(keys[idx[j]], meta, shard, c16,
-                                                           value_checksum(meta, S, c16, raw32[j * n + i]))
+                                                           value_checksum(meta, S, c16, (*raw32)[j * n + i]))
                                      : cl.PutWithChecksum(keys[idx[j]], meta, shard, c16);
                     }, S);
                     QuorumWait w(wq, n - wq + 1);
@@ -1223,27 +1236,37 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         std::vector<std::string> wkeys(nb);
         for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[ord.perm[j]].key);
         pend.clear();
-        // the previous flush's task (its codec call and writes) ends before this one starts
-        const Status w = join_writes();
-        if (!w.ok()) return w;
         // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
         const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
-        writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size),
-                                                  ord = std::move(ord), present = std::move(present),
-                                                  required = std::move(required), wkeys = std::move(wkeys)] {
-            const size_t nw = wkeys.size();
-            std::vector<uint32_t> r16(gpu_checksums_ ? nw * size_t(n) : 0), r32(want32 ? nw * size_t(n) : 0);
+        // the flush's codec call (the task's first step; RSMI_BATCH_CODEC_INLINE: here)
+        auto r16 = std::make_shared<std::vector<uint32_t>>(gpu_checksums_ ? nb * size_t(n) : 0);
+        auto r32 = std::make_shared<std::vector<uint32_t>>(want32 ? nb * size_t(n) : 0);
+        auto po = std::make_shared<MemberOrder>(std::move(ord));
+        auto code = [this, flat, S, n, want32, r16, r32, po, present = std::move(present),
+                     required = std::move(required)] {
             const auto t1 = PhaseClock::now();
-            const int rc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+            const int rc = code_members(*po, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
                 uint8_t* f = flat + j0 * size_t(n) * S;
                 if (!gpu_checksums_)
                     return rsmi_reconstruct_rows_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(),
                                                             required.data());
                 return rsmi_reconstruct_rows_batch_host_crcs(ctx, f, size_t(n) * S, S, cnt, present.data(),
-                                                             required.data(), r16.data() + j0 * size_t(n),
-                                                             want32 ? r32.data() + j0 * size_t(n) : nullptr);
+                                                             required.data(), r16->data() + j0 * size_t(n),
+                                                             want32 ? r32->data() + j0 * size_t(n) : nullptr);
             });
             phase_add(Phase::Codec, t1);
+            return rc;
+        };
+        const bool inline_codec = RSMI_BATCH_CODEC_INLINE;
+        const int pre = inline_codec ? code() : RSMI_OK;
+        // the previous flush's task (its codec call and writes) ends before this one starts
+        const Status w = join_writes();
+        if (!w.ok()) return w;
+        writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size), po,
+                                                  code, pre, inline_codec, r16, r32, wkeys = std::move(wkeys)] {
+            const size_t nw = wkeys.size();
+            const int rc = inline_codec ? pre : code();
+            const MemberOrder& ord = *po;
             std::vector<Status> ps(nw);  // by key order (perm[j]: slot j's key)
             if (rc) {
                 for (auto& x : ps) x = rsmi_status(rc);
@@ -1258,9 +1281,9 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                     out = target.Put(wkeys[j], meta, shard);
                     return;
                 }
-                const uint16_t c16 = entry_checksum(meta, S, r16[size_t(j) * n + size_t(to)]);
+                const uint16_t c16 = entry_checksum(meta, S, (*r16)[size_t(j) * n + size_t(to)]);
                 out = want32 ? target.PutWithChecksums(wkeys[j], meta, shard, c16,
-                                                       value_checksum(meta, S, c16, r32[size_t(j) * n + size_t(to)]))
+                                                       value_checksum(meta, S, c16, (*r32)[size_t(j) * n + size_t(to)]))
                              : target.PutWithChecksum(wkeys[j], meta, shard, c16);
             });
             phase_add(Phase::Put, t2);
