@@ -13,10 +13,15 @@
 #ifndef RSMI_BATCH_SERIAL
 #define RSMI_BATCH_SERIAL 0
 #endif
-// 1: PutMany and RepairDataNodeBatched run each chunk's codec call on the calling thread, before
-// the chunk's writes are handed to the helper (round 5's order), for same-box A/B library builds
-#ifndef RSMI_BATCH_CODEC_INLINE
-#define RSMI_BATCH_CODEC_INLINE 0
+// Where PutMany and RepairDataNodeBatched run a chunk's codec call: on the calling thread before
+// the chunk's writes go to the helper task, or as the task's first step, overlapping the next
+// chunk's staging copy.  The calling thread's critical path per chunk is max(stage + codec,
+// writes) in the first form and max(stage, codec + writes) in the second, so the codec call goes
+// with the shorter of the two: 0 = chosen per chunk from the previous chunk's measured staging and
+// write times (default), 1 = always on the calling thread (round 5), 2 = always in the task (A/B
+// library builds, profiles/r06/b/).
+#ifndef RSMI_BATCH_CODEC_PLACE
+#define RSMI_BATCH_CODEC_PLACE 0
 #endif
 
 namespace rsmi {
@@ -445,6 +450,9 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
             if (writing.valid()) writing.get();
         };
         int cur = 0;
+        // the previous chunk's staging and write times, for the codec call's placement
+        int64_t last_stage = 0;
+        auto last_writes = std::make_shared<std::atomic<int64_t>>(0);
         for (size_t c0 = 0; c0 < g.second.size(); c0 += chunk) {
             const size_t nb = std::min(chunk, g.second.size() - c0);
             // the chunk's blocks ordered by member (a device list): each member codes one range
@@ -465,7 +473,8 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 }
             });
             phase_add(Phase::Stage, t0);
-            // the chunk's codec call (the task's first step; RSMI_BATCH_CODEC_INLINE: here)
+            last_stage = std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t0).count();
+            // the chunk's codec call: here or as the task's first step (RSMI_BATCH_CODEC_PLACE)
             auto raw = std::make_shared<std::vector<uint32_t>>(gpu_checksums_ ? nb * size_t(n) : 0);
             auto raw32 = std::make_shared<std::vector<uint32_t>>(want32 ? nb * size_t(n) : 0);
             auto code = [this, flat, S, k, n, want32, raw, raw32, ord = std::make_shared<MemberOrder>(std::move(ord))] {
@@ -481,13 +490,14 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                 phase_add(Phase::Codec, t1);
                 return rc;
             };
-            const bool inline_codec = RSMI_BATCH_CODEC_INLINE;
+            const bool inline_codec = RSMI_BATCH_CODEC_PLACE == 1 ||
+                                      (RSMI_BATCH_CODEC_PLACE == 0 && last_writes->load() > last_stage);
             const int pre = inline_codec ? code() : RSMI_OK;
             join_writes();  // the previous chunk's task ends before this one starts
             // the codec call, then the blocks' datanode writes (the reference's concurrent Puts),
             // each with its own node fan-out, each shard a view of the staging
             writing = std::async(std::launch::async, [this, &keys, &results, &meta, idx, nb, flat, S, n, wq, want32,
-                                                      code, pre, inline_codec, raw, raw32] {
+                                                      code, pre, inline_codec, raw, raw32, last_writes] {
                 const int rc = inline_codec ? pre : code();
                 if (rc) {
                     for (size_t j = 0; j < nb; j++) results[idx[j]] = rsmi_status(rc);
@@ -515,6 +525,7 @@ Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<
                     results[idx[j]] = w.result("Write failed. Insufficient number of nodes online");
                 });
                 phase_add(Phase::Put, t2);
+                last_writes->store(std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t2).count());
             });
             cur ^= 1;
             if (RSMI_BATCH_SERIAL) join_writes();
@@ -1202,6 +1213,9 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
         return Status::Ok();
     };
     int cur = 0;
+    // the previous flush's staging and write times, for the codec call's placement
+    int64_t last_stage = 0;
+    auto last_writes = std::make_shared<std::atomic<int64_t>>(0);
     auto flush = [&](const std::pair<int, std::string>& gk, std::vector<Pending>& pend) -> Status {
         if (pend.empty()) return Status::Ok();
         const int size = gk.first;
@@ -1233,12 +1247,13 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                 if (present[i]) std::memcpy(flat + (size_t(j) * n + i) * S, p.shards[i].data(), S);
         });
         phase_add(Phase::Stage, t0);
+        last_stage = std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t0).count();
         std::vector<std::string> wkeys(nb);
         for (size_t j = 0; j < nb; j++) wkeys[j] = std::move(pend[ord.perm[j]].key);
         pend.clear();
         // the rebuilt rows' checksums come from the GPU pass too (sender checksums, as in Put)
         const bool want32 = gpu_checksums_ && gpu_value_checksums_ && target.WantsValueChecksum();
-        // the flush's codec call (the task's first step; RSMI_BATCH_CODEC_INLINE: here)
+        // the flush's codec call: here or as the task's first step (RSMI_BATCH_CODEC_PLACE)
         auto r16 = std::make_shared<std::vector<uint32_t>>(gpu_checksums_ ? nb * size_t(n) : 0);
         auto r32 = std::make_shared<std::vector<uint32_t>>(want32 ? nb * size_t(n) : 0);
         auto po = std::make_shared<MemberOrder>(std::move(ord));
@@ -1257,13 +1272,15 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
             phase_add(Phase::Codec, t1);
             return rc;
         };
-        const bool inline_codec = RSMI_BATCH_CODEC_INLINE;
+        const bool inline_codec = RSMI_BATCH_CODEC_PLACE == 1 ||
+                                  (RSMI_BATCH_CODEC_PLACE == 0 && last_writes->load() > last_stage);
         const int pre = inline_codec ? code() : RSMI_OK;
         // the previous flush's task (its codec call and writes) ends before this one starts
         const Status w = join_writes();
         if (!w.ok()) return w;
         writing = std::async(std::launch::async, [this, &target, flat, S, n, to, want32, meta = encode_meta(size), po,
-                                                  code, pre, inline_codec, r16, r32, wkeys = std::move(wkeys)] {
+                                                  code, pre, inline_codec, r16, r32, last_writes,
+                                                  wkeys = std::move(wkeys)] {
             const size_t nw = wkeys.size();
             const int rc = inline_codec ? pre : code();
             const MemberOrder& ord = *po;
@@ -1287,6 +1304,7 @@ Status DagNode::RepairDataNodeBatched(int from, int to, size_t batch, size_t* re
                              : target.PutWithChecksum(wkeys[j], meta, shard, c16);
             });
             phase_add(Phase::Put, t2);
+            last_writes->store(std::chrono::duration_cast<std::chrono::nanoseconds>(PhaseClock::now() - t2).count());
             return ps;
         });
         cur ^= 1;
