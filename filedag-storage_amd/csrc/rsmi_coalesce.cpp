@@ -5,6 +5,8 @@
 
 #include "rsmi_impl.hpp"
 
+#include <cassert>
+
 using namespace rsmi;
 using namespace rsmi::impl;
 
@@ -73,6 +75,9 @@ int done_area(rsmi_ctx* c, hipStream_t st) {
 // Arm a table launch's completion flag (caller holds ctx->mu): the next sequence number, its
 // slot's counter and flag in tb; the host view of the flag is done_flag(c, seq)
 int arm_flag(rsmi_ctx* c, hipStream_t st, BlockBases& tb, uint32_t& seq) {
+    // the flags' slots and counters are ordered by staging[0]'s stream (two launches in flight at
+    // most, alternating slots); a flagged launch on another stream would break that order
+    assert(st == c->staging[0].stream && "completion flag armed on a stream other than staging[0]");
     int rc = done_area(c, st);
     if (rc) return rc;
     if (++c->done_seq == 0) ++c->done_seq;  // 0 is the flags' first value

@@ -2,6 +2,8 @@
 // entry points of include/rsmi.h (see rsmi_impl.hpp for the file map).
 #include "rsmi_impl.hpp"
 
+#include <cassert>
+
 #include <limits>
 
 using namespace rsmi;
@@ -69,8 +71,14 @@ void set_last_kernel(rsmi_ctx* c, const std::string& label) {
 }
 
 CrcScratch& crc_scratch(rsmi_ctx* c, hipStream_t st) {
-    for (const Staging& s : c->staging)
-        if (s.stream == st) return c->own_scratch;
+    // own streams: only staging[0] launches fused or flagged kernels, so a pipelined coalesced
+    // batch still in flight there (ctx->mu released) and the next launch share own_scratch in
+    // stream order (rsmi_impl.hpp CrcScratch)
+    for (size_t i = 0; i < c->staging.size(); i++)
+        if (c->staging[i].stream == st) {
+            assert(i == 0 && "fused CRC scratch used on a staging stream other than staging[0]");
+            return c->own_scratch;
+        }
     auto it = c->stream_scratch.find(st);
     if (it != c->stream_scratch.end()) return it->second;
     // a caller that cycles through many streams: past 32 of them the device is drained once and

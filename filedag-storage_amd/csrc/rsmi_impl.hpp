@@ -76,10 +76,14 @@ struct CrcFuse {
 }  // namespace rsmi
 
 // Device scratch of the fused encode + CRC-16 (records of the tiles or units, and the inline
-// combine's per-block unit counters), one per stream its launches go to: the context's own
-// streams share one (host calls hold the context lock through their synchronisation), and every
-// caller stream of the device-resident calls gets its own, so concurrent calls on different
-// streams never share records or counters.
+// combine's per-block unit counters), one per stream its launches go to, so concurrent calls on
+// different streams never share records or counters.  Every caller stream of the
+// device-resident calls gets its own.  The context's own streams share one, and only staging[0]
+// ever launches a fused (or flagged) kernel (asserted in crc_scratch and arm_flag): host calls
+// hold the context lock through their synchronisation, and a pipelined coalesced batch that is
+// still in flight after the lock is released (rsmi_coalesce.cpp) is ordered before the next
+// launch by staging[0]'s stream order.  The same holds for the page-locked R(shard)
+// areas (raw_area, pipe_area): written by staging[0]'s kernels only.
 struct CrcScratch {
     uint8_t* d_chunks = nullptr;  // tile records and tails (CrcFuse) or unit records
     size_t chunks_cap = 0;
