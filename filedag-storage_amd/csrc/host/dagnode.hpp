@@ -130,7 +130,7 @@ public:
     // With SetGpuChecksums, also compute the mutcask value CRC-32 (cask.go:73-79) on the GPU
     // (a separate rows pass after the encode).  Off by default: the datanode's own
     // carry-less-multiply fold (crc_clmul.hpp, ~30 GiB/s per core, run in the datanode calls'
-    // fan-out) measured faster than the extra GPU pass (DESIGN.md §4a).  Stored values are
+    // fan-out) measured faster than the extra GPU pass (DESIGN.md §4.2).  Stored values are
     // byte-identical either way.
     void SetGpuValueChecksums(bool v) { gpu_value_checksums_ = v; }
     // Get / GetMany read shards with DataNodeClient::GetForVerify and check the stored entry

@@ -82,7 +82,7 @@ __device__ __forceinline__ T* block_rows(const BasesArg<TB>& bases, T* p, uint32
 // stores in flight to page-locked host memory when wave 0 counts.  After the barrier, one
 // system-scope fetch-add counts the workgroup, and the launch's last workgroup resets the counter
 // for the next launch and releases the flag.  A table without a flag (and every table-less
-// instantiation) skips all of it.  ISA check: DESIGN.md §4 (completion flags).
+// instantiation) skips all of it.  ISA check: DESIGN.md §4.3.
 #ifndef RSMI_FLAG_FENCE  // 0: round 5's release (wave 0 only), for the cost A/B (tools/Makefile variant)
 #define RSMI_FLAG_FENCE 1
 #endif
@@ -104,7 +104,7 @@ __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
 
 // K inputs, MT (<= 4) outputs, one 16-byte chunk per lane per row.
 // NT: cache policy, 1 = nontemporal loads and stores (write-heavy tiles), 2 = nontemporal
-// loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.
+// loads, default stores (tiles that read at least 4 rows per row written); DESIGN.md §4.1.
 // WPS: waves per SIMD the register allocation must allow.
 // UA: rows at any byte alignment and pitch (S >= 16).  A lane's 16-byte window starts at
 // min(16*ch, S - 16): the row's last window overlaps the one before it instead of running
@@ -122,7 +122,7 @@ __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
 // not on the 16-byte grid, so its chunk stays out of the quad sums and its value (relative to S)
 // goes to tail[block * (K + MT) + r].  rs_crc16_combine_kernel turns records and tails into
 // R(row).
-// Launch geometry: one tile per wave (DESIGN.md §4); the loop strides over further tiles only
+// Launch geometry: one tile per wave (DESIGN.md §4.1); the loop strides over further tiles only
 // when the caller caps the grid (option waves_per_cu).
 // TB: the blocks lie where a table of block bases says (BlockBases: a coalesced group of callers'
 // own page-locked buffers, one launch for the group); in / out are offsets from each base.
@@ -488,7 +488,7 @@ __device__ __forceinline__ void crc16_combine_rows(const uint16_t* sQ, const uin
 // computes x >> 3 for its GF tables anyway), A = the weights of the tile's position in its unit
 // (crc16.hpp FW, LDS, loaded once per tile and shared by every row).  Per row and tile: 4
 // bitwise ops per dword and 4 MFMAs, against 15 VALU and 8 LDS lookups per dword for the nibble
-// fold (DESIGN.md §4a).
+// fold (DESIGN.md §4.2).
 //
 // A unit is kFusedUnitTiles = 4 consecutive tiles of one block, coded by the 4 waves of one
 // workgroup (one tile each, RSMI_FUSED_COOP) or by one wave, and the counts of a row accumulate
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fused_mfma_kernel(const RsPlanDev
     const uint8_t* ib = block_rows<TB>(bases, in, blk, in_bs);
     uint8_t* ob = block_rows<TB>(bases, out, blk, out_bs);
 #else  // diagnostic build (tools/Makefile diag-cached): the rows of the first 16 blocks only, so
-       // the launch time is the kernel's own issue time (DESIGN.md §4a)
+       // the launch time is the kernel's own issue time (DESIGN.md §4.2)
     const uint8_t* ib = in + uint64_t(blk & 15) * in_bs;
     uint8_t* ob = out + uint64_t(blk & 15) * out_bs;
 #endif
@@ -1015,7 +1015,7 @@ void* repitch_kernel() { return reinterpret_cast<void*>(&rs_repitch_kernel); }
 // value, relative to the item's end, in lane 63; shifting it by (S - item end) mod 32767 bytes
 // places it relative to the row's end, and one atomic XOR adds it into the row's word.  The
 // scan and the shift cost about as much as 8 tiles of folding, so items span 32 tiles
-// (DESIGN.md §4a: 8-tile items spent 30 % of the pass there).  Powers use nibble-sliced tables
+// (DESIGN.md §4.2: 8-tile items spent 30 % of the pass there).  Powers use nibble-sliced tables
 // (P4, conflict-free, 1.9 KiB), so a workgroup stages 12 KiB of LDS.  Bytes at or past S read
 // as zero (zero bytes contribute nothing to R, they only move the reference point, which the
 // final shift accounts for).
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kWG) void rs_crc16_rows_pipe_kernel(const uint32_t*
     }
 }
 
-// The rows pass with the fold on the matrix cores (DESIGN.md §4a), aligned rows.  R(chunk) is
+// The rows pass with the fold on the matrix cores (DESIGN.md §4.2), aligned rows.  R(chunk) is
 // GF(2)-linear in the chunk's 128 bits, so a tile's fold is a GF(2) matrix product; the fp4
 // MFMA v_mfma_scale_f32_16x16x128_f8f6f4 sums integer products exactly, and bit 0 of each count
 // is the product's bit.  B = the tile's data, one data bit per fp4 nibble (v & 0x11111111,

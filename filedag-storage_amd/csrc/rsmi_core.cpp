@@ -268,7 +268,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
             // which balances the launch across CUs and XCDs of uneven effective bandwidth.  A
             // persistent grid (occupancy x CUs, each wave striding over ~26 tiles) gives every CU
             // the same share and waits for the slowest: measured 9-28 % slower on every BASELINE
-            // shape (DESIGN.md §4).  waves_per_cu > 0 caps the grid (the loop in the kernels
+            // shape (DESIGN.md §4.1).  waves_per_cu > 0 caps the grid (the loop in the kernels
             // strides over the remaining tiles).
             long wg_cap = std::numeric_limits<long>::max();
             if (c->opt_waves_per_cu > 0) wg_cap = std::max(1L, long(c->num_cu) * c->opt_waves_per_cu / wpg);

@@ -357,7 +357,7 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * staged through a page-locked one by CPU copies; 0 = never), "coalesce_us" / "coalesce_max"
  * (rsmi_encode_block_coalesced), "crc16_fold" (the CRC-16 rows pass on 16-byte-aligned rows:
  * 1 = default, the fold on the matrix cores (fp4 MFMA); 0 = the nibble-table fold; both
- * bit-exact, DESIGN.md §4a), "crc16_fused_fold" (the encode with the CRC-16 fused in, on
+ * bit-exact, DESIGN.md §4.2), "crc16_fused_fold" (the encode with the CRC-16 fused in, on
  * 16-byte-aligned layouts: 1 = default, rs_fused_mfma_kernel folds on the matrix cores; 0 = the
  * nibble-table variants), "crc32_fold" (the mutcask CRC-32 rows pass: 1 = the fold on the
  * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
@@ -374,7 +374,7 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * a page-locked flag the launch's last workgroup releases, which the caller polls instead of
  * synchronising -- blocking in the synchronisation after 200 us; 0 = event / stream
  * synchronisation).  Kernel variants measured slower than the defaults are not
- * built into the library (DESIGN.md §4).  Returns RSMI_ERR_INVALID_ARG for unknown keys or
+ * built into the library (DESIGN.md §4.1).  Returns RSMI_ERR_INVALID_ARG for unknown keys or
  * values. */
 int rsmi_set_option(rsmi_ctx* ctx, const char* key, long value);
 /* Name of the kernel the last device launch on this context used ("" if none); a copy owned by

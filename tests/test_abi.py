@@ -149,7 +149,7 @@ def test_null_arguments():
     assert L.rsmi_encode_matrix(None, None) == rsmi.ErrInvalidArg
     with rsmi.Codec(2, 1) as c:
         assert L.rsmi_set_option(c._h, b"no_such_knob", 1) == rsmi.ErrInvalidArg
-        # kernel variants measured slower than the defaults are not in the library (DESIGN.md §4)
+        # kernel variants measured slower than the defaults are not in the library (DESIGN.md §4.1)
         for gone in (b"chunks_per_lane", b"nontemporal", b"prefetch", b"tables", b"lds_dma", b"store_aux",
                      b"buffer_stores", b"xcd_order", b"crc_fold", b"crc32_pipe"):
             assert L.rsmi_set_option(c._h, gone, 1) == rsmi.ErrInvalidArg, gone

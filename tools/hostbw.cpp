@@ -1,5 +1,5 @@
 // hostbw.cpp -- diagnostic: host DRAM bandwidth with T threads (read, write, copy), the ceiling
-// under a device group's copy-inclusive batches (DESIGN.md §6): an encode moves k rows of every
+// under a device group's copy-inclusive batches (DESIGN.md §7): an encode moves k rows of every
 // block host -> device and m rows back, so host memory sees (k + m) / k bytes per payload byte
 // whichever GPU the block goes to.  Usage: hostbw [threads = 16] [MiB per thread = 512]
 #include <algorithm>

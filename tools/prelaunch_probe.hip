@@ -1,7 +1,7 @@
 // prelaunch_probe.hip -- diagnostic (not part of the product): can a per-block host call hide its
 // launch behind the host's staging copy?  A per-block DagNode call copies its rows into
 // page-locked memory, then launches one zero-copy kernel and synchronises (~15-20 us of launch and
-// wait, DESIGN.md §5).  Form B queues the kernel first behind a stream wait on a page-locked flag
+// wait, DESIGN.md §8).  Form B queues the kernel first behind a stream wait on a page-locked flag
 // (hipStreamWaitValue32), copies, then releases the flag; form A is the product's order.  The
 // kernel XORs the k = 10 data rows of 26 215 B into one output row over PCIe (a 1-row reconstruct
 // of a 256 KiB RS(10,4) block).  Every iteration's flag value is new and is always written, so no

@@ -36,7 +36,7 @@ def timeit(f, reps=20):
 def main():
     st = torch.cuda.current_stream().cuda_stream
     x = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
-    for _ in range(200):  # past the start-up clock transient
+    for _ in range(200):  # past the start-up clock transient (profiles/r01/README.md)
         x.add_(1)
     torch.cuda.synchronize()
     del x
