@@ -5,6 +5,8 @@
 
 #include "rsmi_impl.hpp"
 
+#include <thread>
+
 #include <cassert>
 
 using namespace rsmi;
@@ -99,13 +101,23 @@ const uint32_t* done_flag(const rsmi_ctx* c, uint32_t seq) { return c->h_done + 
 bool flag_reached(const uint32_t* flag, uint32_t seq) {
     return int32_t(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - seq) >= 0;
 }
+#ifndef RSMI_FLAG_SPIN_US  // pure spinning for this long, then polls that yield the core (A/B builds)
+#define RSMI_FLAG_SPIN_US 200
+#endif
 int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st, hipEvent_t ev) {
     using clk = std::chrono::steady_clock;
-    const auto until = clk::now() + std::chrono::microseconds(200);
+    const auto t0 = clk::now();
+    const auto until = t0 + std::chrono::microseconds(200), spin = t0 + std::chrono::microseconds(RSMI_FLAG_SPIN_US);
+    bool yielding = false;
     for (uint32_t i = 0;; i++) {
         if (flag_reached(flag, seq)) return RSMI_OK;
-        if ((i & 63u) == 63u && clk::now() > until) break;
-        __builtin_ia32_pause();
+        if ((i & 63u) == 63u || yielding) {
+            const auto now = clk::now();
+            if (now > until) break;
+            yielding = now > spin;
+        }
+        if (yielding) std::this_thread::yield();
+        else __builtin_ia32_pause();
     }
     const hipError_t e = ev ? hipEventSynchronize(ev) : hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_status(e);
