@@ -335,6 +335,13 @@ rsmi_ctx* lane_context(rsmi_ctx* c, int lane, int* rc) {
     if (c->lanes.size() < size_t(lane)) c->lanes.resize(size_t(lane), nullptr);
     rsmi_ctx*& l = c->lanes[size_t(lane - 1)];
     if (l) return l;
+    // test hook (option "inject_lane_fault"): this lane's open fails as a device error would,
+    // leaving its slot null
+    for (int v = c->opt_inject_lane_fault.load(); v > 0;)
+        if (c->opt_inject_lane_fault.compare_exchange_weak(v, v - 1)) {
+            *rc = RSMI_ERR_DEVICE;
+            return nullptr;
+        }
     rsmi_ctx* x = nullptr;
     if ((*rc = rsmi_open(c->k, c->m, c->device, &x))) return nullptr;
     {

@@ -478,7 +478,7 @@ int rsmi_set_option(rsmi_ctx* c, const char* key, long value) try {
     // the coalescer's lane contexts code with the same options (the test hook stays with the
     // context whose batches it fails).  A lane whose open failed (or that opened out of order)
     // leaves a null slot (lane_context): skip it.
-    if (std::strcmp(key, "inject_host_fault") != 0) {
+    if (std::strcmp(key, "inject_host_fault") != 0 && std::strcmp(key, "inject_lane_fault") != 0) {
         std::lock_guard<std::mutex> g(c->lanes_mu);
         for (rsmi_ctx* l : c->lanes) {
             if (!l) continue;
@@ -524,6 +524,9 @@ int apply_option(rsmi_ctx* c, const char* key, long value) {
     } else if (!std::strcmp(key, "inject_host_fault")) {
         if (value < 0 || value > 1000) return RSMI_ERR_INVALID_ARG;
         c->opt_inject_host_fault.store(int(value));
+    } else if (!std::strcmp(key, "inject_lane_fault")) {
+        if (value < 0 || value > 1000) return RSMI_ERR_INVALID_ARG;
+        c->opt_inject_lane_fault.store(int(value));
     } else if (!std::strcmp(key, "coalesce_lanes")) {
         if (value < 1 || value > 16) return RSMI_ERR_INVALID_ARG;
         c->opt_coalesce_lanes = value;

@@ -362,8 +362,10 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * nibble-table variants), "crc32_fold" (the mutcask CRC-32 rows pass: 1 = the fold on the
  * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
  * next N coalesced batches throw std::bad_alloc in the executor, so their requests return
- * RSMI_ERR_HOST; default 0), "coalesce_lanes" (coalesced batches coded at once, 1-16, default
- * 2; every option but the test hook also applies to the lanes' child contexts), "coalesce_carry"
+ * RSMI_ERR_HOST; default 0), "inject_lane_fault" (test hook: the next N coalescing lane contexts
+ * fail to open, as a device error would; default 0), "coalesce_lanes" (coalesced batches coded at
+ * once, 1-16, default 2; every option but the test hooks also applies to the lanes' child
+ * contexts), "coalesce_carry"
  * (batches a lane's executor goes on to when they are queued by the time its own completes,
  * before it hands the lane to a waiting caller, 0-16, default 1), "coalesce_pipeline" (1 =
  * default: a coalesced batch coded by the table kernels is left in flight behind an event while

@@ -672,6 +672,27 @@ def test_coalesced_host_fault_reports_err_host():
 
 
 @pytest.mark.gpu
+def test_set_option_after_failed_lane_open():
+    """A coalescing lane whose context fails to open (option "inject_lane_fault") leaves a null
+    lane slot; rsmi_set_option must skip it rather than lock through it, and the
+    context keeps coding: the lane opens on the next warm-up, every option reaches it, and the
+    coalesced encode still equals the plain one."""
+    k, m = 4, 2
+    block = bytes(range(256)) * 64
+    with rsmi.Codec(k, m) as c:
+        c.set_option("coalesce_lanes", 3)
+        c.set_option("inject_lane_fault", 1)
+        with pytest.raises(rsmi.RsmiError) as e:
+            c.warm()  # lane 0 is the context itself; lane 1's open fails, so warm stops there
+        assert e.value.code == rsmi.ErrDevice
+        for key, value in (("waves_per_cu", 0), ("crc16_fold", 1), ("coalesce_flag", 1)):
+            c.set_option(key, value)
+        c.warm()  # lane 1 opens now, then lane 2
+        c.set_option("waves_per_cu", 0)
+        assert c.encode_block_coalesced(block) == c.encode_block(block)
+
+
+@pytest.mark.gpu
 def test_coalesced_reconstruct_concurrent_callers():
     """rsmi_reconstruct_coalesced from 16 threads (concurrent degraded DagNode.Gets): two
     erasure patterns, both data_only modes and two shard sizes in flight together; every
