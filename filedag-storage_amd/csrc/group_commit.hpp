@@ -40,6 +40,10 @@
 #include <type_traits>
 #include <vector>
 
+#ifndef RSMI_GC_SPIN_US
+#define RSMI_GC_SPIN_US 0
+#endif
+
 namespace rsmi {
 
 template <class Req>
@@ -169,21 +173,37 @@ private:
         bool queued = false;  // in pending_ (under mu_)
         std::mutex m;
         std::condition_variable cv;
-        bool woken = false;  // under m
+        bool woken = false;            // under m
+        std::atomic<bool> ready{false};  // woken, readable without m (the spin before the sleep)
     };
     // wake a waiting caller (caller holds mu_: lock order mu_, then the waiter's m)
     static void wake(Waiter& w) {
         {
             std::lock_guard<std::mutex> g(w.m);
             w.woken = true;
+            w.ready.store(true, std::memory_order_release);
         }
         w.cv.notify_one();
     }
-    // sleep until woken; mu_ is released meanwhile and held again on return
+    // sleep until woken; mu_ is released meanwhile and held again on return.  With
+    // RSMI_GC_SPIN_US > 0 the caller first spins that long on the waiter's flag, so a batch that
+    // completes within it costs no futex wake-up (A/B builds; default 0: sleep at once)
     static void sleep(Waiter& w, std::unique_lock<std::mutex>& lk) {
         std::unique_lock<std::mutex> g(w.m);
         w.woken = false;  // under mu_ and m: no wake-up can fall between the caller's check and here
+        w.ready.store(false, std::memory_order_relaxed);
         lk.unlock();
+        if (RSMI_GC_SPIN_US > 0) {
+            g.unlock();
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(RSMI_GC_SPIN_US);
+            for (uint32_t i = 0; !w.ready.load(std::memory_order_acquire); i++) {
+                if ((i & 63u) == 63u && std::chrono::steady_clock::now() > until) break;
+#if defined(__x86_64__)
+                __builtin_ia32_pause();
+#endif
+            }
+            g.lock();
+        }
         w.cv.wait(g, [&] { return w.woken; });
         g.unlock();
         lk.lock();
