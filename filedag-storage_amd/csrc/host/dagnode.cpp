@@ -20,6 +20,11 @@
 // with the shorter of the two: 0 = chosen per chunk from the previous chunk's measured staging and
 // write times (default), 1 = always on the calling thread (round 5), 2 = always in the task (A/B
 // library builds, profiles/r06/b/).
+// 1 (default): a Put writes its block-only data shards while the GPU encodes the parity; 0: every
+// write after the codec call (round 5's order), for same-box A/B library builds
+#ifndef RSMI_PUT_OVERLAP
+#define RSMI_PUT_OVERLAP 1
+#endif
 #ifndef RSMI_BATCH_CODEC_PLACE
 #define RSMI_BATCH_CODEC_PLACE 0
 #endif
@@ -361,42 +366,58 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     Erasure enc;
     Status s = member_erasure(member, int64_t(block.size()), &enc);
     if (!s.ok()) return s;
-    const int n = int(nodes_.size());
+    const int n = int(nodes_.size()), k = config_.data_blocks;
     const size_t S = size_t(enc.ShardSize());
-    bool want32 = false;  // mutcask-backed datanodes keep a CRC-32 of every value as well
-    for (auto& sn : nodes_) want32 |= gpu_checksums_ && gpu_value_checksums_ && sn.client->WantsValueChecksum();
-    // Split + Encode into one page-locked buffer (coded there in place on the GPU), and each
-    // datanode gets its shard as a view of it, as the Go slices alias Split's buffer
-    const auto t0 = PhaseClock::now();
-    uint8_t* flat = block.empty() ? nullptr : block_scratch(size_t(n) * S);
-    if (!block.empty() && !flat) return Status::Error("out of host memory");
-    std::vector<uint32_t> raw(gpu_checksums_ && !block.empty() ? size_t(n) : 0), raw32(want32 ? size_t(n) : 0);
-    if (!block.empty() && lone_paths_ && active_.load() <= 1) {
-        // a lone caller (nothing to coalesce with): Split into the page-locked buffer here, the
-        // copy spread over the idle fan-out pool, then one zero-copy kernel codes it in place
-        const size_t k = size_t(config_.data_blocks);
-        copy_bytes(flat, block.data(), block.size());
-        std::memset(flat + block.size(), 0, k * S - block.size());  // Split zero-padding
-        int rc;
-        rsmi_ctx* ctx = member_ctx(member, &rc);
-        if (!ctx) return rsmi_status(rc);
-        rc = raw.empty() ? rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1)
-                         : rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + k * S, size_t(n) * S, S, 1,
-                                                       raw.data(), raw32.empty() ? nullptr : raw32.data());
-        if (rc) return rsmi_status(rc);
-    } else {
-        s = enc.EncodeDataFlat(block, flat, raw.empty() ? nullptr : raw.data(), raw32.empty() ? nullptr : raw32.data());
-        if (!s.ok()) return s;
-    }
-    phase_add(Phase::Codec, t0);
-    const auto t1 = PhaseClock::now();
     const int wq = EntryQuorum().second;
     std::vector<Status> res(nodes_.size());
     last_shard_ = S;
-    fan(n, [&](int i) {  // one goroutine per datanode, no cancel
+    auto quorum = [&] {
+        QuorumWait w(wq, n - wq + 1);
+        for (const Status& r : res) w.add(r);
+        return w.result("Write failed. Insufficient number of nodes online");
+    };
+    if (block.empty()) {  // erasure.go:52-54: nil shards, no codec call
+        fan(n, [&](int i) { res[i] = nodes_[i].client->Put(key, meta, ByteView(nullptr, 0)); }, 0);
+        return quorum();
+    }
+    bool want32 = false;  // mutcask-backed datanodes keep a CRC-32 of every value as well
+    for (auto& sn : nodes_) want32 |= gpu_checksums_ && gpu_value_checksums_ && sn.client->WantsValueChecksum();
+    // Split into one page-locked buffer (coded there in place on the GPU), and each datanode gets
+    // its shard as a view of it, as the Go slices alias Split's buffer
+    uint8_t* flat = block_scratch(size_t(n) * S);
+    if (!flat) return Status::Error("out of host memory");
+    std::vector<uint32_t> raw(gpu_checksums_ ? size_t(n) : 0), raw32(want32 ? size_t(n) : 0);
+    // a lone caller (nothing to coalesce with) spreads the copy over the idle fan-out pool and
+    // codes the block with one zero-copy kernel; concurrent callers Split on their own thread and
+    // meet in the engine's group commit
+    const bool lone = lone_paths_ && active_.load() <= 1;
+    if (lone) copy_bytes(flat, block.data(), block.size());
+    else copy_to_staging(flat, block.data(), block.size());
+    std::memset(flat + block.size(), 0, size_t(k) * S - block.size());  // Split zero-padding
+    int rc = RSMI_OK;
+    auto codec = [&] {
+        const auto tc = PhaseClock::now();
+        if (lone) {
+            rsmi_ctx* ctx = member_ctx(member, &rc);
+            if (ctx)
+                rc = raw.empty() ? rsmi_encode_batch_host(ctx, flat, size_t(n) * S, flat + size_t(k) * S, size_t(n) * S, S, 1)
+                                 : rsmi_encode_batch_host_crcs(ctx, flat, size_t(n) * S, flat + size_t(k) * S,
+                                                               size_t(n) * S, S, 1, raw.data(),
+                                                               raw32.empty() ? nullptr : raw32.data());
+        } else {
+            const Status e = enc.EncodeSplitFlat(block.size(), flat, raw.empty() ? nullptr : raw.data(),
+                                                 raw32.empty() ? nullptr : raw32.data());
+            rc = e.ok() ? RSMI_OK : RSMI_ERR_DEVICE;
+            if (!e.ok()) s = e;
+        }
+        phase_add(Phase::Codec, tc);
+    };
+    // shard i to datanode i; with its entry checksum (and value checksum) from the GPU pass, or
+    // the datanode computes them (sum = false)
+    auto put_shard = [&](int i, bool sum) {
         DataNodeClient& cl = *nodes_[i].client;
-        const ByteView shard(flat ? flat + size_t(i) * S : nullptr, block.empty() ? 0 : S);  // empty block: nil shards
-        if (raw.empty()) {
+        const ByteView shard(flat + size_t(i) * S, S);
+        if (!sum || raw.empty()) {
             res[i] = cl.Put(key, meta, shard);
             return;
         }
@@ -404,11 +425,38 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
         res[i] = !raw32.empty() && cl.WantsValueChecksum()
                      ? cl.PutWithChecksums(key, meta, shard, c16, value_checksum(meta, S, c16, raw32[i]))
                      : cl.PutWithChecksum(key, meta, shard, c16);
-    }, S);
+    };
+    // The data rows that hold only block bytes are final once Split, so their datanode writes run
+    // while the GPU encodes the parity (the datanodes checksum them; RSMI_PUT_OVERLAP 0: after the
+    // codec call, with the GPU's checksums).  The rest -- the row holding the zero padding, which
+    // the engine's group commit rewrites, and the parity rows -- follow the codec call.  Stored
+    // entries are the same either way; every outcome is replayed in node order.
+    const int early = RSMI_PUT_OVERLAP ? int(std::min<size_t>(size_t(k), block.size() / S)) : 0;
+    if (early > 0 && fan_) {
+        fan_->run(2, [&](int t) {
+            if (t == 0) {
+                codec();
+                return;
+            }
+            const auto tp = PhaseClock::now();
+            fan(early, [&](int i) { put_shard(i, false); }, S);
+            phase_add(Phase::Put, tp);
+        });
+    } else {
+        codec();
+    }
+    if (rc) {
+        // the codec failed: a shard already written is taken back (best effort), so the block is
+        // not left readable from its data shards alone, as a failed encode writes nothing
+        // (node.go:382-386)
+        for (int i = 0; i < early; i++)
+            if (res[i].ok()) (void)nodes_[i].client->Delete(key);
+        return s.ok() ? rsmi_status(rc) : s;
+    }
+    const auto t1 = PhaseClock::now();
+    fan(n - early, [&](int t) { put_shard(early + t, true); }, S);  // one goroutine per datanode, no cancel
     phase_add(Phase::Put, t1);
-    QuorumWait w(wq, int(nodes_.size()) - wq + 1);
-    for (const Status& r : res) w.add(r);
-    return w.result("Write failed. Insufficient number of nodes online");
+    return quorum();
 }
 
 Status DagNode::PutMany(const std::vector<std::string>& keys, const std::vector<Bytes>& blocks) {

@@ -239,6 +239,16 @@ Status Erasure::EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, 
     return rsmi_status(rc);
 }
 
+Status Erasure::EncodeSplitFlat(size_t B, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const {
+    if (B == 0) return Status::Ok();  // erasure.go:52-54
+    int rc;
+    rsmi_ctx* c = call_context(data_blocks_, parity_blocks_, device_, &rc, replica_);
+    if (!c) return rsmi_status(rc);
+    rc = raw ? rsmi_encode_block_coalesced_crcs(c, flat, B, flat, raw, raw32)
+             : rsmi_encode_block_coalesced(c, flat, B, flat, nullptr);
+    return rsmi_status(rc);
+}
+
 Status Erasure::EncodeDataWithCrcs(const Bytes& data, std::vector<Bytes>* shards, std::vector<uint32_t>* raw,
                                    std::vector<uint32_t>* raw32) const {
     const int n = data_blocks_ + parity_blocks_;

@@ -108,6 +108,8 @@ public:
     // flat should be page-locked (block_scratch): the block is Split into it on the calling
     // thread, and the call (alone or in a coalesced group) codes it in place.
     Status EncodeDataFlat(const Bytes& data, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const;
+    // EncodeDataFlat of a block of B bytes the caller has already copied to the start of flat
+    Status EncodeSplitFlat(size_t B, uint8_t* flat, uint32_t* raw, uint32_t* raw32) const;
     Status DecodeDataBlocks(std::vector<Bytes>& shards) const;
     Status DecodeDataAndParityBlocks(std::vector<Bytes>& shards) const;
     int64_t ShardSize() const { return ceil_frac(block_size_, data_blocks_); }

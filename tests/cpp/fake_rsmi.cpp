@@ -16,9 +16,11 @@
 // host cores, erasure.go:37) -- and tools/bench_dagnode can time it beside the GPU build.
 // Batches split their blocks over FAKE_RSMI_THREADS (default OMP_NUM_THREADS, else every core)
 // threads; a single block codes on the calling thread.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -95,6 +97,7 @@ int par_blocks(size_t nblocks, F f) {
 struct rsmi_ctx {
     int k = 0, m = 0, n = 0;
     rsmi::GroupCommit<Req> coal{RSMI_ERR_HOST};
+    std::atomic<int> inject_host_fault{0};  // option "inject_host_fault", as the product's
 };
 
 namespace {
@@ -145,6 +148,9 @@ int reconstruct_one(rsmi_ctx* c, uint8_t* p, size_t S, const uint8_t* present, c
 }
 
 void run_batch(rsmi_ctx* c, std::vector<Req*>& batch) {
+    // test hook (option "inject_host_fault"): this batch fails as a host allocation would
+    for (int v = c->inject_host_fault.load(); v > 0;)
+        if (c->inject_host_fault.compare_exchange_weak(v, v - 1)) throw std::bad_alloc();
     for (Req* r : batch) {
         if (r->encode) {
             const size_t S = r->S, k = size_t(c->k), n = size_t(c->n);
@@ -296,6 +302,12 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     Req req{false, nullptr, 0, shards, S, present, data_only, nullptr, nullptr, RSMI_OK, false};
     c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); });
     return req.rc;
+}
+
+int rsmi_set_option(rsmi_ctx* c, const char* key, long value) {
+    if (!c || !key) return RSMI_ERR_INVALID_ARG;
+    if (!std::strcmp(key, "inject_host_fault")) c->inject_host_fault.store(int(value));
+    return RSMI_OK;  // the coding options have no meaning on the CPU codec
 }
 
 long rsmi_get_stat(const rsmi_ctx* c, const char* key) {

@@ -804,6 +804,35 @@ static void test_concurrent_puts() {
     }
 }
 
+// A Put whose codec call fails writes nothing that outlives it (node.go:382-386 returns before any
+// datanode write): the data shards written while the GPU encoded are taken back.  The failure is
+// the coalescer's host-fault test hook (RSMI_ERR_HOST); the next Put succeeds.
+static void test_put_codec_failure() {
+    const int k = 10, m = 4, n = k + m;
+    Cluster c(k, m);
+    c.node->SetLoneCallerPaths(false);  // through the group commit, where the hook fails a batch
+    int rc;
+    rsmi_ctx* ctx = shared_context(k, m, c.node->MemberDevice(0), &rc, c.node->MemberReplica(0));
+    CHECK(ctx != nullptr);
+    std::mt19937_64 r(404);
+    const Bytes block = rand_bytes(r, big());
+    for (int i = 0; i < c.node->Members(); i++) {
+        rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
+        CHECK(x && rsmi_set_option(x, "inject_host_fault", 1) == RSMI_OK);
+    }
+    Status s = c.node->Put("codec-fails", block);
+    CHECK(!s.ok());
+    for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], "codec-fails").empty());
+    for (int i = 0; i < c.node->Members(); i++) {  // a member the key did not reach keeps its fault armed
+        rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
+        if (x) (void)rsmi_set_option(x, "inject_host_fault", 0);
+    }
+    CHECK_OK(c.node->Put("codec-fails", block));
+    const auto want = oracle_shards(k, m, block);
+    for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], "codec-fails") == want[j]);
+    c.node->SetLoneCallerPaths(true);
+}
+
 // A Dag Node on a device list (DagNode::New): every per-key call codes on the member that owns the
 // key's hash slot (hash_slot.go:20-22, crc16 IBM of the key & 0x3FFF, in contiguous ranges of
 // 16384 / members slots), and each member's group-commit queue sees exactly its own keys.  The two
@@ -1060,6 +1089,7 @@ int main(int argc, char** argv) {
         test_gpu_value_checksums();
         test_gpu_verified_reads();
         test_concurrent_puts();
+        test_put_codec_failure();
         test_member_routing();
         // the member pass: the Dag Node tests again on a two-member device list, every shard
         // and block still the oracle's
@@ -1077,6 +1107,7 @@ int main(int argc, char** argv) {
         test_gpu_entry_checksums();
         test_gpu_verified_reads();
         test_concurrent_puts();
+        test_put_codec_failure();
         g_devices = {0};
         std::printf("member pass: %d checks\n", g_checks - before);
     }
