@@ -869,10 +869,12 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
         std::vector<Status> st;
     };
     auto fetch_chunk = [this, &keys](size_t c0, size_t cn) {
+        const auto t0 = PhaseClock::now();
         Chunk c;
         c.fs.resize(cn);
         c.st.resize(cn);
         fan_keys(int(cn), [&](int q) { c.st[size_t(q)] = fetch_for_get(keys[c0 + size_t(q)], &c.fs[size_t(q)], true); });
+        phase_add(Phase::Fetch, t0);
         return c;
     };
     // the first chunk on this thread (a one-key GetMany is Get: no helper thread), later ones
@@ -965,6 +967,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     for (size_t j = 0; j < nb; j++) tmp[j] = g.second[b0 + ord.perm[j]];
                     std::copy(tmp.begin(), tmp.end(), g.second.begin() + long(b0));
                 }
+                const auto ts = PhaseClock::now();
                 uint8_t* flat = thread_staging().reserve(nb * size_t(n) * S);  // missing rows: don't-care bytes
                 if (!flat) {
                     unchecked(g.second, b0, nb);
@@ -974,6 +977,8 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     for (int c = 0; c < n; c++)
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
+                phase_add(Phase::Stage, ts);
+                const auto tc = PhaseClock::now();
                 // with verified reads the same kernel returns R of every survivor it read
                 const int drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
                     uint8_t* f = flat + j0 * size_t(n) * S;
@@ -981,6 +986,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                                                                        r16.data() + j0 * size_t(k))
                                   : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
                 });
+                phase_add(Phase::Codec, tc);
                 if (drc != RSMI_OK) {  // finish_get reports a device error per key
                     unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
@@ -998,6 +1004,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                 // each block straight from the staging (its k data rows are the Split buffer: the
                 // first BlockSize bytes, node.go:311-319), without copying the rebuilt rows into
                 // the key's shards first; a key to be fetched again keeps nothing from here
+                const auto ta = PhaseClock::now();
                 fan_keys(int(nb), [&](int j) {
                     const size_t q = g.second[b0 + j];
                     if (redo_after[q]) return;
@@ -1005,6 +1012,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
                     fs[q].assembled = true;
                 });
+                phase_add(Phase::Stage, ta);  // the assembly copies count as staging
             }
         }
         // a bad survivor: that key's fetch again, checked wave by wave (quorum, repair list and

@@ -212,8 +212,12 @@ int main(int argc, char** argv) {
     double getbv = 1e30;
     for (int rep = 0; rep < 3; rep++) {
         d->SetGpuVerifiedReads(false);
+        d->SetPhaseTiming(rep == 0);
+        d->ResetPhases();
         t0 = clk::now();
         d->GetMany(keys, &gm, &st, best_batch);
+        if (rep == 0) phase_json("getmany", secs(t0));
+        d->SetPhaseTiming(false);
         getb = std::min(getb, secs(t0));
         d->SetGpuVerifiedReads(true);
         t0 = clk::now();

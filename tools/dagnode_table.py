@@ -24,7 +24,7 @@ def phases(path):
         print(f"\nRS({k},{m}) {B // 1024} KiB: per-phase host time, ms, median of runs (summed over threads)")
         print("| leg | codec | wall | fetch | stage | codec call | datanode puts |")
         print("|---|---|---|---|---|---|---|")
-        for leg in ("put", "putmany", "put_threads", "get", "get_threads", "repair_batched"):
+        for leg in ("put", "putmany", "put_threads", "get", "getmany", "get_threads", "repair_batched"):
             for codec in ("gpu", "cpu"):
                 v = [r[leg] for r in rows if r["codec"] == codec and (r["k"], r["m"], r["B"]) == (k, m, B) and leg in r]
                 if not v:
