@@ -25,6 +25,11 @@
 #ifndef RSMI_PUT_OVERLAP
 #define RSMI_PUT_OVERLAP 1
 #endif
+// 1 (default): GetMany copies each block's present data rows into the block while the GPU rebuilds
+// the missing ones (unverified reads); 0: the whole block from the staging after the decode
+#ifndef RSMI_GETMANY_OVERLAP
+#define RSMI_GETMANY_OVERLAP 1
+#endif
 #ifndef RSMI_BATCH_CODEC_PLACE
 #define RSMI_BATCH_CODEC_PLACE 0
 #endif
@@ -978,15 +983,43 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
                 phase_add(Phase::Stage, ts);
-                const auto tc = PhaseClock::now();
                 // with verified reads the same kernel returns R of every survivor it read
-                const int drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
-                    uint8_t* f = flat + j0 * size_t(n) * S;
-                    return verify ? rsmi_reconstruct_batch_host_verify(ctx, f, size_t(n) * S, S, cnt, present.data(), 1,
-                                                                       r16.data() + j0 * size_t(k))
-                                  : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
-                });
-                phase_add(Phase::Codec, tc);
+                int drc = RSMI_OK;
+                auto decode = [&] {
+                    const auto tc = PhaseClock::now();
+                    drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                        uint8_t* f = flat + j0 * size_t(n) * S;
+                        return verify ? rsmi_reconstruct_batch_host_verify(ctx, f, size_t(n) * S, S, cnt, present.data(),
+                                                                           1, r16.data() + j0 * size_t(k))
+                                      : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
+                    });
+                    phase_add(Phase::Codec, tc);
+                };
+                // Without verification, each block's present data rows are final before the decode:
+                // they are copied from the fetched shards into the block while the GPU rebuilds the
+                // missing ones, and only the rebuilt rows are copied out afterwards (RSMI_GETMANY_OVERLAP)
+                const int32_t bsz = g.first.first;
+                auto row_len = [&](int c) { return std::min(S, size_t(bsz) - std::min(size_t(bsz), size_t(c) * S)); };
+                const bool early = RSMI_GETMANY_OVERLAP && !verify && fan_;
+                if (early) {
+                    fan_->run(2, [&](int t) {
+                        if (t == 0) {
+                            decode();
+                            return;
+                        }
+                        const auto ta = PhaseClock::now();
+                        fan_keys(int(nb), [&](int j) {
+                            const size_t q = g.second[b0 + j];
+                            Bytes& blk = (*blocks)[k0 + q];
+                            blk.resize(size_t(bsz));
+                            for (int c = 0; c < k; c++)
+                                if (present[c] && row_len(c)) std::memcpy(blk.data() + size_t(c) * S, fs[q].shards[c].data(), row_len(c));
+                        });
+                        phase_add(Phase::Stage, ta);
+                    });
+                } else {
+                    decode();
+                }
                 if (drc != RSMI_OK) {  // finish_get reports a device error per key
                     unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
@@ -1009,7 +1042,13 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     const size_t q = g.second[b0 + j];
                     if (redo_after[q]) return;
                     const uint8_t* base = flat + size_t(j) * n * S;
-                    (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
+                    if (early) {  // the present rows are in place: the rebuilt ones only
+                        for (int c = 0; c < k; c++)
+                            if (!present[c] && row_len(c))
+                                std::memcpy((*blocks)[k0 + q].data() + size_t(c) * S, base + size_t(c) * S, row_len(c));
+                    } else {
+                        (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
+                    }
                     fs[q].assembled = true;
                 });
                 phase_add(Phase::Stage, ta);  // the assembly copies count as staging
