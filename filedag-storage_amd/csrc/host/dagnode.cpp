@@ -25,10 +25,9 @@
 #ifndef RSMI_PUT_OVERLAP
 #define RSMI_PUT_OVERLAP 1
 #endif
-// 1 (default): GetMany copies each block's present data rows into the block while the GPU rebuilds
-// the missing ones (unverified reads); 0: the whole block from the staging after the decode
-#ifndef RSMI_GETMANY_OVERLAP
-#define RSMI_GETMANY_OVERLAP 1
+// the smallest shard whose data rows a Put writes while the GPU encodes
+#ifndef RSMI_PUT_OVERLAP_MIN_SHARD
+#define RSMI_PUT_OVERLAP_MIN_SHARD 65536
 #endif
 #ifndef RSMI_BATCH_CODEC_PLACE
 #define RSMI_BATCH_CODEC_PLACE 0
@@ -431,12 +430,15 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
                      ? cl.PutWithChecksums(key, meta, shard, c16, value_checksum(meta, S, c16, raw32[i]))
                      : cl.PutWithChecksum(key, meta, shard, c16);
     };
-    // The data rows that hold only block bytes are final once Split, so their datanode writes run
-    // while the GPU encodes the parity (the datanodes checksum them; RSMI_PUT_OVERLAP 0: after the
-    // codec call, with the GPU's checksums).  The rest -- the row holding the zero padding, which
-    // the engine's group commit rewrites, and the parity rows -- follow the codec call.  Stored
-    // entries are the same either way; every outcome is replayed in node order.
-    const int early = RSMI_PUT_OVERLAP ? int(std::min<size_t>(size_t(k), block.size() / S)) : 0;
+    // Large shards: the data rows that hold only block bytes are final once Split, so their
+    // datanode writes run while the GPU encodes the parity (the datanodes checksum them).  The
+    // rest -- the row holding the zero padding, which the engine's group commit rewrites, and the
+    // parity rows -- follow the codec call.  Small shards write every row after the codec call,
+    // with the GPU's checksums: there the second fan-out costs more than the overlap saves
+    // (DESIGN.md §5.3).  Stored entries are the same either way; every outcome is replayed in
+    // node order.
+    const bool overlap = RSMI_PUT_OVERLAP && S >= size_t(RSMI_PUT_OVERLAP_MIN_SHARD);
+    const int early = overlap ? int(std::min<size_t>(size_t(k), block.size() / S)) : 0;
     if (early > 0 && fan_) {
         fan_->run(2, [&](int t) {
             if (t == 0) {
@@ -983,43 +985,15 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
                 phase_add(Phase::Stage, ts);
+                const auto tc = PhaseClock::now();
                 // with verified reads the same kernel returns R of every survivor it read
-                int drc = RSMI_OK;
-                auto decode = [&] {
-                    const auto tc = PhaseClock::now();
-                    drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
-                        uint8_t* f = flat + j0 * size_t(n) * S;
-                        return verify ? rsmi_reconstruct_batch_host_verify(ctx, f, size_t(n) * S, S, cnt, present.data(),
-                                                                           1, r16.data() + j0 * size_t(k))
-                                      : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
-                    });
-                    phase_add(Phase::Codec, tc);
-                };
-                // Without verification, each block's present data rows are final before the decode:
-                // they are copied from the fetched shards into the block while the GPU rebuilds the
-                // missing ones, and only the rebuilt rows are copied out afterwards (RSMI_GETMANY_OVERLAP)
-                const int32_t bsz = g.first.first;
-                auto row_len = [&](int c) { return std::min(S, size_t(bsz) - std::min(size_t(bsz), size_t(c) * S)); };
-                const bool early = RSMI_GETMANY_OVERLAP && !verify && fan_;
-                if (early) {
-                    fan_->run(2, [&](int t) {
-                        if (t == 0) {
-                            decode();
-                            return;
-                        }
-                        const auto ta = PhaseClock::now();
-                        fan_keys(int(nb), [&](int j) {
-                            const size_t q = g.second[b0 + j];
-                            Bytes& blk = (*blocks)[k0 + q];
-                            blk.resize(size_t(bsz));
-                            for (int c = 0; c < k; c++)
-                                if (present[c] && row_len(c)) std::memcpy(blk.data() + size_t(c) * S, fs[q].shards[c].data(), row_len(c));
-                        });
-                        phase_add(Phase::Stage, ta);
-                    });
-                } else {
-                    decode();
-                }
+                const int drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
+                    uint8_t* f = flat + j0 * size_t(n) * S;
+                    return verify ? rsmi_reconstruct_batch_host_verify(ctx, f, size_t(n) * S, S, cnt, present.data(), 1,
+                                                                       r16.data() + j0 * size_t(k))
+                                  : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
+                });
+                phase_add(Phase::Codec, tc);
                 if (drc != RSMI_OK) {  // finish_get reports a device error per key
                     unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
@@ -1042,13 +1016,7 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     const size_t q = g.second[b0 + j];
                     if (redo_after[q]) return;
                     const uint8_t* base = flat + size_t(j) * n * S;
-                    if (early) {  // the present rows are in place: the rebuilt ones only
-                        for (int c = 0; c < k; c++)
-                            if (!present[c] && row_len(c))
-                                std::memcpy((*blocks)[k0 + q].data() + size_t(c) * S, base + size_t(c) * S, row_len(c));
-                    } else {
-                        (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
-                    }
+                    (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
                     fs[q].assembled = true;
                 });
                 phase_add(Phase::Stage, ta);  // the assembly copies count as staging

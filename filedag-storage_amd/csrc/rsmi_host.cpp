@@ -11,6 +11,7 @@
 // time).
 
 #include "rsmi_impl.hpp"
+#include <new>
 
 using namespace rsmi;
 using namespace rsmi::impl;
@@ -568,8 +569,19 @@ int rsmi_reconstruct(rsmi_ctx* c, uint8_t* shards, size_t S, const uint8_t* pres
     return rsmi::impl::exception_status();
 }
 
+namespace {
+// test hook (option "inject_host_fault"): a direct host encode fails as a host allocation would,
+// as the coalesced batches do (rsmi_coalesce.cpp)
+void direct_fault_hook(rsmi_ctx* c) {
+    if (!c) return;
+    for (int v = c->opt_inject_host_fault.load(); v > 0;)
+        if (c->opt_inject_host_fault.compare_exchange_weak(v, v - 1)) throw std::bad_alloc();
+}
+}  // namespace
+
 int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                            size_t parity_block_stride, size_t S, size_t nblocks) try {
+    direct_fault_hook(c);
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, nullptr);
 } catch (...) {
     return rsmi::impl::exception_status();
@@ -578,6 +590,7 @@ int rsmi_encode_batch_host(rsmi_ctx* c, const uint8_t* data, size_t data_block_s
 int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw_out) try {
     if (!raw_out) return RSMI_ERR_INVALID_ARG;
+    direct_fault_hook(c);
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw_out);
 } catch (...) {
     return rsmi::impl::exception_status();
@@ -586,6 +599,7 @@ int rsmi_encode_batch_host_crc(rsmi_ctx* c, const uint8_t* data, size_t data_blo
 int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t data_block_stride, uint8_t* parity,
                                 size_t parity_block_stride, size_t S, size_t nblocks, uint32_t* raw16_out,
                                 uint32_t* raw32_out) try {
+    direct_fault_hook(c);
     return encode_host_impl(c, data, data_block_stride, parity, parity_block_stride, S, nblocks, raw16_out,
                             raw32_out);
 } catch (...) {

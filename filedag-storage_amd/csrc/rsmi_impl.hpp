@@ -183,7 +183,7 @@ struct rsmi_ctx {
     // a batch that throws (std::bad_alloc from the executor's host containers) fails its
     // requests as the boundary reports host-resource exceptions (include/rsmi.h ABI v3)
     rsmi::GroupCommit<CoalReq> coal{RSMI_ERR_HOST};
-    std::atomic<int> opt_inject_host_fault{0};  // test hook: the next coalesced batches throw std::bad_alloc
+    std::atomic<int> opt_inject_host_fault{0};  // test hook: the next coalesced batches or direct host encodes throw std::bad_alloc
     std::atomic<int> opt_inject_lane_fault{0};  // test hook: the next lane contexts fail to open (RSMI_ERR_DEVICE)
     uint8_t* h_coal = nullptr;  // page-locked staging of the executing batch
     size_t h_coal_cap = 0;

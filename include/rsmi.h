@@ -361,8 +361,8 @@ int rsmi_group_reconstruct_rows_batch_host(rsmi_group* group, uint8_t* shards, s
  * 16-byte-aligned layouts: 1 = default, rs_fused_mfma_kernel folds on the matrix cores; 0 = the
  * nibble-table variants), "crc32_fold" (the mutcask CRC-32 rows pass: 1 = the fold on the
  * matrix cores, 0 = the nibble-table fold; both bit-exact), "inject_host_fault" (test hook: the
- * next N coalesced batches throw std::bad_alloc in the executor, so their requests return
- * RSMI_ERR_HOST; default 0), "inject_lane_fault" (test hook: the next N coalescing lane contexts
+ * next N coalesced batches, or direct rsmi_encode_batch_host* calls, throw std::bad_alloc, so their
+ * requests return RSMI_ERR_HOST; default 0), "inject_lane_fault" (test hook: the next N coalescing lane contexts
  * fail to open, as a device error would; default 0), "coalesce_lanes" (coalesced batches coded at
  * once, 1-16, default 2; every option but the test hooks also applies to the lanes' child
  * contexts), "coalesce_carry"

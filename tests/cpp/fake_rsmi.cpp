@@ -197,6 +197,8 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t dbs, ui
                                 size_t nblocks, uint32_t* raw16, uint32_t* raw32) {
     if (!c || !data || !parity) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
+    for (int v = c->inject_host_fault.load(); v > 0;)  // as the product's direct host encodes
+        if (c->inject_host_fault.compare_exchange_weak(v, v - 1)) return RSMI_ERR_HOST;
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     (void)m;
     return par_blocks(nblocks, [&](size_t b0, size_t b1) {

@@ -810,26 +810,31 @@ static void test_concurrent_puts() {
 static void test_put_codec_failure() {
     const int k = 10, m = 4, n = k + m;
     Cluster c(k, m);
-    c.node->SetLoneCallerPaths(false);  // through the group commit, where the hook fails a batch
     int rc;
-    rsmi_ctx* ctx = shared_context(k, m, c.node->MemberDevice(0), &rc, c.node->MemberReplica(0));
-    CHECK(ctx != nullptr);
     std::mt19937_64 r(404);
-    const Bytes block = rand_bytes(r, big());
-    for (int i = 0; i < c.node->Members(); i++) {
-        rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
-        CHECK(x && rsmi_set_option(x, "inject_host_fault", 1) == RSMI_OK);
+    // through the group commit (lone paths off, where the hook fails a batch) and as a lone caller
+    // (the hook fails the direct call); with shards above the overlap threshold the block-only
+    // data shards are written while the GPU encodes, and taken back when the codec call fails
+    for (const int mode : {0, 1, 2}) {
+        const bool lone = mode == 2;
+        c.node->SetLoneCallerPaths(lone);
+        const Bytes block = rand_bytes(r, mode ? size_t(k) * 65536 + 17 : big());
+        const std::string key = "codec-fails-" + std::to_string(mode);
+        for (int i = 0; i < c.node->Members(); i++) {
+            rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
+            CHECK(x && rsmi_set_option(x, "inject_host_fault", 1) == RSMI_OK);
+        }
+        Status s = c.node->Put(key, block);
+        CHECK(!s.ok());
+        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key).empty());
+        for (int i = 0; i < c.node->Members(); i++) {  // a member the key did not reach keeps its fault armed
+            rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
+            if (x) (void)rsmi_set_option(x, "inject_host_fault", 0);
+        }
+        CHECK_OK(c.node->Put(key, block));
+        const auto want = oracle_shards(k, m, block);
+        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key) == want[j]);
     }
-    Status s = c.node->Put("codec-fails", block);
-    CHECK(!s.ok());
-    for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], "codec-fails").empty());
-    for (int i = 0; i < c.node->Members(); i++) {  // a member the key did not reach keeps its fault armed
-        rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
-        if (x) (void)rsmi_set_option(x, "inject_host_fault", 0);
-    }
-    CHECK_OK(c.node->Put("codec-fails", block));
-    const auto want = oracle_shards(k, m, block);
-    for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], "codec-fails") == want[j]);
     c.node->SetLoneCallerPaths(true);
 }
 
