@@ -932,6 +932,17 @@ static void test_group_commit_exec_throws() {
     CHECK(last.done && last.rc == 100);
 }
 
+// The grouping checks below need callers to pile up behind a running batch; on a loaded machine
+// (a sanitizer build beside other jobs) the threads may otherwise run one after another, each
+// call its own batch.  The first batch therefore waits (up to a second) until every thread has
+// entered submit, then a little longer for them to queue.
+static void hold_first_batch(std::atomic<bool>& first, const std::atomic<int>& entered, int T) {
+    if (!first.exchange(false)) return;
+    const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(1);
+    while (entered.load() < T && std::chrono::steady_clock::now() < until) std::this_thread::yield();
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+}
+
 // group_commit.hpp with several lanes (and lanes that carry on to queued batches): at most
 // `lanes` batches execute at once, the batches
 // executing at once hold distinct lane ids, every request completes exactly once with its own
@@ -941,13 +952,16 @@ static void test_group_commit_lanes() {
         int id = 0, rc = -1;
         bool done = false;
     };
+    const int T = 12, per = 20;
     for (int lanes : {1, 2, 3})
     for (int carry : {0, 2}) {
         rsmi::GroupCommit<Req> gc(-7);
         std::atomic<int> running{0}, peak{0}, overlap{0};
         std::atomic<uint32_t> busy{0};
-        std::atomic<int> executed{0};
+        std::atomic<int> executed{0}, entered{0};
+        std::atomic<bool> first{true};
         auto exec = [&](std::vector<Req*>& batch, int lane) {
+            hold_first_batch(first, entered, T);
             const uint32_t bit = 1u << lane;
             if (lane < 0 || lane >= lanes || (busy.fetch_or(bit) & bit)) overlap++;  // lane id in use twice
             const int now = ++running;
@@ -961,13 +975,13 @@ static void test_group_commit_lanes() {
             running--;
             busy.fetch_and(~bit);
         };
-        const int T = 12, per = 20;
         std::vector<Req> reqs(size_t(T * per));
         std::vector<std::thread> th;
         for (int t = 0; t < T; t++)
             th.emplace_back([&, t] {
                 for (int i = t; i < T * per; i += T) {
                     reqs[size_t(i)].id = i;
+                    entered++;
                     gc.submit(reqs[size_t(i)], 256, 0, lanes, exec, carry);
                 }
             });
@@ -997,14 +1011,17 @@ static void test_group_commit_pipelined() {
         bool done = false;
         std::atomic<int> finished{0};
     };
+    const int T = 12, per = 20;
     for (int lanes : {1, 2})
     for (int carry : {1, 3}) {
         rsmi::GroupCommit<Req> gc(-7);
         std::mutex mu;
         std::vector<std::vector<int>> launched(static_cast<size_t>(lanes)), finished(static_cast<size_t>(lanes));
-        std::atomic<int> seq{0}, bad{0}, deep{0};
+        std::atomic<int> seq{0}, bad{0}, deep{0}, entered{0};
+        std::atomic<bool> first{true};
         std::vector<std::atomic<int>> inflight(static_cast<size_t>(lanes));
         auto exec = [&](std::vector<Req*>& batch, int lane) -> std::function<void()> {
+            hold_first_batch(first, entered, T);
             const int b = seq++;
             {
                 std::lock_guard<std::mutex> g(mu);
@@ -1030,13 +1047,13 @@ static void test_group_commit_pipelined() {
                 if (boom) throw std::bad_alloc();  // the wait itself fails: the batch completes with the fail code
             };
         };
-        const int T = 12, per = 20;
         std::vector<Req> reqs(size_t(T * per));
         std::vector<std::thread> th;
         for (int t = 0; t < T; t++)
             th.emplace_back([&, t] {
                 for (int i = t; i < T * per; i += T) {
                     reqs[size_t(i)].id = i;
+                    entered++;
                     gc.submit(reqs[size_t(i)], 6, 0, lanes, exec, carry);
                 }
             });
