@@ -453,11 +453,11 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
         codec();
     }
     if (rc) {
-        // the codec failed: a shard already written is taken back (best effort), so the block is
-        // not left readable from its data shards alone, as a failed encode writes nothing
-        // (node.go:382-386)
-        for (int i = 0; i < early; i++)
-            if (res[i].ok()) (void)nodes_[i].client->Delete(key);
+        // the codec failed: the error is returned (node.go:382-386) and the data shards already
+        // written stay, as the reference leaves the shards of a Put whose write quorum fails
+        // (node.go:389-407).  They hold exactly the bytes a successful Put stores.  Deleting them
+        // instead would destroy the shards of a block stored earlier under the same key (keys are
+        // content ids, so a repeated Put rewrites identical shards).
         return s.ok() ? rsmi_status(rc) : s;
     }
     const auto t1 = PhaseClock::now();

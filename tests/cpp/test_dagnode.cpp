@@ -804,36 +804,52 @@ static void test_concurrent_puts() {
     }
 }
 
-// A Put whose codec call fails writes nothing that outlives it (node.go:382-386 returns before any
-// datanode write): the data shards written while the GPU encoded are taken back.  The failure is
-// the coalescer's host-fault test hook (RSMI_ERR_HOST); the next Put succeeds.
+// A Put whose codec call fails returns the error (node.go:382-386).  With shards above the overlap
+// threshold the block-only data shards were written while the GPU encoded; they stay, holding
+// exactly the bytes a successful Put stores (no parity, no padded row), as the reference leaves
+// the shards of a Put whose write quorum fails.  A block stored earlier under the same key (keys
+// are content ids) stays readable through a failed repeat Put.  The failure is the coalescer's
+// host-fault test hook (RSMI_ERR_HOST); the next Put succeeds.
 static void test_put_codec_failure() {
     const int k = 10, m = 4, n = k + m;
     Cluster c(k, m);
     int rc;
     std::mt19937_64 r(404);
+    auto arm = [&](int v) {  // a member the key did not reach keeps its fault armed until disarmed
+        for (int i = 0; i < c.node->Members(); i++) {
+            rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
+            if (v)
+                CHECK(x && rsmi_set_option(x, "inject_host_fault", 1) == RSMI_OK);
+            else if (x)
+                (void)rsmi_set_option(x, "inject_host_fault", 0);
+        }
+    };
     // through the group commit (lone paths off, where the hook fails a batch) and as a lone caller
-    // (the hook fails the direct call); with shards above the overlap threshold the block-only
-    // data shards are written while the GPU encodes, and taken back when the codec call fails
+    // (the hook fails the direct call); mode 0 below the overlap threshold, 1 and 2 above it
     for (const int mode : {0, 1, 2}) {
         const bool lone = mode == 2;
         c.node->SetLoneCallerPaths(lone);
         const Bytes block = rand_bytes(r, mode ? size_t(k) * 65536 + 17 : big());
         const std::string key = "codec-fails-" + std::to_string(mode);
-        for (int i = 0; i < c.node->Members(); i++) {
-            rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
-            CHECK(x && rsmi_set_option(x, "inject_host_fault", 1) == RSMI_OK);
-        }
+        const auto want = oracle_shards(k, m, block);
+        arm(1);
         Status s = c.node->Put(key, block);
         CHECK(!s.ok());
-        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key).empty());
-        for (int i = 0; i < c.node->Members(); i++) {  // a member the key did not reach keeps its fault armed
-            rsmi_ctx* x = shared_context(k, m, c.node->MemberDevice(i), &rc, c.node->MemberReplica(i));
-            if (x) (void)rsmi_set_option(x, "inject_host_fault", 0);
+        for (int j = 0; j < n; j++) {
+            const Bytes got = stored_shard(*c.dn[j], key);
+            CHECK(got.empty() || (j < k - 1 && got == want[j]));  // never parity, never wrong bytes
         }
+        arm(0);
         CHECK_OK(c.node->Put(key, block));
-        const auto want = oracle_shards(k, m, block);
         for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key) == want[j]);
+        // the same block Put again with the codec failing: the stored block survives it
+        arm(1);
+        CHECK(!c.node->Put(key, block).ok());
+        arm(0);
+        for (int j = 0; j < n; j++) CHECK(stored_shard(*c.dn[j], key) == want[j]);
+        Bytes got;
+        CHECK_OK(c.node->Get(key, &got));
+        CHECK(got == block);
     }
     c.node->SetLoneCallerPaths(true);
 }
