@@ -165,6 +165,14 @@ threads_flag)
 group_sweep)
   timeout -k 10 300 ./tools/build/latency --group-sweep > $O/group_sweep.txt 2>&1 || fail group_sweep $O/group_sweep.txt
   cat $O/group_sweep.txt ;;
+kernarg_trace)
+  # the Dag Node bench (GPU codec, RS(10,4) 256 KiB) under a kernel trace with HIP_FORCE_DEV_KERNARG
+  # 0 and 1: which kernels each setting dispatches, and their count and time (tools/kernel_counts.py)
+  for v in 0 1; do
+    rm -rf $O/kt_$v
+    (cd /tmp && HIP_FORCE_DEV_KERNARG=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/kt_$v" -o t -- "$R/tools/build/bench_dagnode" 10 4 262144 512 > "$R/$O/kt_$v.log" 2>&1) || fail "kernarg trace $v" $O/kt_$v.log
+  done
+  python3 tools/kernel_counts.py $O/kt_0/t_kernel_trace.csv $O/kt_1/t_kernel_trace.csv | tee $O/kernarg_trace.txt ;;
 threads_traced)
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/$O/trace" -o t -- "$R/tools/build/latency" --threads > "$R/$O/threads_traced.txt" 2>&1) || fail "traced threads" $O/threads_traced.txt
   tail -5 $O/threads_traced.txt ;;
