@@ -315,9 +315,9 @@ class Layout:
 # ---------------------------------------------------------------- CPU legs (rank 0 only)
 def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds, world=1):
     """The oracle's SIMD restatement of the reference CPU path (test infrastructure, used here
-    only as the reported baseline) on host cores, over the same blocks the GPU coded.  Rank 0
-    times it after every rank's GPU legs, at any N (the same run's CPU figure beside each point
-    of the 1..8-GPU curve)."""
+    only as the reported baseline) on host cores, over the same blocks the GPU coded.  Timed at
+    N = 1 only (rank 0, after the GPU legs): the multi-GPU lines carry none, so the scaling runs
+    stay short."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc
 
@@ -358,9 +358,7 @@ def cpu_baseline(k, m, S, B, data_host, lost, data_only, seconds, world=1):
         "cores": threads,
         "kind": "port",
         "sample": f"{reps} passes x the bench's own {nb} blocks of {B // 1024} KiB RS({k},{m}) {what}, "
-                  f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s"
-                  + (f"; rank 0 of {world}, timed after every rank's GPU legs finished, the other ranks idle at a "
-                     "barrier" if world > 1 else ""),
+                  f"oracle/rs_cpu_fast.c {L.rs_cpu_isa().decode()}, {threads} threads, {el:.1f} s",
         "single_core_value": round(reps1 * nb * B / el1 / 2**30, 3),
         "host_cpus": os.cpu_count(),
         "ranks": world,
@@ -536,7 +534,8 @@ def run_mock(a, world, rank):
     el = max_over_ranks(time.perf_counter() - t0, world)
     per = gather({"rank": rank, "blocks": count}, world)
     if rank == 0:
-        cpu = cpu_baseline(k, m, S, k * S, data, [], True, min(a.cpu_seconds, 0.2), world) if a.cpu_seconds > 0 else None
+        cpu = (cpu_baseline(k, m, S, k * S, data, [], True, min(a.cpu_seconds, 0.2), world)
+               if a.cpu_seconds > 0 and world == 1 else None)
         emit(json.dumps({"metric": "mock", "mock": True, "value": round(nb * world * k * S * a.steps / el / 2**30, 4),
                           "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(el * 1e3 / a.steps, 4), "higher_is_better": True, "scaling": "weak",
@@ -745,10 +744,9 @@ def main():
                      else [int(x) for x in a.group.split(",")])
         out["copy_inclusive"] = copy_inclusive(codec, k, m, S, min(nb, max(1, (1 << 30) // B)), lost, data_only,
                                                world, group)
-    if rank == 0 and a.cpu_seconds > 0:
-        # every rank's GPU legs are done (gather above), so the host cores are free; at N > 1 the
-        # other ranks wait idle at finish()'s barrier (their processes stay alive, sleeping) while
-        # rank 0 times the CPU codec on its own share of the job's blocks
+    if rank == 0 and a.cpu_seconds > 0 and world == 1:
+        # the GPU legs are done, so the host cores are free (N = 1 only: the multi-GPU lines carry
+        # no CPU figure)
         data_host = lay.rows(buf, 0, k).cpu().numpy()  # the bench's own blocks
         out["cpu_baseline"] = cpu_baseline(k, m, S, B, data_host, lost, data_only, a.cpu_seconds, world)
     if rank == 0:

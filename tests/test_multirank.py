@@ -82,8 +82,7 @@ def test_bench_spawns_ranks_itself_mock(n):
     assert j["n_gpus"] == n and j["mock"] and j["steps"] == 3
     assert sorted(r["rank"] for r in j["config"]["ranks"]) == list(range(n))
     assert sum(r["blocks"] for r in j["config"]["ranks"]) == 8 * n
-    cb = j["cpu_baseline"]  # rank 0 times the CPU codec at every N, after the ranks' legs
-    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["ranks"] == n and cb["kind"] == "port"
+    assert j["cpu_baseline"] is None  # timed at N = 1 only
 
 
 def test_bench_rejects_world_size_mismatch():
@@ -149,8 +148,7 @@ def test_bench_two_ranks_torchrun_on_one_gpu():
     assert j["n_gpus"] == 2 and j["steps"] == 5 and j["scaling"] == "weak"
     payload = 2 * 256 * 262144 * 5
     assert abs(j["value"] - payload / (j["ms_per_step"] * 5e-3) / 2**30) / j["value"] < 0.01
-    cb = j["cpu_baseline"]  # rank 0 times the CPU codec at N = 2 as well, after both ranks' legs
-    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["ranks"] == 2 and "rank 0 of 2" in cb["sample"]
+    assert j["cpu_baseline"] is None  # timed at N = 1 only
 
 
 @pytest.mark.gpu
