@@ -126,6 +126,9 @@ __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
 // when the caller caps the grid (option waves_per_cu).
 // TB: the blocks lie where a table of block bases says (BlockBases: a coalesced group of callers'
 // own page-locked buffers, one launch for the group); in / out are offsets from each base.
+#ifndef RSMI_ROWS_FIRST  // 1: the coding table staged after the first rows are issued (A/B)
+#define RSMI_ROWS_FIRST 0
+#endif
 template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false, bool TB = false>
 __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
@@ -139,6 +142,23 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     constexpr int NSL = (NSH + 3) / 4;     // CRC: rows each lane keeps (r = q mod 4)
     __shared__ u32x4 s_tbl[K * kColDwords / 4];
     __shared__ uint32_t s_crc[CRC ? kCrcQWords : 1];
+#if RSMI_ROWS_FIRST
+    // the coding table is loaded into registers here and written to LDS (stage, one barrier) once
+    // the wave's first rows are in flight, so a wave's first HBM loads do not wait for the table's
+    // round trip and the barrier
+    LdsTable<K * kColDwords> lt;
+    lt.load(plan->tbl);
+    if constexpr (CRC)
+        for (int i = threadIdx.x; i < kCrcQWords; i += kWG) s_crc[i] = crc_tbl[kCrcQOff + i];
+    __builtin_amdgcn_sched_barrier(0);
+    bool staged = false;  // wave-uniform: every wave passes the staging barrier exactly once
+    auto stage = [&]() {
+        if (staged) return;
+        lt.store(reinterpret_cast<uint32_t*>(s_tbl));
+        __syncthreads();
+        staged = true;
+    };
+#else
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
@@ -147,6 +167,8 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             for (int i = threadIdx.x; i < kCrcQWords; i += kWG) s_crc[i] = crc_tbl[kCrcQOff + i];
     }
     __syncthreads();
+    auto stage = [] {};
+#endif
 
     constexpr uint32_t kWavesPerWG = kWG / kWave;
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -169,7 +191,10 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             return;
         }
     } else {
-        if (t >= ntiles) return;
+        if (t >= ntiles) {
+            stage();  // the workgroup's other waves may have tiles: their barrier needs this one
+            return;
+        }
     }
 
     constexpr int P = rows_in_flight<K, MT>();
@@ -295,6 +320,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
         u32x4 v[P];
 #pragma unroll
         for (int c = 0; c < P; c++) v[c] = load_col(c);
+        stage();  // RSMI_ROWS_FIRST: the table to LDS while the first tile's rows are in flight
 
         // acc ^= p1^p2^p3 per column, folded two columns at a time with 3-input XORs:
         // even columns leave p3 pending, odd columns retire it (1.5 VALU per column).
@@ -420,6 +446,7 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
             blk++;
         }
     }
+    stage();  // a table launch's waves past the last tile (no-op once staged)
     launch_done<TB>(bases);
 }
 
