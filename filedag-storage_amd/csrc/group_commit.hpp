@@ -23,6 +23,14 @@
 // executor that leaves callers queued while a lane is free (a batch capped at `cap`) wakes the
 // first of them too, so two lanes released together cannot leave a free lane idle.
 //
+// Idle work (rsmi_set_wait_hook): a caller may hand submit a host task of its own to run while
+// its request is coded.  A caller that waits for another thread's batch runs it before it first
+// sleeps (it then checks the queue again, so a lane freed meanwhile is not lost: a released lane
+// wakes the first queued caller that is not inside its task).  An executor whose batch is its own
+// request alone runs it once the batch is launched, before the batch's wait; an executor coding
+// other callers' requests runs it after they are completed, so none of them waits for it.  Either
+// way it runs exactly once, before submit returns.
+//
 // Pipelined batches: exec may return a finisher (a callable; empty or exec returning void: the
 // batch ran to completion) instead of waiting for its own work.  The executor then launches the
 // next queued batch (within `carry`) behind it before it calls the finisher, so the device is
@@ -52,8 +60,10 @@ public:
     static constexpr int kMaxLanes = 32;
     explicit GroupCommit(int fail_rc) : fail_rc_(fail_rc) {}
     // carry: batches a lane runs after its own before it hands over (0: hand over at once)
+    // idle (may be null): the caller's own host task, run once on this thread (see above)
     template <class Exec>
-    void submit(Req& req, size_t cap, long wait_us, int lanes, Exec&& exec, int carry = 0) {
+    void submit(Req& req, size_t cap, long wait_us, int lanes, Exec&& exec, int carry = 0,
+                void (*idle)(void*) = nullptr, void* idle_arg = nullptr) {
         calls_++;
         lanes = std::min(std::max(lanes, 1), kMaxLanes);
         cap = std::max<size_t>(cap, 1);
@@ -63,10 +73,27 @@ public:
         pending_.push_back(&me);
         me.queued = true;
         fill_cv_.notify_one();  // an executor waiting out wait_us may now have enough
+        // the idle task, unlocked; returns with lk held
+        auto run_idle = [&]() {
+            void (*fn)(void*) = idle;
+            idle = nullptr;
+            me.in_idle = true;
+            lk.unlock();
+            try {
+                fn(idle_arg);
+            } catch (...) {  // the caller's task: its failure is its own, the batch goes on
+            }
+            lk.lock();
+            me.in_idle = false;
+        };
         while (!req.done) {
             // only a caller whose own request is still queued executes: it is then certain to
             // find work, and a caller whose request is already in a batch just waits for it
             if (!me.queued || executing_ >= lanes) {
+                if (idle) {
+                    run_idle();  // then look again: a lane may have been freed meanwhile
+                    continue;
+                }
                 sleep(me, lk);
                 continue;
             }
@@ -104,7 +131,7 @@ public:
                 pending_.erase(pending_.begin(), pending_.begin() + take);
                 // a batch capped at `cap` leaves callers queued: with a lane free, the first of
                 // them executes the next batch now instead of waiting for this lane
-                if (!pending_.empty() && executing_ < lanes) wake(*pending_.front());
+                if (!pending_.empty() && executing_ < lanes) wake_next();
                 lk.unlock();
                 try {
                     if constexpr (std::is_void_v<std::invoke_result_t<Exec&, std::vector<Req*>&, int>>)
@@ -131,6 +158,8 @@ public:
                 if (flights.size() == 1 && flights.front().fin) start();  // the next, behind it
                 Flight f = std::move(flights.front());
                 flights.pop_front();
+                // a batch of this caller's request alone: its idle task overlaps the batch's work
+                if (idle && f.fin && f.batch.size() == 1 && f.batch[0] == &me) run_idle();
                 if (f.fin) {
                     lk.unlock();
                     finish(f);
@@ -141,8 +170,9 @@ public:
             }
             busy_ &= ~(uint64_t(1) << lane);
             executing_--;
-            if (!pending_.empty()) wake(*pending_.front());  // the next batch's executor
+            if (!pending_.empty()) wake_next();  // the next batch's executor
         }
+        if (idle) run_idle();  // an executor of other callers' requests too: after they returned
     }
     uint64_t calls() const { return calls_.load(); }
     uint64_t batches() const { return batches_.load(); }
@@ -170,7 +200,8 @@ private:
     }
     struct Waiter {
         Req* req = nullptr;
-        bool queued = false;  // in pending_ (under mu_)
+        bool queued = false;   // in pending_ (under mu_)
+        bool in_idle = false;  // running its idle task, not asleep (under mu_)
         std::mutex m;
         std::condition_variable cv;
         bool woken = false;            // under m
@@ -184,6 +215,16 @@ private:
             w.ready.store(true, std::memory_order_release);
         }
         w.cv.notify_one();
+    }
+    // wake the first queued caller that is not inside its idle task (it would take the free lane
+    // only once the task ends), else the first (caller holds mu_, pending_ not empty)
+    void wake_next() {
+        for (Waiter* w : pending_)
+            if (!w->in_idle) {
+                wake(*w);
+                return;
+            }
+        wake(*pending_.front());
     }
     // sleep until woken; mu_ is released meanwhile and held again on return.  With
     // RSMI_GC_SPIN_US > 0 the caller first spins that long on the waiter's flag, so a batch that

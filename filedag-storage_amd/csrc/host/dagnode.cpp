@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
 #include <future>
 #include <map>
 #include <stdexcept>
@@ -25,12 +26,18 @@
 #ifndef RSMI_PUT_OVERLAP
 #define RSMI_PUT_OVERLAP 1
 #endif
-// the smallest shard whose data rows a Put writes while the GPU encodes
-#ifndef RSMI_PUT_OVERLAP_MIN_SHARD
-#define RSMI_PUT_OVERLAP_MIN_SHARD 65536
+// blocks up to this size: the calling thread writes those shards inside its codec call's wait
+// (rsmi_set_wait_hook); larger blocks hand them to the fan-out pool, which writes them in parallel
+#ifndef RSMI_PUT_HOOK_MAX_BLOCK
+#define RSMI_PUT_HOOK_MAX_BLOCK 1048576
 #endif
 #ifndef RSMI_BATCH_CODEC_PLACE
 #define RSMI_BATCH_CODEC_PLACE 0
+#endif
+// 0: no writes inside the codec call's wait (the blocks RSMI_PUT_HOOK_MAX_BLOCK covers write every
+// shard after the call, round 5's order), for A/B library builds
+#ifndef RSMI_PUT_WAIT_HOOK
+#define RSMI_PUT_WAIT_HOOK 1
 #endif
 
 namespace rsmi {
@@ -430,15 +437,20 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
                      ? cl.PutWithChecksums(key, meta, shard, c16, value_checksum(meta, S, c16, raw32[i]))
                      : cl.PutWithChecksum(key, meta, shard, c16);
     };
-    // Large shards: the data rows that hold only block bytes are final once Split, so their
-    // datanode writes run while the GPU encodes the parity (the datanodes checksum them).  The
-    // rest -- the row holding the zero padding, which the engine's group commit rewrites, and the
-    // parity rows -- follow the codec call.  Small shards write every row after the codec call,
-    // with the GPU's checksums: there the second fan-out costs more than the overlap saves
-    // (DESIGN.md §5.3).  Stored entries are the same either way; every outcome is replayed in
-    // node order.
-    const bool overlap = RSMI_PUT_OVERLAP && S >= size_t(RSMI_PUT_OVERLAP_MIN_SHARD);
-    const int early = overlap ? int(std::min<size_t>(size_t(k), block.size() / S)) : 0;
+    // The data rows that hold only block bytes are final once Split, so their datanode writes run
+    // while the GPU encodes the parity (the datanodes checksum them).  The rest -- the row holding
+    // the zero padding, which the engine's group commit rewrites, and the parity rows -- follow the
+    // codec call, with the GPU's checksums.  Blocks up to RSMI_PUT_HOOK_MAX_BLOCK: the calling
+    // thread writes those rows itself inside its codec call's wait -- the engine runs them between
+    // the launch and the wait, or while another caller's batch codes the block
+    // (rsmi_set_wait_hook) -- with no hand-off.  Larger blocks: the fan-out pool writes them in
+    // parallel beside the codec call (one thread's sequential writes would outlast the encode).
+    // Stored entries are the same either way; every outcome is replayed in node order
+    // (DESIGN.md §5.3).
+    const bool pool = RSMI_PUT_OVERLAP && block.size() > size_t(RSMI_PUT_HOOK_MAX_BLOCK);
+    const int full = int(std::min<size_t>(size_t(k), block.size() / S));  // rows of block bytes only
+    const int early = pool ? full : 0;
+    const int hooked = RSMI_PUT_OVERLAP && RSMI_PUT_WAIT_HOOK && !pool ? full : 0;
     if (early > 0 && fan_) {
         fan_->run(2, [&](int t) {
             if (t == 0) {
@@ -449,6 +461,27 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
             fan(early, [&](int i) { put_shard(i, false); }, S);
             phase_add(Phase::Put, tp);
         });
+    } else if (hooked > 0) {
+        struct Writes {
+            std::function<void()> run;
+            std::exception_ptr err;  // nothing may escape into the engine: rethrown below
+            static void call(void* p) {
+                auto* w = static_cast<Writes*>(p);
+                try {
+                    w->run();
+                } catch (...) {
+                    w->err = std::current_exception();
+                }
+            }
+        } writes{[&] {
+            const auto tp = PhaseClock::now();
+            for (int i = 0; i < hooked; i++) put_shard(i, false);
+            phase_add(Phase::Put, tp);
+        }, nullptr};
+        rsmi_set_wait_hook(&Writes::call, &writes);
+        codec();
+        rsmi_run_wait_hook();  // a call that failed before its launch leaves the writes to here
+        if (writes.err) std::rethrow_exception(writes.err);
     } else {
         codec();
     }
@@ -461,7 +494,8 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
         return s.ok() ? rsmi_status(rc) : s;
     }
     const auto t1 = PhaseClock::now();
-    fan(n - early, [&](int t) { put_shard(early + t, true); }, S);  // one goroutine per datanode, no cancel
+    const int first = early + hooked;  // the rows still to write
+    fan(n - first, [&](int t) { put_shard(first + t, true); }, S);  // one goroutine per datanode, no cancel
     phase_add(Phase::Put, t1);
     return quorum();
 }

@@ -400,12 +400,15 @@ std::function<void()> run_coalesced(rsmi_ctx* c, int lane, std::vector<rsmi_ctx:
 // Queue a request and either wait for an executor or become one (group_commit.hpp).  The device
 // check takes no lock once the context is bound, so callers queue while a batch is being coded
 // (under the lock) instead of waiting behind it.
+// The calling thread's wait hook (rsmi_set_wait_hook) goes in as the caller's idle task: run
+// while another thread's batch codes its request, or once its own lone batch is launched.
 int coalesce(rsmi_ctx* c, rsmi_ctx::CoalReq& req) {
     int rc = ensure_device_fast(c);
     if (rc) return rc;
+    const WaitHook h = take_wait_hook();
     c->coal.submit(req, size_t(c->opt_coalesce_max), c->opt_coalesce_us, int(c->opt_coalesce_lanes),
                    [c](std::vector<rsmi_ctx::CoalReq*>& batch, int lane) { return run_coalesced(c, lane, batch); },
-                   int(c->opt_coalesce_carry));
+                   int(c->opt_coalesce_carry), h.fn, h.arg);
     return req.rc;
 }
 

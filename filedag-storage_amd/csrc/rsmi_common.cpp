@@ -9,12 +9,22 @@
 #include "crc16.hpp"
 #include "crc32.hpp"
 #include "host/datanode.hpp"
+#include "wait_hook.hpp"
 
 using namespace rsmi;
 
 namespace {
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+thread_local WaitHook t_wait_hook;  // rsmi_set_wait_hook: this thread's pending hook
 }  // namespace
+
+namespace rsmi {
+WaitHook take_wait_hook() {
+    const WaitHook h = t_wait_hook;
+    t_wait_hook = WaitHook{};
+    return h;
+}
+}  // namespace rsmi
 
 extern "C" {
 
@@ -95,6 +105,15 @@ int rsmi_partition(size_t nblocks, int parts, int i, size_t* start, size_t* coun
     *start = ii * base + std::min(ii, extra);
     *count = base + (ii < extra ? 1 : 0);
     return RSMI_OK;
+}
+
+void rsmi_set_wait_hook(void (*fn)(void*), void* arg) { t_wait_hook = WaitHook{fn, fn ? arg : nullptr}; }
+
+int rsmi_run_wait_hook(void) {
+    const WaitHook h = take_wait_hook();
+    if (!h) return 0;
+    h();
+    return 1;
 }
 
 int rsmi_key_slot(const uint8_t* key, size_t len) {

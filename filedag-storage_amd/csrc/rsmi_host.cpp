@@ -189,6 +189,9 @@ int encode_small(rsmi_ctx* c, const Plan& plan, const uint8_t* data, size_t dbs,
         if (!d32) return RSMI_ERR_DEVICE;
         if ((rc = repitch(d32, raw32_sz, reinterpret_cast<uint8_t*>(cr), raw32_sz, raw32_sz, 1, st))) return rc;
     }
+    // a one-block call (a lone DagNode.Put): the calling thread's wait hook runs while the kernel
+    // codes the block (rsmi_set_wait_hook)
+    if (nblocks == 1) run_pending_wait_hook();
     if (armed) {
         if ((rc = wait_flag(done_flag(c, seq), seq, st, nullptr))) {
             (void)hipStreamSynchronize(st);

@@ -25,6 +25,7 @@
 #include "crc16.hpp"
 #include "crc32.hpp"
 #include "gf256.hpp"
+#include "wait_hook.hpp"
 #include "group_commit.hpp"
 #include "rs_plan.hpp"
 

@@ -83,6 +83,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_encode_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, u8p, c_size, c_size, c_size, c_size, ctypes.c_void_p]),
         "rsmi_reconstruct_batch_dev": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, c_size, u8p, ctypes.c_int, ctypes.c_void_p]),
         "rsmi_encode_block_coalesced": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p]),
+        "rsmi_encode_block_coalesced_crcs": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_void_p,
+                                                            ctypes.c_void_p]),
         "rsmi_reconstruct_coalesced": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, u8p, ctypes.c_int]),
         "rsmi_get_stat": (ctypes.c_long, [ctypes.c_void_p, ctypes.c_char_p]),
         "rsmi_crc16_ibm": (ctypes.c_uint16, [u8p, c_size]),
@@ -132,6 +134,8 @@ def lib() -> ctypes.CDLL:
         "rsmi_group_reconstruct_rows_batch_host": (ctypes.c_int, [ctypes.c_void_p, u8p, c_size, c_size, c_size, u8p,
                                                                 u8p]),
         "rsmi_last_kernel": (ctypes.c_char_p, [ctypes.c_void_p]),
+        "rsmi_set_wait_hook": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+        "rsmi_run_wait_hook": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

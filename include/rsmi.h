@@ -33,8 +33,9 @@ extern "C" {
  * on the host returns RSMI_ERR_HOST instead (new status).
  * 4: coalesced calls run on up to "coalesce_lanes" batches at once (new option, default 2);
  * rsmi_warm is new; the device-resident CRC entry points may run concurrently on different streams
- * of one context; rsmi_last_kernel returns a per-thread copy. */
-#define RSMI_ABI_VERSION 4
+ * of one context; rsmi_last_kernel returns a per-thread copy.
+ * 5: the per-thread wait hook (rsmi_set_wait_hook, rsmi_run_wait_hook). */
+#define RSMI_ABI_VERSION 5
 
 typedef struct rsmi_ctx rsmi_ctx;
 
@@ -189,6 +190,25 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* ctx, uint8_t* shards, size_t S, const u
 /* Counters: "coalesced_calls", "coalesced_batches" (both coalesced entry points).  -1 for an
  * unknown key. */
 long rsmi_get_stat(const rsmi_ctx* ctx, const char* key);
+
+/* A host task for the calling thread to run while its next codec call's device work is in
+ * flight.  DagNode.Put (node.go:376-399) encodes and then writes every shard; the data shards
+ * that hold only block bytes are final once Split, so the host mirror writes them to their
+ * datanodes while the GPU encodes the parity, on the calling thread, without a hand-off.  The
+ * hook is per thread and one-shot: the next rsmi_encode_block_coalesced(_crcs),
+ * rsmi_reconstruct_coalesced or one-block rsmi_encode_batch_host(_crcs) call on this thread
+ * takes it and runs fn(arg) once on this thread -- after its device work is launched and before
+ * it waits for it, or, when the call has no work of its own in flight at that point (a caller whose
+ * block another thread's batch codes), before it blocks.  A call may hold the context's lock while
+ * fn runs, so fn must make no codec call (host-only helpers such as the CRC folds are fine) and
+ * must not throw.  Other entry points, and calls that fail before launching, leave the hook
+ * pending.  fn == NULL clears it. */
+void rsmi_set_wait_hook(void (*fn)(void*), void* arg);
+
+/* Run the calling thread's hook if it is still pending (no call took it) and clear it: 1 if it
+ * ran, 0 if there was none.  Setting a hook, making the call and then calling this runs the
+ * task exactly once whatever path the call took. */
+int rsmi_run_wait_hook(void);
 
 /* ------------------------------------------------------------------ datanode CRC-16 */
 

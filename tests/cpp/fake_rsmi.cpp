@@ -31,6 +31,7 @@
 #include "../../filedag-storage_amd/csrc/crc16.hpp"
 #include "../../filedag-storage_amd/csrc/crc32.hpp"
 #include "../../filedag-storage_amd/csrc/group_commit.hpp"
+#include "../../filedag-storage_amd/csrc/wait_hook.hpp"
 #include "../../include/rsmi.h"
 #include "../../oracle/rs_oracle.h"
 
@@ -201,6 +202,7 @@ int rsmi_encode_batch_host_crcs(rsmi_ctx* c, const uint8_t* data, size_t dbs, ui
         if (c->inject_host_fault.compare_exchange_weak(v, v - 1)) return RSMI_ERR_HOST;
     const size_t k = size_t(c->k), m = size_t(c->m), n = k + m;
     (void)m;
+    if (nblocks == 1) rsmi::run_pending_wait_hook();  // as the product's one-block call, before the coding
     return par_blocks(nblocks, [&](size_t b0, size_t b1) {
         for (size_t b = b0; b < b1; b++) {
             const int rc = encode_one(c, data + b * dbs, parity + b * pbs, S);
@@ -282,7 +284,9 @@ int rsmi_encode_block_coalesced_crcs(rsmi_ctx* c, const uint8_t* block, size_t B
     if (B == 0) return RSMI_ERR_SHORT_DATA;
     if (!block || !shards_out) return RSMI_ERR_INVALID_ARG;
     Req req{true, block, B, shards_out, rsmi_shard_size(B, c->k), nullptr, 0, raw16, raw32, RSMI_OK, false};
-    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); });
+    const rsmi::WaitHook h = rsmi::take_wait_hook();  // the caller's idle task, as the product's
+    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); }, 0, h.fn,
+                   h.arg);
     return req.rc;
 }
 
@@ -302,7 +306,9 @@ int rsmi_reconstruct_coalesced(rsmi_ctx* c, uint8_t* shards, size_t S, const uin
     if (!any) return RSMI_OK;
     if (np < c->k) return RSMI_ERR_TOO_FEW_SHARDS;
     Req req{false, nullptr, 0, shards, S, present, data_only, nullptr, nullptr, RSMI_OK, false};
-    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); });
+    const rsmi::WaitHook h = rsmi::take_wait_hook();
+    c->coal.submit(req, 256, 0, coal_lanes(), [c](std::vector<Req*>& batch, int) { run_batch(c, batch); }, 0, h.fn,
+                   h.arg);
     return req.rc;
 }
 

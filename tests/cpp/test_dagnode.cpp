@@ -804,8 +804,9 @@ static void test_concurrent_puts() {
     }
 }
 
-// A Put whose codec call fails returns the error (node.go:382-386).  With shards above the overlap
-// threshold the block-only data shards were written while the GPU encoded; they stay, holding
+// A Put whose codec call fails returns the error (node.go:382-386).  The block-only data shards
+// were written while the GPU encoded (blocks above 1 MiB by the pool, smaller ones by the calling
+// thread inside the codec call's wait, rsmi_set_wait_hook); they stay, holding
 // exactly the bytes a successful Put stores (no parity, no padded row), as the reference leaves
 // the shards of a Put whose write quorum fails.  A block stored earlier under the same key (keys
 // are content ids) stays readable through a failed repeat Put.  The failure is the coalescer's
@@ -825,11 +826,11 @@ static void test_put_codec_failure() {
         }
     };
     // through the group commit (lone paths off, where the hook fails a batch) and as a lone caller
-    // (the hook fails the direct call); mode 0 below the overlap threshold, 1 and 2 above it
-    for (const int mode : {0, 1, 2}) {
-        const bool lone = mode == 2;
+    // (the hook fails the direct call); modes 0 and 3 written inside the wait, 1 and 2 by the pool
+    for (const int mode : {0, 1, 2, 3}) {
+        const bool lone = mode >= 2;
         c.node->SetLoneCallerPaths(lone);
-        const Bytes block = rand_bytes(r, mode ? size_t(k) * 65536 + 17 : big());
+        const Bytes block = rand_bytes(r, mode == 1 || mode == 2 ? size_t(k) * 131072 + 17 : big());
         const std::string key = "codec-fails-" + std::to_string(mode);
         const auto want = oracle_shards(k, m, block);
         arm(1);
@@ -1090,6 +1091,99 @@ static void test_group_commit_pipelined() {
     }
 }
 
+// group_commit.hpp idle tasks (the engine side of rsmi_set_wait_hook): every caller's task runs
+// exactly once, on the caller's own thread, before its submit returns; a lone caller's task runs
+// while its batch is in flight (after exec launched it, before its finisher); every request still
+// completes with its own result, over 1..3 lanes, with plain and pipelined execs.
+static void test_group_commit_idle() {
+    struct Req {
+        int id = 0, rc = -1;
+        bool done = false;
+    };
+    struct Task {
+        std::atomic<int> runs{0};
+        std::thread::id ran_on;
+        int id = 0;
+        const std::atomic<int>* launched = nullptr;  // per request: 1 once launched, 2 once finished
+        std::atomic<int> saw = {0};                  // the state of the task's own batch when it ran
+    };
+    auto task = [](void* p) {
+        auto* t = static_cast<Task*>(p);
+        t->ran_on = std::this_thread::get_id();
+        if (t->launched) t->saw = t->launched[t->id].load();
+        std::this_thread::sleep_for(std::chrono::microseconds(30));
+        t->runs++;
+    };
+    // one caller: every batch is its own request alone, so the task overlaps the batch
+    {
+        rsmi::GroupCommit<Req> gc(-7);
+        std::vector<std::atomic<int>> state(40);
+        auto exec = [&](std::vector<Req*>& batch, int) -> std::function<void()> {
+            for (Req* r : batch) {
+                r->rc = r->id;
+                state[size_t(r->id)] = 1;
+            }
+            std::vector<Req*> mine = batch;
+            return [&state, mine]() {
+                for (Req* r : mine) state[size_t(r->id)] = 2;
+            };
+        };
+        for (int i = 0; i < 40; i++) {
+            Req r;
+            r.id = i;
+            Task t;
+            t.id = i;
+            t.launched = state.data();
+            gc.submit(r, 8, 0, 2, exec, 1, +task, &t);
+            CHECK(r.done && r.rc == i && t.runs.load() == 1 && t.saw.load() == 1);
+            CHECK(t.ran_on == std::this_thread::get_id());
+        }
+    }
+    const int T = 12, per = 15;
+    for (int lanes : {1, 2, 3})
+    for (int piped : {0, 1}) {
+        rsmi::GroupCommit<Req> gc(-7);
+        std::atomic<int> entered{0};
+        std::atomic<bool> first{true};
+        auto plain = [&](std::vector<Req*>& batch, int) {
+            hold_first_batch(first, entered, T);
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+            for (Req* r : batch) r->rc = r->id;
+        };
+        auto pipe = [&](std::vector<Req*>& batch, int) -> std::function<void()> {
+            hold_first_batch(first, entered, T);
+            for (Req* r : batch) r->rc = r->id;
+            return [] { std::this_thread::sleep_for(std::chrono::microseconds(100)); };
+        };
+        std::vector<Req> reqs(size_t(T * per));
+        std::vector<Task> tasks(size_t(T * per));
+        std::vector<std::thread> th;
+        std::atomic<int> wrong_thread{0}, early{0};
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                for (int i = t; i < T * per; i += T) {
+                    reqs[size_t(i)].id = i;
+                    entered++;
+                    if (piped)
+                        gc.submit(reqs[size_t(i)], 6, 0, lanes, pipe, 1, +task, &tasks[size_t(i)]);
+                    else
+                        gc.submit(reqs[size_t(i)], 6, 0, lanes, plain, 1, +task, &tasks[size_t(i)]);
+                    if (tasks[size_t(i)].runs.load() != 1) early++;  // ran before submit returned
+                    if (tasks[size_t(i)].ran_on != std::this_thread::get_id()) wrong_thread++;
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int i = 0; i < T * per; i++) {
+            CHECK(reqs[size_t(i)].done && reqs[size_t(i)].rc == i);
+            CHECK(tasks[size_t(i)].runs.load() == 1);
+        }
+        CHECK(early.load() == 0 && wrong_thread.load() == 0);
+        CHECK(gc.calls() == uint64_t(T * per) && gc.batches() < gc.calls());
+        std::printf("group commit with idle tasks, %d lane(s), %s: %llu calls in %llu batches\n", lanes,
+                    piped ? "pipelined" : "plain", (unsigned long long)gc.calls(), (unsigned long long)gc.batches());
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     if (rs_oracle_selftest() != 0) {
@@ -1107,6 +1201,7 @@ int main(int argc, char** argv) {
 #endif
     test_group_commit_lanes();
     test_group_commit_pipelined();
+    test_group_commit_idle();
     if (mode == "sanitize") {  // the Dag Node suite at 1/32 scale on the fake device layer
         g_big /= 32;
         g_leaf = g_leaf / 32 + 14;

@@ -39,11 +39,12 @@ def test_library_exports_every_declared_symbol():
 def test_python_binding_covers_header():
     L = rsmi.lib()
     for s in declared_symbols():
-        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free", "rsmi_group_close", "rsmi_group_host_free"), s
+        assert getattr(L, s).restype is not None or s in ("rsmi_close", "rsmi_host_free", "rsmi_group_close", "rsmi_group_host_free",
+                                                          "rsmi_set_wait_hook"), s
 
 
 def test_abi_version_and_status_strings():
-    assert rsmi.lib().rsmi_abi_version() == 4
+    assert rsmi.lib().rsmi_abi_version() == 5
     for code in (0, 1, 2, 3, 4, 5, 6, 7, 8, 100, 101, 102):
         assert rsmi.status_string(code) not in ("", "unknown status")
 
@@ -215,3 +216,32 @@ def test_small_call_option_validates():
         assert L.rsmi_set_option(c._h, b"small_call_bytes", 0) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"small_call_bytes", 1 << 30) == rsmi.OK
         assert L.rsmi_set_option(c._h, b"small_call_bytes", -1) == rsmi.ErrInvalidArg
+
+
+def test_wait_hook_is_per_thread_and_one_shot():
+    """rsmi_set_wait_hook / rsmi_run_wait_hook without a device: a pending hook runs once through
+    rsmi_run_wait_hook, NULL clears it, a call that fails before launching (no GPU here) leaves it
+    pending, and another thread does not see this thread's hook."""
+    import threading
+
+    L = rsmi.lib()
+    ran = []
+    cb = ctypes.CFUNCTYPE(None, ctypes.c_void_p)(lambda arg: ran.append(arg))
+    assert L.rsmi_run_wait_hook() == 0
+    L.rsmi_set_wait_hook(cb, 7)
+    assert L.rsmi_run_wait_hook() == 1 and ran == [7]
+    assert L.rsmi_run_wait_hook() == 0 and ran == [7]
+    L.rsmi_set_wait_hook(cb, 8)
+    L.rsmi_set_wait_hook(None, None)
+    assert L.rsmi_run_wait_hook() == 0 and ran == [7]
+    L.rsmi_set_wait_hook(cb, 9)
+    other = []
+    t = threading.Thread(target=lambda: other.append(L.rsmi_run_wait_hook()))
+    t.start()
+    t.join()
+    assert other == [0] and ran == [7]
+    with rsmi.Codec(10, 4) as c:
+        with pytest.raises(rsmi.RsmiError):
+            c.encode_block_coalesced(b"")  # an argument error: nothing launched
+    assert ran == [7]
+    assert L.rsmi_run_wait_hook() == 1 and ran == [7, 9]

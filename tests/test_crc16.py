@@ -382,6 +382,60 @@ def test_coalesced_lone_call_in_place_on_page_locked_buffer(k, m, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["coalesced", "one_block"])
+@pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (10, 4, 4099)])
+def test_wait_hook_runs_once_inside_the_call(path, k, m, B):
+    """rsmi_set_wait_hook (DagNode.Put's data-shard writes beside the encode, node.go:376-399):
+    the next coalesced encode or one-block host encode on this thread runs the hook exactly once,
+    on this thread, while the kernel codes the block in place; the hook reads the final data rows
+    meanwhile, and shards and R(shard) still equal the oracle's.  A call that fails before
+    launching leaves the hook to rsmi_run_wait_hook."""
+    import threading
+
+    n = k + m
+    S = (B + k - 1) // k
+    L = rsmi.lib()
+    block = bytes(np.random.default_rng(B + 7 * k).integers(0, 256, size=B, dtype=np.uint8))
+    want = orc.split(k, m, block)
+    want[k:] = orc.encode(k, m, want[:k])
+    p = L.rsmi_host_alloc(n * S)
+    assert p
+    try:
+        out = np.ctypeslib.as_array((ctypes.c_uint8 * (n * S)).from_address(p))
+        seen = []
+        me = threading.get_ident()
+
+        def hook(arg):
+            seen.append((threading.get_ident(), bytes(out[: (B // S) * S])))
+
+        cb = ctypes.CFUNCTYPE(None, ctypes.c_void_p)(hook)
+        raw = (ctypes.c_uint32 * n)()
+        with rsmi.Codec(k, m) as c:
+            for rep in range(3):
+                out[:] = 0xA5
+                out[:B] = np.frombuffer(block, dtype=np.uint8)  # Split's copy, by the caller
+                L.rsmi_set_wait_hook(cb, None)
+                if path == "coalesced":
+                    rc = L.rsmi_encode_block_coalesced_crcs(c._h, p, B, p, raw, None)
+                else:
+                    out[B:k * S] = 0
+                    rc = L.rsmi_encode_batch_host_crcs(c._h, p, n * S, p + k * S, n * S, S, 1, raw, None)
+                assert rc == 0
+                assert L.rsmi_run_wait_hook() == 0  # the call took it
+                assert len(seen) == rep + 1 and seen[-1][0] == me
+                assert seen[-1][1] == bytes(want[: B // S].reshape(-1))  # the data rows were final
+                assert np.array_equal(out.reshape(n, S), want)
+                for r in range(n):
+                    assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(want[r].tobytes())
+            L.rsmi_set_wait_hook(cb, None)
+            assert L.rsmi_encode_block_coalesced_crcs(c._h, p, 0, p, raw, None) == rsmi.ErrShortData
+            assert len(seen) == 3
+            assert L.rsmi_run_wait_hook() == 1 and len(seen) == 4
+    finally:
+        L.rsmi_host_free(p)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (4, 2, 4099), (16, 4, 4194304)])
 def test_coalesced_encode_split_by_caller_pageable(k, m, B):
     """rsmi_encode_block_coalesced with block == shards_out on pageable memory (the staging path
