@@ -39,6 +39,11 @@
 #ifndef RSMI_PUT_WAIT_HOOK
 #define RSMI_PUT_WAIT_HOOK 1
 #endif
+// 1 (default): a lone degraded Get copies the block's present data rows inside its decode call's
+// wait (rsmi_set_wait_hook); 0: the whole block from the staging after the call (A/B builds)
+#ifndef RSMI_GET_WAIT_HOOK
+#define RSMI_GET_WAIT_HOOK 1
+#endif
 
 namespace rsmi {
 namespace host {
@@ -76,6 +81,33 @@ private:
     bool decided_ = false;
     Status result_;
 };
+
+// task() on this thread inside the next codec call's wait (rsmi_set_wait_hook), or right after the
+// call when the call did not take it, so it runs exactly once; an exception from task() is rethrown
+// once the call has returned (none may cross the C-ABI), and one from call() leaves no hook behind
+template <class Call>
+int with_wait_task(const std::function<void()>& task, Call&& call) {
+    struct Task {
+        const std::function<void()>* fn;
+        std::exception_ptr err;
+        static void run(void* p) {
+            auto* t = static_cast<Task*>(p);
+            try {
+                (*t->fn)();
+            } catch (...) {
+                t->err = std::current_exception();
+            }
+        }
+    } t{&task, nullptr};
+    struct Clear {
+        ~Clear() { rsmi_set_wait_hook(nullptr, nullptr); }
+    } clear;
+    rsmi_set_wait_hook(&Task::run, &t);
+    const int rc = call();
+    rsmi_run_wait_hook();
+    if (t.err) std::rethrow_exception(t.err);
+    return rc;
+}
 
 }  // namespace
 
@@ -462,26 +494,16 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
             phase_add(Phase::Put, tp);
         });
     } else if (hooked > 0) {
-        struct Writes {
-            std::function<void()> run;
-            std::exception_ptr err;  // nothing may escape into the engine: rethrown below
-            static void call(void* p) {
-                auto* w = static_cast<Writes*>(p);
-                try {
-                    w->run();
-                } catch (...) {
-                    w->err = std::current_exception();
-                }
-            }
-        } writes{[&] {
-            const auto tp = PhaseClock::now();
-            for (int i = 0; i < hooked; i++) put_shard(i, false);
-            phase_add(Phase::Put, tp);
-        }, nullptr};
-        rsmi_set_wait_hook(&Writes::call, &writes);
-        codec();
-        rsmi_run_wait_hook();  // a call that failed before its launch leaves the writes to here
-        if (writes.err) std::rethrow_exception(writes.err);
+        with_wait_task(
+            [&] {
+                const auto tp = PhaseClock::now();
+                for (int i = 0; i < hooked; i++) put_shard(i, false);
+                phase_add(Phase::Put, tp);
+            },
+            [&] {
+                codec();
+                return rc;
+            });
     } else {
         codec();
     }
@@ -819,11 +841,34 @@ Status DagNode::decode_into_block(const std::string& key, Fetched& f, size_t S, 
             else copy_bytes(flat + size_t(i) * S, f.shards[i].data(), S);
             used++;
         }
-    rc = rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), 1);
-    if (rc) return rsmi_status(rc);
+    // the block (the first BlockSize bytes of the k data rows): the present data rows straight from
+    // the fetched shards while the GPU rebuilds the missing ones (rsmi_set_wait_hook; not from the
+    // staging, whose lines the kernel is reading over PCIe), then the rebuilt rows
     const size_t bs = size_t(f.meta.block_size);
-    block->assign(flat, flat + std::min(bs, size_t(k) * S));
-    block->resize(bs);
+    if (RSMI_GET_WAIT_HOOK) {
+        rc = with_wait_task(
+            [&] {
+                // row by row, so only the missing rows' places are zero-filled before they arrive
+                block->clear();
+                block->reserve(bs);
+                for (int i = 0; i < k && block->size() < bs; i++) {
+                    const size_t take = std::min(S, bs - block->size());
+                    if (present[i])
+                        block->insert(block->end(), f.shards[i].begin(), f.shards[i].begin() + long(take));
+                    else
+                        block->resize(block->size() + take);
+                }
+            },
+            [&] { return rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), 1); });
+        if (rc) return rsmi_status(rc);
+        for (int i = 0; i < k && size_t(i) * S < bs; i++)  // the rebuilt rows into their places
+            if (!present[i]) std::memcpy(block->data() + size_t(i) * S, flat + size_t(i) * S, std::min(S, bs - size_t(i) * S));
+    } else {
+        rc = rsmi_reconstruct_batch_host(ctx, flat, size_t(n) * S, S, 1, present.data(), 1);
+        if (rc) return rsmi_status(rc);
+        block->assign(flat, flat + std::min(bs, size_t(k) * S));
+        block->resize(bs);
+    }
     *done = true;
     return Status::Ok();
 }

@@ -404,6 +404,9 @@ int reconstruct_small(rsmi_ctx* c, const Plan& plan, uint8_t* shards, size_t bs,
         return rc;
     const uint32_t *h16, *h32;
     if ((rc = readback(c, d16, d32, raw_sz, st, h16, h32))) return rc;
+    // a one-block call (a lone degraded DagNode.Get): the calling thread's wait hook runs while the
+    // kernel rebuilds the block (rsmi_set_wait_hook)
+    if (nblocks == 1) run_pending_wait_hook();
     if (armed) {
         if ((rc = wait_flag(done_flag(c, seq), seq, st, nullptr))) {
             (void)hipStreamSynchronize(st);

@@ -196,13 +196,16 @@ long rsmi_get_stat(const rsmi_ctx* ctx, const char* key);
  * that hold only block bytes are final once Split, so the host mirror writes them to their
  * datanodes while the GPU encodes the parity, on the calling thread, without a hand-off.  The
  * hook is per thread and one-shot: the next rsmi_encode_block_coalesced(_crcs),
- * rsmi_reconstruct_coalesced or one-block rsmi_encode_batch_host(_crcs) call on this thread
+ * rsmi_reconstruct_coalesced, or one-block host call of rsmi_encode_batch_host(_crcs),
+ * rsmi_reconstruct_batch_host or rsmi_reconstruct_rows_batch_host(_crcs) that runs as one
+ * in-place kernel (page-locked rows, or a small call) on this thread
  * takes it and runs fn(arg) once on this thread -- after its device work is launched and before
  * it waits for it, or, when the call has no work of its own in flight at that point (a caller whose
  * block another thread's batch codes), before it blocks.  A call may hold the context's lock while
  * fn runs, so fn must make no codec call (host-only helpers such as the CRC folds are fine) and
- * must not throw.  Other entry points, and calls that fail before launching, leave the hook
- * pending.  fn == NULL clears it. */
+ * must not throw.  Other entry points, calls that take the copy-engine pipeline and calls that
+ * fail before launching leave the hook pending.  fn == NULL clears it.  A lone DagNode.Get uses it
+ * too: it copies the block's present data rows while the GPU rebuilds the missing ones. */
 void rsmi_set_wait_hook(void (*fn)(void*), void* arg);
 
 /* Run the calling thread's hook if it is still pending (no call took it) and clear it: 1 if it

@@ -228,6 +228,7 @@ int rsmi_reconstruct_rows_batch_host_crcs(rsmi_ctx* c, uint8_t* shards, size_t b
     if (!c || !shards || !present || !required) return RSMI_ERR_INVALID_ARG;
     if (S == 0) return RSMI_ERR_SHARD_NO_DATA;
     const size_t n = size_t(c->n);
+    if (nblocks == 1) rsmi::run_pending_wait_hook();  // as the product's one-block call, before the coding
     return par_blocks(nblocks, [&](size_t b0, size_t b1) {
         for (size_t b = b0; b < b1; b++) {
             const int rc = reconstruct_one(c, shards + b * bs, S, present, required);
