@@ -44,6 +44,12 @@
 #ifndef RSMI_GET_WAIT_HOOK
 #define RSMI_GET_WAIT_HOOK 1
 #endif
+// 1: GetMany assembles its decoded blocks' present data rows from the fetched shards while the GPU
+// rebuilds the missing ones (measured level, profiles/r06/ac; A/B builds); 0 (default): every block
+// from the staging after the decode
+#ifndef RSMI_GETMANY_PRESENT_OVERLAP
+#define RSMI_GETMANY_PRESENT_OVERLAP 0
+#endif
 
 namespace rsmi {
 namespace host {
@@ -1064,6 +1070,31 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                         if (present[c]) std::memcpy(flat + (j * n + c) * S, fs[g.second[b0 + j]].shards[c].data(), S);
                 });
                 phase_add(Phase::Stage, ts);
+                // without verified reads (no key can be refetched), the blocks' present data rows go
+                // in straight from the fetched shards on the key pool while the GPU rebuilds the
+                // missing ones, row by row as in a lone Get (not from the staging, whose lines the
+                // decode is reading over PCIe); the rebuilt rows follow the decode
+                const bool rows_ahead = RSMI_GETMANY_PRESENT_OVERLAP && !verify;
+                std::future<void> pre;
+                if (rows_ahead)
+                    pre = std::async(std::launch::async, [&, b0, nb] {
+                        const auto tp = PhaseClock::now();
+                        fan_keys(int(nb), [&](int j) {
+                            const size_t q = g.second[b0 + size_t(j)];
+                            Bytes& blk = (*blocks)[k0 + q];
+                            const size_t bs = size_t(fs[q].meta.block_size);
+                            blk.clear();
+                            blk.reserve(bs);
+                            for (int c = 0; c < k && blk.size() < bs; c++) {
+                                const size_t take = std::min(S, bs - blk.size());
+                                if (present[c])
+                                    blk.insert(blk.end(), fs[q].shards[c].begin(), fs[q].shards[c].begin() + long(take));
+                                else
+                                    blk.resize(blk.size() + take);
+                            }
+                        });
+                        phase_add(Phase::Stage, tp);
+                    });
                 const auto tc = PhaseClock::now();
                 // with verified reads the same kernel returns R of every survivor it read
                 const int drc = code_members(ord, [&](rsmi_ctx* ctx, size_t j0, size_t cnt) {
@@ -1073,7 +1104,8 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                                   : rsmi_reconstruct_batch_host(ctx, f, size_t(n) * S, S, cnt, present.data(), 1);
                 });
                 phase_add(Phase::Codec, tc);
-                if (drc != RSMI_OK) {  // finish_get reports a device error per key
+                if (pre.valid()) pre.get();
+                if (drc != RSMI_OK) {  // finish_get reports a device error per key (and rewrites the block)
                     unchecked(g.second, b0, nb);
                     continue;  // leave these keys to the per-key path
                 }
@@ -1095,7 +1127,15 @@ void DagNode::GetMany(const std::vector<std::string>& keys, std::vector<Bytes>* 
                     const size_t q = g.second[b0 + j];
                     if (redo_after[q]) return;
                     const uint8_t* base = flat + size_t(j) * n * S;
-                    (*blocks)[k0 + q].assign(base, base + size_t(fs[q].meta.block_size));
+                    const size_t bs = size_t(fs[q].meta.block_size);
+                    if (rows_ahead) {  // the rebuilt rows only
+                        for (int c = 0; c < k && size_t(c) * S < bs; c++)
+                            if (!present[c])
+                                std::memcpy((*blocks)[k0 + q].data() + size_t(c) * S, base + size_t(c) * S,
+                                            std::min(S, bs - size_t(c) * S));
+                    } else {
+                        (*blocks)[k0 + q].assign(base, base + bs);
+                    }
                     fs[q].assembled = true;
                 });
                 phase_add(Phase::Stage, ta);  // the assembly copies count as staging
