@@ -502,6 +502,7 @@ Status DagNode::Put(const std::string& key, const Bytes& block) {  // node.go:35
     } else if (hooked > 0) {
         with_wait_task(
             [&] {
+                // one after another (through the node fan-out instead: level)
                 const auto tp = PhaseClock::now();
                 for (int i = 0; i < hooked; i++) put_shard(i, false);
                 phase_add(Phase::Put, tp);
