@@ -51,6 +51,11 @@
 #ifndef RSMI_GC_SPIN_US
 #define RSMI_GC_SPIN_US 0
 #endif
+// 1: a caller with an idle task runs it before it would execute a batch as well, so the callers
+// queued meanwhile join that batch (A/B builds; 0, the default: only while waiting, see above)
+#ifndef RSMI_GC_IDLE_FIRST
+#define RSMI_GC_IDLE_FIRST 0
+#endif
 
 namespace rsmi {
 
@@ -89,7 +94,7 @@ public:
         while (!req.done) {
             // only a caller whose own request is still queued executes: it is then certain to
             // find work, and a caller whose request is already in a batch just waits for it
-            if (!me.queued || executing_ >= lanes) {
+            if (!me.queued || executing_ >= lanes || (RSMI_GC_IDLE_FIRST && idle)) {
                 if (idle) {
                     run_idle();  // then look again: a lane may have been freed meanwhile
                     continue;
