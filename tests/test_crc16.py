@@ -382,14 +382,16 @@ def test_coalesced_lone_call_in_place_on_page_locked_buffer(k, m, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["coalesced", "one_block"])
+@pytest.mark.parametrize("path", ["coalesced", "one_block", "reconstruct"])
 @pytest.mark.parametrize("k,m,B", [(10, 4, 262144), (2, 1, 262144), (10, 4, 4099)])
 def test_wait_hook_runs_once_inside_the_call(path, k, m, B):
     """rsmi_set_wait_hook (DagNode.Put's data-shard writes beside the encode, node.go:376-399):
     the next coalesced encode or one-block host encode on this thread runs the hook exactly once,
     on this thread, while the kernel codes the block in place; the hook reads the final data rows
     meanwhile, and shards and R(shard) still equal the oracle's.  A call that fails before
-    launching leaves the hook to rsmi_run_wait_hook."""
+    launching leaves the hook to rsmi_run_wait_hook.  "reconstruct": the one-block in-place
+    ReconstructData of a lone degraded DagNode.Get (node.go:277-326), data row 0 lost; the hook
+    reads the survivors while the kernel rebuilds row 0."""
     import threading
 
     n = k + m
@@ -417,16 +419,25 @@ def test_wait_hook_runs_once_inside_the_call(path, k, m, B):
                 L.rsmi_set_wait_hook(cb, None)
                 if path == "coalesced":
                     rc = L.rsmi_encode_block_coalesced_crcs(c._h, p, B, p, raw, None)
-                else:
+                elif path == "one_block":
                     out[B:k * S] = 0
                     rc = L.rsmi_encode_batch_host_crcs(c._h, p, n * S, p + k * S, n * S, S, 1, raw, None)
+                else:
+                    out.reshape(n, S)[:] = want
+                    out[:S] = 0xEE  # data row 0 lost
+                    present = (ctypes.c_uint8 * n)(*[0] + [1] * (n - 1))
+                    rc = L.rsmi_reconstruct_batch_host(c._h, p, n * S, S, 1, present, 1)
                 assert rc == 0
                 assert L.rsmi_run_wait_hook() == 0  # the call took it
                 assert len(seen) == rep + 1 and seen[-1][0] == me
-                assert seen[-1][1] == bytes(want[: B // S].reshape(-1))  # the data rows were final
+                if path == "reconstruct":  # the survivors were as given (row 0 is the kernel's)
+                    assert seen[-1][1][S:] == bytes(want[1: B // S].reshape(-1))
+                else:
+                    assert seen[-1][1] == bytes(want[: B // S].reshape(-1))  # the data rows were final
                 assert np.array_equal(out.reshape(n, S), want)
                 for r in range(n):
-                    assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(want[r].tobytes())
+                    if path != "reconstruct":
+                        assert rsmi.crc16_entry(b"", raw[r], S) == orc.crc16_ibm(want[r].tobytes())
             L.rsmi_set_wait_hook(cb, None)
             assert L.rsmi_encode_block_coalesced_crcs(c._h, p, 0, p, raw, None) == rsmi.ErrShortData
             assert len(seen) == 3
