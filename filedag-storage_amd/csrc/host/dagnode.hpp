@@ -21,7 +21,9 @@
 //   * RepairDataNodeBatched rebuilds only the repaired node's row for many keys at once
 //     with rsmi_reconstruct_rows_batch_host;
 //   * GetMany decodes the blocks that need it in GPU batches (8(f) rank 3);
-//   * MigrateBlocks moves blocks between erasure sets as batched decode + encode (rank 4).
+//   * MigrateBlocks moves blocks between erasure sets as batched decode + encode (rank 4);
+//   * Put writes its block-only data shards, and a lone degraded Get copies its present data rows
+//     into the block, while the codec call is in flight (rsmi_set_wait_hook).
 #pragma once
 #include <array>
 #include <atomic>
