@@ -130,7 +130,7 @@ __device__ __forceinline__ void launch_done(const BasesArg<TB>& bases) {
 #define RSMI_ROWS_FIRST 0
 #endif
 template <int K, int MT, int NT, int WPS = kMinWavesPerSimd, bool UA = false, bool CRC = false, bool TB = false>
-__global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
+__global__ __launch_bounds__(kFastWG, WPS) void rs_fast_kernel(const RsPlanDev* __restrict__ plan,
                                                        const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                        uint64_t in_bs, uint64_t in_rs, uint64_t out_bs,
                                                        uint64_t out_rs, uint32_t S, uint32_t cpb, uint32_t tpb,
@@ -146,10 +146,11 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     // the coding table is loaded into registers here and written to LDS (stage, one barrier) once
     // the wave's first rows are in flight, so a wave's first HBM loads do not wait for the table's
     // round trip and the barrier
+    static_assert(kFastWG == kWG, "LdsTable stages with kWG threads");
     LdsTable<K * kColDwords> lt;
     lt.load(plan->tbl);
     if constexpr (CRC)
-        for (int i = threadIdx.x; i < kCrcQWords; i += kWG) s_crc[i] = crc_tbl[kCrcQOff + i];
+        for (int i = threadIdx.x; i < kCrcQWords; i += kFastWG) s_crc[i] = crc_tbl[kCrcQOff + i];
     __builtin_amdgcn_sched_barrier(0);
     bool staged = false;  // wave-uniform: every wave passes the staging barrier exactly once
     auto stage = [&]() {
@@ -162,15 +163,15 @@ __global__ __launch_bounds__(kWG, WPS) void rs_fast_kernel(const RsPlanDev* __re
     {
         const uint32_t* src = plan->tbl;
         uint32_t* dst = reinterpret_cast<uint32_t*>(s_tbl);
-        for (int i = threadIdx.x; i < K * kColDwords; i += kWG) dst[i] = src[i];
+        for (int i = threadIdx.x; i < K * kColDwords; i += kFastWG) dst[i] = src[i];
         if constexpr (CRC)
-            for (int i = threadIdx.x; i < kCrcQWords; i += kWG) s_crc[i] = crc_tbl[kCrcQOff + i];
+            for (int i = threadIdx.x; i < kCrcQWords; i += kFastWG) s_crc[i] = crc_tbl[kCrcQOff + i];
     }
     __syncthreads();
     auto stage = [] {};
 #endif
 
-    constexpr uint32_t kWavesPerWG = kWG / kWave;
+    constexpr uint32_t kWavesPerWG = kFastWG / kWave;
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t nw = gridDim.x * kWavesPerWG;

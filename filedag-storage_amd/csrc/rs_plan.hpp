@@ -7,6 +7,10 @@ namespace rsmi {
 
 constexpr int kWave = 64;       // CDNA wavefront
 constexpr int kWG = 256;        // threads per workgroup (4 waves)
+#ifndef RSMI_FAST_WG  // threads per workgroup of the coding kernel rs_fast_kernel (A/B builds)
+#define RSMI_FAST_WG 256
+#endif
+constexpr int kFastWG = RSMI_FAST_WG;
 constexpr int kMaxK = 256;      // k + m <= 256 (erasure.go:22)
 constexpr int kMaxMT = 4;       // outputs per launch tile
 constexpr int kColDwords = 20;  // per input column: 5 table fields x 4 outputs

@@ -263,7 +263,7 @@ int launch_plan(rsmi_ctx* c, const Plan& plan, const uint8_t* in, uint64_t in_rs
         if (fn) {
             const uint64_t cpb = (S + 15) / 16;
             const uint64_t tpb = (cpb + uint64_t(kWave) - 1) / uint64_t(kWave);
-            constexpr int wpg = kWG / kWave;
+            constexpr int wpg = kFastWG / kWave;
             // One tile per wave: the hardware dispatcher hands each free slot the next workgroup,
             // which balances the launch across CUs and XCDs of uneven effective bandwidth.  A
             // persistent grid (occupancy x CUs, each wave striding over ~26 tiles) gives every CU
