@@ -181,6 +181,10 @@ public:
     }
     uint64_t calls() const { return calls_.load(); }
     uint64_t batches() const { return batches_.load(); }
+    // wake-ups of sleeping callers and the time from each wake() to the caller running again
+    // (diagnostic: the scheduler's wake-up latency under the group commit)
+    uint64_t wakes() const { return wakes_.load(); }
+    uint64_t wake_ns() const { return wake_ns_.load(); }
 
 private:
     struct Waiter;
@@ -211,12 +215,14 @@ private:
         std::condition_variable cv;
         bool woken = false;            // under m
         std::atomic<bool> ready{false};  // woken, readable without m (the spin before the sleep)
+        std::chrono::steady_clock::time_point woke_at;  // under m: when wake() ran
     };
     // wake a waiting caller (caller holds mu_: lock order mu_, then the waiter's m)
     static void wake(Waiter& w) {
         {
             std::lock_guard<std::mutex> g(w.m);
             w.woken = true;
+            w.woke_at = std::chrono::steady_clock::now();
             w.ready.store(true, std::memory_order_release);
         }
         w.cv.notify_one();
@@ -234,7 +240,7 @@ private:
     // sleep until woken; mu_ is released meanwhile and held again on return.  With
     // RSMI_GC_SPIN_US > 0 the caller first spins that long on the waiter's flag, so a batch that
     // completes within it costs no futex wake-up (A/B builds; default 0: sleep at once)
-    static void sleep(Waiter& w, std::unique_lock<std::mutex>& lk) {
+    void sleep(Waiter& w, std::unique_lock<std::mutex>& lk) {
         std::unique_lock<std::mutex> g(w.m);
         w.woken = false;  // under mu_ and m: no wake-up can fall between the caller's check and here
         w.ready.store(false, std::memory_order_relaxed);
@@ -251,6 +257,9 @@ private:
             g.lock();
         }
         w.cv.wait(g, [&] { return w.woken; });
+        wakes_++;
+        wake_ns_ += uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                  w.woke_at).count());
         g.unlock();
         lk.lock();
     }
@@ -260,7 +269,7 @@ private:
     int executing_ = 0;
     uint64_t busy_ = 0;  // lanes with a batch executing
     const int fail_rc_;
-    std::atomic<uint64_t> calls_{0}, batches_{0};
+    std::atomic<uint64_t> calls_{0}, batches_{0}, wakes_{0}, wake_ns_{0};
 };
 
 }  // namespace rsmi

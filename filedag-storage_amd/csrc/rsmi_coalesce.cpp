@@ -484,6 +484,8 @@ long rsmi_get_stat(const rsmi_ctx* c, const char* key) {
     if (!c || !key) return -1;
     if (!std::strcmp(key, "coalesced_calls")) return long(c->coal.calls());
     if (!std::strcmp(key, "coalesced_batches")) return long(c->coal.batches());
+    if (!std::strcmp(key, "coalesced_wakes")) return long(c->coal.wakes());
+    if (!std::strcmp(key, "coalesced_wake_ns")) return long(c->coal.wake_ns());
     return -1;
 }
 

@@ -187,8 +187,9 @@ int rsmi_encode_block_coalesced_crcs(rsmi_ctx* ctx, const uint8_t* block, size_t
  * with different shard sizes or patterns run as separate groups of the same batch. */
 int rsmi_reconstruct_coalesced(rsmi_ctx* ctx, uint8_t* shards, size_t S, const uint8_t* present, int data_only);
 
-/* Counters: "coalesced_calls", "coalesced_batches" (both coalesced entry points).  -1 for an
- * unknown key. */
+/* Counters: "coalesced_calls", "coalesced_batches" (both coalesced entry points); diagnostic:
+ * "coalesced_wakes", the wake-ups of callers that slept, and "coalesced_wake_ns", the summed time
+ * from each wake-up call to the caller running again.  -1 for an unknown key. */
 long rsmi_get_stat(const rsmi_ctx* ctx, const char* key);
 
 /* A host task for the calling thread to run while its next codec call's device work is in

@@ -135,15 +135,23 @@ int main(int argc, char** argv) {
         for (auto& x : th) x.join();
     };
     if (!std::getenv("BENCH_DAGNODE_NO_WARM")) put_threads();  // diagnostic switch: no untimed pass
+    long w0 = 0, wn0 = 0;
     if (ctx) {
         c0 = node_stat("coalesced_calls");
         b0 = node_stat("coalesced_batches");
+        w0 = node_stat("coalesced_wakes");
+        wn0 = node_stat("coalesced_wake_ns");
     }
     d->SetPhaseTiming(true);
     d->ResetPhases();
     t0 = clk::now();
     put_threads();
     const double putT = secs(t0);
+    if (ctx) {  // the group commit's wake-ups during the timed pass (diagnostic)
+        const long w = node_stat("coalesced_wakes") - w0, wn = node_stat("coalesced_wake_ns") - wn0;
+        std::printf("WAKE put_threads: %ld wake-ups for %d calls, %.1f us from wake-up call to running (mean)\n", w, N,
+                    w ? double(wn) / double(w) / 1e3 : 0.0);
+    }
     phase_json("put_threads", putT);
     d->SetPhaseTiming(false);
     const long calls = ctx ? node_stat("coalesced_calls") - c0 : 0;
